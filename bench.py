@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Benchmark: batched Treasure Game env-steps/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs ENVS_PER_GPU]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one TreasureGame.step() (TG/:91-96) of EVERY env of the batch: the on-device
+synthetic policy writes the actions (uniform over the 9 options, counter hash keyed by the
+global env index), k_step runs each env's option to completion with auto-reset, completed
+episodes are drained on the device and, for N > 1, all-gathered over RCCL.  Per-GPU work is
+fixed (1,048,576 envs per GPU = config C3, C4 at 8 GPUs), so scaling is weak.  Inputs are
+resident in HBM when the timed region starts.
+
+Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (the step kernel's
+algorithmic bytes per launch over its HIP-event-timed duration vs the 8 TB/s HBM peak) and
+``cpu_baseline`` (the C oracle timed on this box's host cores, a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (whole node) at 1M batched envs, 1/2/4/8 MI355X; bit-exact vs CPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ACTION_SEED = 0x5EED0001
+EP_CAP = 4096          # episode records gathered per rank per step (padded)
+# algorithmic bytes of one env-step in k_step:
+#   action 4 + obs 72 + reward 4 + valid 1 + done 1 + state read/write 2 x 40 = 162 per env,
+#   + 24 per random() draw (2 MT words, each: read mt[p], mt[p+397|p-227], write mt[p])
+BYTES_PER_ENV = 162
+BYTES_PER_DRAW = 24
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=1 << 20, help="envs per GPU")
+    ap.add_argument("--policy", default="uniform", choices=["uniform", "masked"])
+    ap.add_argument("--no-autoreset", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target duration of the CPU-baseline sample (0 disables it)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_step.json"),
+                    help="PMC-derived HBM bytes per k_step launch (profiles/), if measured")
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds, policy):
+    """The C oracle (oracle/, the CPU restatement of the reference) on this box's host cores:
+    a bounded sample of the same workload (same seeds, action stream and auto-reset)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # noqa: E402 — bench's cpu_baseline leg only
+    O.build()
+    cores = len(os.sched_getaffinity(0))
+    threads = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    pol = 1 if policy == "masked" else 0
+    steps = 200
+    n = 4096
+    t0 = time.perf_counter()
+    O.run(0, 0, n, steps, ACTION_SEED, pol, True, full=False, nthreads=threads)
+    dt = time.perf_counter() - t0
+    n = max(threads * 64, int(n * seconds / max(dt, 1e-3)))
+    t0 = time.perf_counter()
+    O.run(0, 0, n, steps, ACTION_SEED, pol, True, full=False, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "C oracle (oracle/tg_oracle.c, CPU restatement of the reference step path), "
+                      "envs 0..%d x %d steps, %s policy, auto-reset, %d OpenMP threads, %.1f s"
+                      % (n - 1, steps, policy, threads, dt),
+            "reference_python_1core_measured_in_build_container": 14400.0}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus %d needs torch.distributed.run with %d processes"
+                             % (args.gpus, args.gpus))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    import gym_treasure_game_amd as tg
+    import gym_treasure_game_amd.dist as D
+
+    total = args.envs * world
+    offset, count = D.shard(total, rank, world)
+    autoreset = not args.no_autoreset
+    vec = tg.TreasureGameVec(count, seed=0, global_offset=offset, autoreset=False, device=dev)
+    vec.autoreset = autoreset  # final_obs is not requested: obs/reward/valid/done only
+    vec.reset()
+    ep_rows = torch.empty((EP_CAP, 2), dtype=torch.int64, device=dev)
+    ep_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    if world > 1:
+        all_rows = torch.empty((world * EP_CAP, 2), dtype=torch.int64, device=dev)
+        all_cnt = torch.empty(world, dtype=torch.int32, device=dev)
+    L, h = vec._L, vec.handle
+    obs, rew, val, don = vec._obs, vec._rew, vec._valid, vec._done
+    act = vec._act
+    flags = tg._lib.TG_STEP_AUTORESET if autoreset else 0
+    import ctypes
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    pol = tg._lib.TG_POLICY_MASKED if args.policy == "masked" else tg._lib.TG_POLICY_UNIFORM
+    args_step = (h, p(act), p(obs), p(rew), p(val), p(don), None, flags, stream)
+
+    def one_step(t):
+        tg._lib.check(L.tg_policy_actions(h, ACTION_SEED, t, pol, p(act), stream), "actions")
+        tg._lib.check(L.tg_step(*args_step), "tg_step")
+        tg._lib.check(L.tg_episodes(h, p(ep_rows), p(ep_cnt), EP_CAP, stream), "episodes")
+        if world > 1:  # the one collective: completed episodes over RCCL/xGMI
+            dist.all_gather_into_tensor(all_cnt, ep_cnt)
+            dist.all_gather_into_tensor(all_rows, ep_rows)
+
+    for t in range(args.warmup):
+        one_step(t)
+    torch.cuda.synchronize(dev)
+    vec.stats_reset()
+    vec.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + args.steps):
+        one_step(t)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    st = vec.stats()
+    errs = vec.errors()
+    if world > 1:
+        dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+        dt = float(dt_t.item())
+        tot = torch.tensor([st["steps"], st["ticks"], st["draws"], st["valid_steps"],
+                            st["episodes"]], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        node = dict(zip(["steps", "ticks", "draws", "valid_steps", "episodes"], tot.tolist()))
+    else:
+        node = {k: st[k] for k in ("steps", "ticks", "draws", "valid_steps", "episodes")}
+
+    if rank == 0:
+        env_steps = total * args.steps
+        assert node["steps"] == env_steps, (node, env_steps)
+        launches = max(st["launches"], 1)
+        kern_s = st["kernel_ms"] / 1e3 / launches
+        alg_bytes = (BYTES_PER_ENV * st["steps"] + BYTES_PER_DRAW * st["draws"]) / launches
+        achieved = alg_bytes / kern_s / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            tj = json.load(open(args.traffic_json))
+            if tj.get("envs") == args.envs and tj.get("policy") == args.policy:
+                traffic = tj.get("hbm_bytes_per_launch")
+        line = {
+            "metric": METRIC, "value": env_steps / dt, "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "int32+f64", "data": "synthetic",
+            "config": {"workload": "C3/C4: %d batched treasure_game-v0 envs per GPU, vector obs, "
+                                   "%s random options, auto-reset%s"
+                                   % (args.envs, args.policy,
+                                      " + RCCL episode gather" if world > 1 else ""),
+                       "envs_per_gpu": args.envs, "total_envs": total, "policy": args.policy,
+                       "autoreset": autoreset, "parallelism": "env-shard x%d" % world},
+            "ticks_per_s": node["ticks"] / dt,
+            "valid_step_frac": node["valid_steps"] / max(node["steps"], 1),
+            "draws_per_step": node["draws"] / max(node["steps"], 1),
+            "episodes": node["episodes"], "error_flags": errs,
+            "roofline": {"bound": "hbm", "kernel": "k_step", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "kernel_ms": kern_s * 1e3,
+                         "alg_bytes_per_launch": alg_bytes},
+        }
+        if args.cpu_seconds > 0 and world == 1:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.policy)
+        print(json.dumps(line), flush=True)
+    vec.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

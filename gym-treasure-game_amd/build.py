@@ -1,0 +1,41 @@
+"""Build libtg_amd.so in-tree with hipcc for gfx950.
+
+    python -m gym_treasure_game_amd.build [--force]
+
+The flags matter for parity: -ffp-contract=off keeps uniform()'s a + (b-a)*r and the obs
+divisions IEEE-exact (no FMA contraction), and fast-math is never enabled.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "tg_amd.hip")
+DEPS = [SRC, os.path.join(HERE, "csrc", "tg_core.h"), os.path.join(HERE, "csrc", "tg_level.h"),
+        os.path.join(os.path.dirname(HERE), "include", "tg_amd.h")]
+OUT = os.path.join(HERE, "libtg_amd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+         "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
+
+
+def needs_build():
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(d) > t for d in DEPS)
+
+
+def build(force=False, verbose=False):
+    if not force and not needs_build():
+        return OUT
+    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,618 @@
+// tg_amd.hip — MI355X (gfx950) batched Treasure Game: kernels + the C ABI of include/tg_amd.h.
+//
+// One wavefront lane per env.  Per launch every lane loads its env from struct-of-arrays
+// HBM (16-B + 16-B + 8-B coalesced loads), runs the requested option to completion
+// (_Option.run, OP/:20-36) over the level grid staged in LDS, writes obs / reward / valid /
+// done, and stores the env back.  Auto-reset compacts completed episodes with a wavefront
+// ballot + one atomic per wave.  No MFMA: the path is integer/branch work plus a handful of
+// IEEE f64 ops (obs divisions, uniform/gauss), built with -ffp-contract=off.
+//
+// HBM layout per handle (N envs):
+//   st4[N]  uint4   {pos = px | py<<16 (i16 pair), flags, objs = kx,ky,gx,gy (i8 x4), mt_pos}
+//   ang[N]  double2 {handle0.angle, handle1.angle}
+//   ep[N]   int2    {episode return, episode length}
+//   mt[N][624] u32  env-major MT19937 words (2,496 B per env)
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/tg_amd.h"
+#include "tg_core.h"
+#include "tg_level.h"
+
+using namespace tg;
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+thread_local std::string g_err;
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) return fail(TG_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------
+// SoA pack / unpack
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void unpack(const uint4 s, const double2 a, Env& e) {
+  e.px = (int)(int16_t)(s.x & 0xFFFFu);
+  e.py = (int)(int16_t)(s.x >> 16);
+  e.f = s.y;
+  e.kx = (int)(int8_t)(s.z & 0xFF);
+  e.ky = (int)(int8_t)((s.z >> 8) & 0xFF);
+  e.gx = (int)(int8_t)((s.z >> 16) & 0xFF);
+  e.gy = (int)(int8_t)(s.z >> 24);
+  e.mti = s.w;
+  e.ang0 = a.x;
+  e.ang1 = a.y;
+}
+__device__ __forceinline__ uint4 pack(const Env& e) {
+  uint4 s;
+  s.x = ((uint32_t)e.px & 0xFFFFu) | ((uint32_t)e.py << 16);
+  s.y = e.f;
+  s.z = ((uint32_t)e.kx & 0xFF) | (((uint32_t)e.ky & 0xFF) << 8) | (((uint32_t)e.gx & 0xFF) << 16) |
+        ((uint32_t)e.gy << 24);
+  s.w = e.mti;
+  return s;
+}
+
+struct Soa {
+  uint4* st4;
+  double2* ang;
+  int2* ep;
+  uint32_t* mt;
+};
+
+__device__ __forceinline__ void stage_grid(uint8_t* lds, const uint8_t* grid, int ncell) {
+  for (int i = threadIdx.x; i < ncell; i += BLOCK) lds[i] = grid[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ void store_obs(double* out, int64_t i, const double o[9]) {
+  double* p = out + i * 9;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) p[k] = o[k];
+}
+
+// 64-lane sum (wave64)
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+enum { ST_STEPS, ST_VALID, ST_TICKS, ST_DRAWS, ST_EPISODES, ST_EP_OVERFLOW, ST_COUNT };
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+// random.seed(seed0 + i); TreasureGame() — the constructor builds the game once
+// (_TreasureGameImpl.__init__, IM/:31-53: 4 draws); env.reset() is a separate call
+__global__ __launch_bounds__(BLOCK) void k_create(Soa S, int64_t n, Level L, uint64_t seed0,
+                                                   const uint32_t* __restrict__ genrand) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  uint32_t* mt = S.mt + i * MT_N;
+  seed_mt(mt, genrand, seed0 + (uint64_t)i);
+  Env e{};
+  e.f = 0;
+  Rng rng{mt, 0u, 0u};
+  reset_env(L, e, rng);
+  e.mti = rng.pos;
+  S.st4[i] = pack(e);
+  S.ang[i] = make_double2(e.ang0, e.ang1);
+  S.ep[i] = make_int2(0, 0);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
+                                                  const uint8_t* __restrict__ mask,
+                                                  double* __restrict__ obs) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  Env e;
+  unpack(S.st4[i], S.ang[i], e);
+  if (!mask || mask[i]) {
+    Rng rng{S.mt + i * MT_N, e.mti, 0u};
+    reset_env(L, e, rng);
+    e.mti = rng.pos;
+    S.st4[i] = pack(e);
+    S.ang[i] = make_double2(e.ang0, e.ang1);
+    S.ep[i] = make_int2(0, 0);
+  }
+  if (obs) {
+    double o[9];
+    observe(L, e, o);
+    store_obs(obs, i, o);
+  }
+}
+
+template <bool AUTORESET, bool FINAL>
+__global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
+                                                 const uint8_t* __restrict__ grid,
+                                                 const int32_t* __restrict__ actions,
+                                                 double* __restrict__ obs,
+                                                 int32_t* __restrict__ reward,
+                                                 uint8_t* __restrict__ valid,
+                                                 uint8_t* __restrict__ done_out,
+                                                 double* __restrict__ final_obs,
+                                                 tg_episode* __restrict__ eps, int32_t* eps_count,
+                                                 int32_t eps_cap, int64_t g0,
+                                                 unsigned long long* __restrict__ stats,
+                                                 uint32_t* __restrict__ err_or) {
+  __shared__ uint8_t lgrid[MAX_CELLS];
+  stage_grid(lgrid, grid, L.W * L.H);
+  const Map m{lgrid, L.W, L.H};
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = i < n;
+
+  int ticks = 0, ran = 0, dn = 0;
+  uint32_t draws = 0;
+  Env e;
+  int2 ep = make_int2(0, 0);
+  if (live) {
+    unpack(S.st4[i], S.ang[i], e);
+    ep = S.ep[i];
+    Rng rng{S.mt + i * MT_N, e.mti, 0u};
+    const StepResult r = env_step(L, m, e, actions[i], rng);
+    ticks = r.ticks;
+    ran = r.ran;
+    dn = r.done;
+    double o[9];
+    observe(L, e, o);  // get_state (TG/:94)
+    reward[i] = r.reward;
+    valid[i] = (uint8_t)ran;
+    done_out[i] = (uint8_t)dn;
+    ep.x += r.reward;
+    ep.y += 1;
+    if (FINAL) store_obs(final_obs, i, o);
+    if (AUTORESET && dn) {
+      reset_env(L, e, rng);
+      observe(L, e, o);
+    }
+    store_obs(obs, i, o);
+    e.mti = rng.pos;
+    draws = rng.draws;
+    if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+  }
+  // completed episodes: wavefront ballot + one atomic per wave
+  if (AUTORESET) {
+    const unsigned long long b = __ballot(live && dn);
+    if (b) {
+      const int lane = threadIdx.x & 63;
+      const int cnt = __popcll(b);
+      const int first = __ffsll((long long)b) - 1;
+      int base = 0;
+      if (lane == first) base = atomicAdd(eps_count, cnt);
+      base = __shfl(base, first, 64);
+      if (live && dn) {
+        const int slot = base + __popcll(b & ((1ull << lane) - 1ull));
+        if (slot < eps_cap) {
+          tg_episode r;
+          r.env = g0 + i;
+          r.ret = ep.x;
+          r.len = ep.y;
+          eps[slot] = r;
+        } else {
+          atomicAdd(&stats[ST_EP_OVERFLOW], 1ull);
+        }
+        ep = make_int2(0, 0);
+      }
+    }
+  }
+  if (live) {
+    S.st4[i] = pack(e);
+    S.ang[i] = make_double2(e.ang0, e.ang1);
+    S.ep[i] = ep;
+  }
+  // launch counters for the roofline (one atomic per wave and counter)
+  const int s_steps = wave_sum(live ? 1 : 0), s_valid = wave_sum(ran), s_ticks = wave_sum(ticks),
+            s_draws = wave_sum((int)draws), s_dn = wave_sum(AUTORESET ? dn : 0);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&stats[ST_STEPS], (unsigned long long)s_steps);
+    atomicAdd(&stats[ST_VALID], (unsigned long long)s_valid);
+    atomicAdd(&stats[ST_TICKS], (unsigned long long)s_ticks);
+    atomicAdd(&stats[ST_DRAWS], (unsigned long long)s_draws);
+    if (AUTORESET && s_dn) atomicAdd(&stats[ST_EPISODES], (unsigned long long)s_dn);
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
+                                                 const uint8_t* __restrict__ grid,
+                                                 uint16_t* __restrict__ out) {
+  __shared__ uint8_t lgrid[MAX_CELLS];
+  stage_grid(lgrid, grid, L.W * L.H);
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const Map m{lgrid, L.W, L.H};
+  Env e;
+  unpack(S.st4[i], S.ang[i], e);
+  out[i] = (uint16_t)available_mask(L, m, e);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_observe(Soa S, int64_t n, Level L,
+                                                    double* __restrict__ obs) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  Env e;
+  unpack(S.st4[i], S.ang[i], e);
+  double o[9];
+  observe(L, e, o);
+  store_obs(obs, i, o);
+}
+
+__device__ __forceinline__ uint64_t sm64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// a[t, g] = h(a0, g, t) % 9, or the k-th set bit of available_mask (masked-uniform)
+__global__ __launch_bounds__(BLOCK) void k_actions(Soa S, int64_t n, Level L,
+                                                    const uint8_t* __restrict__ grid,
+                                                    uint64_t a0, int64_t g0, int64_t t,
+                                                    int policy, int32_t* __restrict__ out) {
+  __shared__ uint8_t lgrid[MAX_CELLS];
+  if (policy == TG_POLICY_MASKED) stage_grid(lgrid, grid, L.W * L.H);
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = sm64(sm64(a0 ^ sm64((uint64_t)(g0 + i))) ^ (uint64_t)t);
+  int a = (int)(h % 9ull);
+  if (policy == TG_POLICY_MASKED) {
+    const Map m{lgrid, L.W, L.H};
+    Env e;
+    unpack(S.st4[i], S.ang[i], e);
+    const uint32_t mk = available_mask(L, m, e);
+    const int c = __popc(mk);
+    if (c) {
+      uint32_t k = (uint32_t)(h % (uint64_t)c);
+      uint32_t mm = mk;
+      while (k--) mm &= mm - 1u;
+      a = __ffs(mm) - 1;
+    }
+  }
+  out[i] = a;
+}
+
+// move up to `cap` completed-episode records to `out`, keep the rest queued (device only,
+// so the per-step episode gather never waits on the host)
+__global__ __launch_bounds__(BLOCK) void k_drain_episodes(tg_episode* __restrict__ eps,
+                                                           int32_t* eps_count, int32_t eps_cap,
+                                                           tg_episode* __restrict__ out,
+                                                           int32_t* __restrict__ count,
+                                                           int32_t cap) {
+  int32_t n = *eps_count;
+  if (n > eps_cap) n = eps_cap;
+  const int32_t m = n < cap ? n : cap;
+  for (int32_t k = threadIdx.x; k < m; k += BLOCK) out[k] = eps[k];
+  __syncthreads();
+  for (int32_t base = m; base < n; base += BLOCK) {  // shift the remainder down in chunks
+    const int32_t k = base + threadIdx.x;
+    tg_episode r;
+    if (k < n) r = eps[k];
+    __syncthreads();
+    if (k < n) eps[k - m] = r;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *eps_count = n - m;
+    *count = m;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4, int64_t n,
+                                                   uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t f = i < n ? (st4[i].y & E_MASK) : 0u;
+  if (f) atomicOr(out, f);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// handle
+// ------------------------------------------------------------------------------------------
+struct tg_batch {
+  int device = 0;
+  int64_t n = 0;
+  int64_t g0 = 0;
+  uint64_t seed0 = 0;
+  Level L{};
+  uint8_t* grid = nullptr;
+  uint32_t* genrand = nullptr;
+  Soa S{};
+  tg_episode* eps = nullptr;
+  int32_t* eps_count = nullptr;
+  int32_t eps_cap = 0;
+  unsigned long long* stats = nullptr;  // ST_COUNT
+  uint32_t* err = nullptr;
+  bool timing = false;
+  std::vector<hipEvent_t> ev;  // (start, stop) pairs
+  size_t ev_used = 0;
+  double kernel_ms_done = 0.0;
+};
+
+namespace {
+int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
+
+int bind(const tg_batch* h) {
+  int cur = -1;
+  HIP_TRY(hipGetDevice(&cur));
+  if (cur != h->device) HIP_TRY(hipSetDevice(h->device));
+  return TG_OK;
+}
+#define BIND(h)                       \
+  do {                                \
+    if (!(h)) return fail(TG_E_INVAL, "null handle"); \
+    int rc_ = bind(h);                \
+    if (rc_) return rc_;              \
+  } while (0)
+
+int flush_timing(tg_batch* h) {
+  for (size_t k = 0; k + 1 < h->ev_used; k += 2) {
+    HIP_TRY(hipEventSynchronize(h->ev[k + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]));
+    h->kernel_ms_done += ms;
+  }
+  h->ev_used = 0;
+  return TG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+const char* tg_last_error(void) { return g_err.c_str(); }
+const char* tg_version(void) { return "tg_amd 0.1 gfx950"; }
+int64_t tg_num_envs(const tg_batch* h) { return h ? h->n : 0; }
+
+int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offset, int device,
+              const char* dom, const char* objs, const char* inter) {
+  if (!out || n <= 0 || global_offset < 0) return fail(TG_E_INVAL, "tg_create: bad arguments");
+  *out = nullptr;
+  if (!dom && !objs && !inter) {
+    dom = kDefaultDomain;
+    objs = kDefaultObjects;
+    inter = kDefaultInteractions;
+  } else if (!dom || !objs || !inter) {
+    return fail(TG_E_INVAL, "tg_create: give all three level texts or none");
+  }
+  Level L;
+  std::vector<uint8_t> grid;
+  std::string perr;
+  if (parse_level(dom, objs, inter, L, grid, perr)) return fail(TG_E_INVAL, "%s", perr.c_str());
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return fail(TG_E_NODEV, "tg_create: no HIP device %d (found %d)", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(TG_E_NODEV, "tg_create: device %d is %s, this build targets gfx950", device,
+                prop.gcnArchName);
+
+  tg_batch* h = new tg_batch();
+  h->device = device;
+  h->n = n;
+  h->g0 = global_offset;
+  h->seed0 = seed_base;
+  h->L = L;
+  // completed-episode queue: drained by tg_episodes; records beyond it are counted as dropped
+  const int64_t cap = 4 * n > (1 << 16) ? 4 * n : (1 << 16);
+  h->eps_cap = (int32_t)(cap < (1 << 28) ? cap : (1 << 28));
+  auto cleanup = [&](int code) {
+    tg_destroy(h);
+    return code;
+  };
+  uint32_t gen[MT_N];
+  gen[0] = 19650218u;  // init_genrand(19650218) — the common prefix of init_by_array
+  for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
+#define ALLOC(ptr, bytes)                                                                   \
+  if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess)                                    \
+    return cleanup(fail(TG_E_NOMEM, "hipMalloc %zu B for " #ptr, (size_t)(bytes)));
+  ALLOC(h->grid, grid.size());
+  ALLOC(h->genrand, sizeof gen);
+  ALLOC(h->S.st4, sizeof(uint4) * n);
+  ALLOC(h->S.ang, sizeof(double2) * n);
+  ALLOC(h->S.ep, sizeof(int2) * n);
+  ALLOC(h->S.mt, sizeof(uint32_t) * MT_N * (size_t)n);
+  ALLOC(h->eps, sizeof(tg_episode) * (size_t)h->eps_cap);
+  ALLOC(h->eps_count, sizeof(int32_t));
+  ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT);
+  ALLOC(h->err, sizeof(uint32_t));
+#undef ALLOC
+  if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
+      hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT) != hipSuccess ||
+      hipMemset(h->err, 0, sizeof(uint32_t)) != hipSuccess)
+    return cleanup(fail(TG_E_HIP, "tg_create: upload failed"));
+  hipLaunchKernelGGL(k_create, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, h->L,
+                     seed_base + (uint64_t)global_offset, h->genrand);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) return cleanup(fail(TG_E_HIP, "k_create: %s", hipGetErrorString(e)));
+  *out = h;
+  return TG_OK;
+}
+
+void tg_destroy(tg_batch* h) {
+  if (!h) return;
+  int cur = -1;
+  if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
+  for (auto ev : h->ev) (void)hipEventDestroy(ev);
+  void* bufs[] = {h->grid, h->genrand, h->S.st4, h->S.ang, h->S.ep, h->S.mt,
+                  h->eps,  h->eps_count, h->stats, h->err};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  delete h;
+}
+
+int tg_reset(tg_batch* h, const uint8_t* mask, double* obs, void* stream) {
+  BIND(h);
+  hipLaunchKernelGGL(k_reset, dim3(grid_for(h->n)), dim3(BLOCK), 0, (hipStream_t)stream, h->S,
+                     h->n, h->L, mask, obs);
+  HIP_TRY(hipGetLastError());
+  return TG_OK;
+}
+
+int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, uint8_t* valid,
+            uint8_t* done, double* final_obs, uint32_t flags, void* stream) {
+  BIND(h);
+  if (!actions || !obs || !reward || !valid || !done)
+    return fail(TG_E_INVAL, "tg_step: actions/obs/reward/valid/done are required");
+  hipStream_t st = (hipStream_t)stream;
+  const bool ar = flags & TG_STEP_AUTORESET;
+  const bool fo = final_obs != nullptr;
+  if (h->timing) {
+    while (h->ev.size() < h->ev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      h->ev.push_back(ev);
+    }
+    HIP_TRY(hipEventRecord(h->ev[h->ev_used], st));
+  }
+  auto kern = ar ? (fo ? k_step<true, true> : k_step<true, false>)
+                 : (fo ? k_step<false, true> : k_step<false, false>);
+  hipLaunchKernelGGL(kern, dim3(grid_for(h->n)), dim3(BLOCK), 0, st, h->S, h->n, h->L, h->grid,
+                     actions, obs, reward, valid, done, final_obs, h->eps, h->eps_count,
+                     h->eps_cap, h->g0, h->stats, h->err);
+  HIP_TRY(hipGetLastError());
+  if (h->timing) {
+    HIP_TRY(hipEventRecord(h->ev[h->ev_used + 1], st));
+    h->ev_used += 2;
+    if (h->ev_used >= 4096) return flush_timing(h);
+  }
+  return TG_OK;
+}
+
+int tg_available_mask(tg_batch* h, uint16_t* mask, void* stream) {
+  BIND(h);
+  if (!mask) return fail(TG_E_INVAL, "tg_available_mask: null output");
+  hipLaunchKernelGGL(k_mask, dim3(grid_for(h->n)), dim3(BLOCK), 0, (hipStream_t)stream, h->S,
+                     h->n, h->L, h->grid, mask);
+  HIP_TRY(hipGetLastError());
+  return TG_OK;
+}
+
+int tg_observe(tg_batch* h, double* obs, void* stream) {
+  BIND(h);
+  if (!obs) return fail(TG_E_INVAL, "tg_observe: null output");
+  hipLaunchKernelGGL(k_observe, dim3(grid_for(h->n)), dim3(BLOCK), 0, (hipStream_t)stream, h->S,
+                     h->n, h->L, obs);
+  HIP_TRY(hipGetLastError());
+  return TG_OK;
+}
+
+int tg_policy_actions(tg_batch* h, uint64_t a0, int64_t t, int policy, int32_t* actions,
+                      void* stream) {
+  BIND(h);
+  if (!actions || (policy != TG_POLICY_UNIFORM && policy != TG_POLICY_MASKED))
+    return fail(TG_E_INVAL, "tg_policy_actions: bad arguments");
+  hipLaunchKernelGGL(k_actions, dim3(grid_for(h->n)), dim3(BLOCK), 0, (hipStream_t)stream, h->S,
+                     h->n, h->L, h->grid, a0, h->g0, t, policy, actions);
+  HIP_TRY(hipGetLastError());
+  return TG_OK;
+}
+
+int tg_episodes(tg_batch* h, tg_episode* out, int32_t* count, int32_t cap, void* stream) {
+  BIND(h);
+  if (!out || !count || cap < 0) return fail(TG_E_INVAL, "tg_episodes: bad arguments");
+  hipLaunchKernelGGL(k_drain_episodes, dim3(1), dim3(BLOCK), 0, (hipStream_t)stream, h->eps,
+                     h->eps_count, h->eps_cap, out, count, cap);
+  HIP_TRY(hipGetLastError());
+  return TG_OK;
+}
+
+int tg_errors(tg_batch* h, uint32_t* out, void* stream) {
+  BIND(h);
+  if (!out) return fail(TG_E_INVAL, "tg_errors: null output");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_errors, dim3(grid_for(h->n)), dim3(BLOCK), 0, st, h->S.st4, h->n, h->err);
+  HIP_TRY(hipGetLastError());
+  uint32_t v = 0;
+  HIP_TRY(hipMemcpyAsync(&v, h->err, sizeof v, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *out = v;
+  return TG_OK;
+}
+
+int tg_set_timing(tg_batch* h, int enable) {
+  BIND(h);
+  h->timing = enable != 0;
+  return TG_OK;
+}
+
+int tg_get_stats(tg_batch* h, tg_stats* out) {
+  BIND(h);
+  if (!out) return fail(TG_E_INVAL, "tg_get_stats: null output");
+  HIP_TRY(hipDeviceSynchronize());
+  int rc = flush_timing(h);
+  if (rc) return rc;
+  unsigned long long s[ST_COUNT];
+  HIP_TRY(hipMemcpy(s, h->stats, sizeof s, hipMemcpyDeviceToHost));
+  out->steps = (int64_t)s[ST_STEPS];
+  out->valid_steps = (int64_t)s[ST_VALID];
+  out->ticks = (int64_t)s[ST_TICKS];
+  out->draws = (int64_t)s[ST_DRAWS];
+  out->episodes = (int64_t)s[ST_EPISODES];
+  out->episodes_dropped = (int64_t)s[ST_EP_OVERFLOW];
+  out->launches = out->steps / (h->n ? h->n : 1);
+  out->kernel_ms = h->kernel_ms_done;
+  return TG_OK;
+}
+
+int tg_stats_reset(tg_batch* h) {
+  BIND(h);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT));
+  h->ev_used = 0;
+  h->kernel_ms_done = 0.0;
+  return TG_OK;
+}
+
+int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, double* ang,
+                  uint32_t* mt, uint32_t* mt_pos) {
+  BIND(h);
+  HIP_TRY(hipDeviceSynchronize());
+  const int64_t n = h->n;
+  if (pos || flags || objs || mt_pos) {
+    std::vector<uint4> st((size_t)n);
+    HIP_TRY(hipMemcpy(st.data(), h->S.st4, sizeof(uint4) * n, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; ++i) {
+      const uint4 s = st[(size_t)i];
+      if (pos) {
+        pos[2 * i] = (int16_t)(s.x & 0xFFFFu);
+        pos[2 * i + 1] = (int16_t)(s.x >> 16);
+      }
+      if (flags) flags[i] = s.y;
+      if (objs) {
+        objs[4 * i] = (int8_t)(s.z & 0xFF);
+        objs[4 * i + 1] = (int8_t)((s.z >> 8) & 0xFF);
+        objs[4 * i + 2] = (int8_t)((s.z >> 16) & 0xFF);
+        objs[4 * i + 3] = (int8_t)(s.z >> 24);
+      }
+      if (mt_pos) mt_pos[i] = s.w;
+    }
+  }
+  if (ang) HIP_TRY(hipMemcpy(ang, h->S.ang, sizeof(double2) * n, hipMemcpyDeviceToHost));
+  if (mt) HIP_TRY(hipMemcpy(mt, h->S.mt, sizeof(uint32_t) * MT_N * (size_t)n, hipMemcpyDeviceToHost));
+  return TG_OK;
+}
+
+}  // extern "C"

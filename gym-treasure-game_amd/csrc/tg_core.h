@@ -1,0 +1,623 @@
+// tg_core.h — per-env Treasure Game step physics for the MI355X kernel (gfx950).
+//
+// Everything here is `__host__ __device__` straight-line integer code operating on one env
+// held in registers.  tg_amd.hip wraps it in the batched kernels (one wavefront lane per env,
+// level grid in LDS, struct-of-arrays state in HBM).  The host instantiation exists only so
+// the test harness (tests/native/) can run the exact same code on the build machine, which
+// has no GPU; the product API never executes it on the CPU.
+//
+// Differences in FORM from the reference (not in results — parity is pinned by the oracle):
+//   * collision predicates (IM/:232-288) are evaluated on the 48x48-cell grid with at most 6
+//     cell lookups instead of up to 104 pixel probes: the reference pixel map is constant per
+//     cell (build_map IM/:204-216, door.update_map OB/:246-253) and OOB is WALL (IM/:218-225);
+//   * near_enough (OB/:46-53) is the exact integer test d^2 < r^2 (inputs are integers);
+//   * the trigger cascade (OB/:76-94) is an explicit 8-bit-frame stack in one u64 register;
+//   * MT19937 twists lazily, one word at the point of consumption (see Rng below).
+// Prefixes: TG/ treasure_game.py, IM/ _treasure_game_impl.py, OB/ _objects.py,
+// MO/ _move_options.py, OP/ _option.py under gym_treasure_game/envs/.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TG_HD __host__ __device__ __forceinline__
+
+namespace tg {
+
+constexpr int S = 48;          // xscale == yscale (_scale.py:8-9)
+constexpr int INCR = S / 10;   // x_incr / y_incr (IM/:46-47)
+constexpr int HALFW = S / 4;   // player_width // 2 (IM/:49)
+constexpr int MT_N = 624, MT_M = 397;
+constexpr int MAX_W = 64, MAX_H = 64;
+constexpr int TICK_CAP = 1 << 14;  // the reference has no cap (OP/:28-31); observed max 105
+
+// cell codes in the LDS grid; a door object's cell holds DOORSLOT+i and resolves per env
+enum : int { C_OPEN = 0, C_WALL = 1, C_LADDER = 2, C_DOOR = 3, C_OTHER = 4, C_DOORSLOT = 8 };
+// primitive actions (_actions.py:7-13)
+enum : int { P_NOP = 0, P_UP, P_DOWN, P_LEFT, P_RIGHT, P_JUMP, P_INTERACT };
+// options in create_options order (IM/:495)
+enum : int { O_GO_LEFT = 0, O_GO_RIGHT, O_UP_LADDER, O_DOWN_LADDER, O_INTERACT, O_DOWN_LEFT,
+             O_DOWN_RIGHT, O_JUMP_LEFT, O_JUMP_RIGHT, O_COUNT };
+
+// ---- per-env flag word -------------------------------------------------------------------
+// interactive object i (0..2 doors, 3..4 handles, 5 bolt) keeps its boolean at bit 6+i:
+// door.closed, handle.up, bolt.locked.
+constexpr uint32_t F_JT = 0x1Fu;          // jump_ticker (0..23)
+constexpr uint32_t F_FACING = 1u << 5;    // facing_right (render only)
+constexpr int F_OBJ = 6;                  // first interactive-object bit
+constexpr int F_BAGLEN = 12;              // 3 bits: len(player_bag)
+constexpr int F_BAGITEM = 15;             // 7 bits: item i is gold (1) or key (0)
+constexpr uint32_t E_TICKCAP = 1u << 24;  // option exceeded TICK_CAP
+constexpr uint32_t E_BAG = 1u << 25;      // bag overflow (unreachable in the default level)
+constexpr uint32_t E_ACTION = 1u << 26;   // action outside [-9, 8] (reference: IndexError)
+constexpr uint32_t E_NEARINT = 1u << 27;  // a reset's gauss landed within 1e-9 of an int()
+                                          // boundary (device libm vs glibc watch)
+constexpr uint32_t E_MASK = 0xFF000000u;
+
+// ---- level (kernel argument; the grid itself is staged in LDS) ----------------------------
+struct Level {
+  int32_t W, H;            // cells (IM/:196-197)
+  int32_t start_x, start_y;  // first non-WALL description cell (IM/:173-176)
+  int8_t door_cx[3], door_cy[3];
+  int8_t handle_cx[2], handle_cy[2];
+  int8_t key_cx, key_cy, bolt_cx, bolt_cy, gold_cx, gold_cy;
+  uint32_t init_flags;     // door/handle/bolt initial booleans at their F_OBJ bits
+  uint32_t trig[6][2];     // trigger lists [object][polarity]: count(4b) + 7 x (target 3b, val 1b)
+};
+
+// ---- per-env state (registers) -------------------------------------------------------------
+struct Env {
+  int px, py;            // playerx / playery (IM/:42)
+  uint32_t f;            // flags above
+  int kx, ky, gx, gy;    // key / goldcoin cell (OB/:34-38)
+  double ang0, ang1;     // handle angles (OB/:111-114)
+  uint32_t mti;          // lazy-twist MT position (0..623)
+};
+
+TG_HD int floordiv(int a, int b) {  // Python // for b > 0
+  int q = a / b;
+  return (a % b != 0 && a < 0) ? q - 1 : q;
+}
+
+// ==========================================================================================
+// CPython random, lazily twisted.
+//   CPython (_randommodule.c genrand_uint32) twists all 624 words when index hits 624.  Word
+//   p of the new generation reads mt[p], mt[p+1] (old) and mt[p+397] (old, p < 227) or
+//   mt[p-227] (already new), and mt[0] (new) for p = 623.  Generating word p in place right
+//   before it is consumed therefore produces the identical stream: positions < p are new,
+//   positions >= p old.  A freshly seeded state (CPython index = 624) is position 0.
+//   No 624-iteration loop, hence no wavefront divergence on the twist.
+// ==========================================================================================
+struct Rng {
+  uint32_t* mt;   // this env's 624 words (HBM on device)
+  uint32_t pos;
+  uint32_t draws;  // random() calls (instrumentation for the roofline)
+
+  TG_HD uint32_t next_u32() {
+    const uint32_t p = pos;
+    const uint32_t p1 = (p == MT_N - 1) ? 0u : p + 1;
+    const uint32_t pm = (p < MT_N - MT_M) ? p + MT_M : p - (MT_N - MT_M);
+    const uint32_t a = mt[p], b = mt[p1], c = mt[pm];
+    const uint32_t y0 = (a & 0x80000000u) | (b & 0x7fffffffu);
+    uint32_t y = c ^ (y0 >> 1) ^ ((y0 & 1u) ? 0x9908b0dfu : 0u);
+    mt[p] = y;
+    pos = p1;
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+  // random_random (53-bit): exact in double, FMA-safe
+  TG_HD double random() {
+    const uint32_t a = next_u32() >> 5;
+    const uint32_t b = next_u32() >> 6;
+    ++draws;
+    return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
+  }
+  // Random.uniform = a + (b-a)*random(); built with -ffp-contract=off (no FMA)
+  TG_HD double uniform(double a, double b) { return a + (b - a) * random(); }
+};
+
+// init_by_array([seed lo, seed hi?]) into this env's words; position 0 (see above)
+TG_HD void seed_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed) {
+  const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
+  const uint32_t klen = key1 ? 2u : 1u;
+  // pass 1: k = max(N, klen) = N iterations starting at i = 1 (wraps once onto mt[1])
+  uint32_t prev = genrand19650218[0];
+  uint32_t m0 = prev;
+  uint32_t j = 0;
+  uint32_t i = 1;
+  for (int k = 0; k < MT_N; ++k) {
+    const uint32_t cur = (i == 1 && k == MT_N - 1) ? mt[1] : genrand19650218[i];
+    const uint32_t key = (j == 0) ? key0 : key1;
+    const uint32_t v = (cur ^ ((prev ^ (prev >> 30)) * 1664525u)) + key + j;
+    mt[i] = v;
+    prev = v;
+    ++i;
+    ++j;
+    if (i >= (uint32_t)MT_N) { m0 = mt[MT_N - 1]; prev = m0; i = 1; }
+    if (j >= klen) j = 0;
+  }
+  mt[0] = m0;
+  // pass 2: N-1 iterations
+  for (int k = 0; k < MT_N - 1; ++k) {
+    const uint32_t cur = mt[i];
+    const uint32_t v = (cur ^ ((prev ^ (prev >> 30)) * 1566083941u)) - i;
+    mt[i] = v;
+    prev = v;
+    ++i;
+    if (i >= (uint32_t)MT_N) { mt[0] = mt[MT_N - 1]; prev = mt[0]; i = 1; }
+  }
+  mt[0] = 0x80000000u;
+}
+
+// ==========================================================================================
+// Map probes
+// ==========================================================================================
+struct Map {
+  const uint8_t* g;  // LDS on device
+  int W, H;
+
+  TG_HD int cell(uint32_t f, int cx, int cy) const {  // object_type_at_cell (IM/:227-230)
+    if ((unsigned)cx >= (unsigned)W || (unsigned)cy >= (unsigned)H) return C_WALL;
+    int c = g[cy * W + cx];
+    if (c & C_DOORSLOT) c = ((f >> (F_OBJ + (c & 7))) & 1u) ? C_DOOR : C_OPEN;
+    return c;
+  }
+  TG_HD int at(uint32_t f, int x, int y) const {  // object_type_at (IM/:218-225)
+    if (x < 0 || y < 0 || x >= W * S || y >= H * S) return C_WALL;
+    return cell(f, x / S, y / S);
+  }
+
+  // up_clear (IM/:232-238): xs {px-4, px, px+4} x ys [py-4, py-1] all OPEN
+  TG_HD bool up_clear(const Env& e) const {
+    const int x0 = e.px - INCR, x1 = e.px + INCR, y0 = e.py - INCR, y1 = e.py - 1;
+    if (x0 < 0 || y0 < 0 || x1 >= W * S || y1 >= H * S) return false;
+    const int c0 = x0 / S, c1 = x1 / S, r0 = y0 / S, r1 = y1 / S;
+    return cell(e.f, c0, r0) == C_OPEN && cell(e.f, c1, r0) == C_OPEN &&
+           cell(e.f, c0, r1) == C_OPEN && cell(e.f, c1, r1) == C_OPEN;
+  }
+  // can_go_up (IM/:240-250): ys {py-4, py, py+44} x xs {px-12, px+12}, any LADDER
+  TG_HD bool can_go_up(const Env& e) const {
+    if (e.py <= 1) return false;
+    const int xa = e.px - HALFW, xb = e.px + HALFW;
+    const int ys[3] = {e.py - INCR, e.py, e.py + S - INCR};
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      any |= (int)(at(e.f, xa, ys[j]) == C_LADDER) | (int)(at(e.f, xb, ys[j]) == C_LADDER);
+    return any;
+  }
+  // can_go_down (IM/:252-257): ys [py, py+51] x xs {px-12, px+12}, any LADDER
+  TG_HD bool can_go_down(const Env& e) const {
+    const int y0 = e.py < 0 ? 0 : e.py;
+    const int y1 = (e.py + S + INCR - 1 >= H * S) ? H * S - 1 : e.py + S + INCR - 1;
+    if (y0 > y1) return false;
+    const int r0 = y0 / S, r1 = y1 / S;  // r1 - r0 <= 2
+    bool any = false;
+    const int xs[2] = {e.px - HALFW, e.px + HALFW};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int x = xs[i];
+      if (x < 0 || x >= W * S) continue;
+      const int c = x / S;
+      any |= cell(e.f, c, r0) == C_LADDER;
+      if (r0 + 1 <= r1) any |= cell(e.f, c, r0 + 1) == C_LADDER;
+      if (r0 + 2 <= r1) any |= cell(e.f, c, r0 + 2) == C_LADDER;
+    }
+    return any;
+  }
+  // can_go_left / can_go_right (IM/:259-281): x = px -/+ 16 at ys {py+4, py+44}
+  TG_HD bool can_go_side(const Env& e, int dir) const {
+    const int x = e.px + dir * (HALFW + INCR);
+    const int ta = at(e.f, x, e.py + INCR), tb = at(e.f, x, e.py + S - INCR);
+    return !(ta == C_WALL || ta == C_DOOR || tb == C_WALL || tb == C_DOOR);
+  }
+  // can_fall (IM/:283-288): xs {px-10, px+10} x ys {py, py+50} all OPEN
+  TG_HD bool can_fall(const Env& e) const {
+    const int xa = e.px - HALFW + 2, xb = e.px + HALFW - 2, ya = e.py, yb = e.py + S + 2;
+    return at(e.f, xa, ya) == C_OPEN && at(e.f, xa, yb) == C_OPEN && at(e.f, xb, ya) == C_OPEN &&
+           at(e.f, xb, yb) == C_OPEN;
+  }
+};
+
+// ==========================================================================================
+// Objects, bag, triggers (OB/, IM/:402-445)
+// ==========================================================================================
+// near_enough (OB/:46-53) for the player probe (px, py + 24): centre (cx*48+24, cy*48+24)
+TG_HD bool near_cell(const Env& e, int cx, int cy, int r2) {
+  const int dx = e.px - (cx * S + S / 2);
+  const int dy = e.py - cy * S;
+  return dx * dx + dy * dy < r2;
+}
+constexpr int R2_OBJ = (S / 2) * (S / 2);            // radius xscale/2 (OB/:23)
+constexpr int R2_HANDLE = (S * 3 / 4) * (S * 3 / 4);  // radius xscale*0.75 (OB/:115)
+
+TG_HD int bag_len(uint32_t f) { return (f >> F_BAGLEN) & 7; }
+TG_HD uint32_t bag_items(uint32_t f) { return (f >> F_BAGITEM) & 0x7F; }
+TG_HD bool got_key(uint32_t f) {   // player_got_key (IM/:418-422)
+  const uint32_t live = (1u << bag_len(f)) - 1u;
+  return (~bag_items(f) & live) != 0;
+}
+TG_HD bool got_gold(uint32_t f) {  // player_got_goldcoin (IM/:424-428)
+  const uint32_t live = (1u << bag_len(f)) - 1u;
+  return (bag_items(f) & live) != 0;
+}
+TG_HD void bag_push(uint32_t& f, bool gold) {
+  const int n = bag_len(f);
+  if (n >= 7) { f |= E_BAG; return; }
+  f = (f & ~(7u << F_BAGLEN)) | ((uint32_t)(n + 1) << F_BAGLEN);
+  if (gold) f |= 1u << (F_BAGITEM + n);
+}
+// drop_key (IM/:434-439): remove the first key, move it to (-1,-1)
+TG_HD void drop_key(Env& e) {
+  const int n = bag_len(e.f);
+  const uint32_t items = bag_items(e.f);
+  const uint32_t keys = ~items & ((1u << n) - 1u);
+  if (!keys) return;
+  const int i = __builtin_ctz(keys);
+  const uint32_t lo = items & ((1u << i) - 1u), hi = (items >> (i + 1)) << i;
+  e.f = (e.f & ~((7u << F_BAGLEN) | (0x7Fu << F_BAGITEM))) | ((uint32_t)(n - 1) << F_BAGLEN) |
+        ((lo | hi) << F_BAGITEM);
+  e.kx = -1;
+  e.ky = -1;
+}
+
+// is_object_at (IM/:402-409): handles, closed doors, bolt, gold, key at the cell
+TG_HD bool is_object_at(const Level& L, const Env& e, int xc, int yc) {
+  bool r = (xc == L.handle_cx[0] && yc == L.handle_cy[0]) |
+           (xc == L.handle_cx[1] && yc == L.handle_cy[1]) |
+           (xc == L.bolt_cx && yc == L.bolt_cy) | (xc == e.gx && yc == e.gy) |
+           (xc == e.kx && yc == e.ky);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    r |= (xc == L.door_cx[i] && yc == L.door_cy[i] && ((e.f >> (F_OBJ + i)) & 1u));
+  return r;
+}
+// is_closed_door_at (IM/:411-416)
+TG_HD bool is_closed_door_at(const Level& L, const Env& e, int xc, int yc) {
+  bool r = false;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    r |= (xc == L.door_cx[i] && yc == L.door_cy[i] && ((e.f >> (F_OBJ + i)) & 1u));
+  return r;
+}
+
+// handle.set_angle_wiggle (OB/:127-131)
+TG_HD void wiggle(Env& e, int h, Rng& rng) {
+  const bool up = (e.f >> (F_OBJ + 3 + h)) & 1u;
+  const double a = up ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
+  if (h == 0) e.ang0 = a; else e.ang1 = a;
+}
+// set_val of door (OB/:231-235) / handle (OB/:145-149) / bolt (OB/:175-178): apply only
+TG_HD bool set_val(Env& e, int o, int v, Rng& rng) {
+  const uint32_t bit = 1u << (F_OBJ + o);
+  if ((((e.f & bit) != 0) ? 1 : 0) == v) return false;
+  e.f ^= bit;
+  if (o == 3 || o == 4) wiggle(e, o - 3, rng);
+  return true;
+}
+// set_val(o0, v0) followed by the process_trigger cascade (OB/:76-94), depth-first in file
+// order with the previously_triggered guard; frames are 8 bits of one u64.
+TG_HD void cascade(const Level& L, Env& e, int o0, int v0, Rng& rng) {
+  if (!set_val(e, o0, v0, rng)) return;
+  uint64_t stack = (uint64_t)(o0 | (v0 << 3));
+  uint32_t prev = 1u << o0;
+  int depth = 1;
+  while (depth > 0) {
+    const uint32_t fr = (uint32_t)(stack & 0xFFu);
+    const int o = fr & 7, v = (fr >> 3) & 1, ei = fr >> 4;
+    const uint32_t list = L.trig[o][v];
+    if (ei < (int)(list & 0xFu)) {
+      stack += 0x10u;
+      const uint32_t edge = (list >> (4 + 4 * ei)) & 0xFu;
+      const int t = edge & 7, tv = (edge >> 3) & 1;
+      if (!(prev & (1u << t)) && set_val(e, t, tv, rng)) {
+        stack = (stack << 8) | (uint64_t)(t | (tv << 3));
+        prev |= 1u << t;
+        ++depth;
+      }
+    } else {
+      stack >>= 8;
+      prev &= ~(1u << o);
+      --depth;
+    }
+  }
+}
+// handle.flip (OB/:117-122): uniform(0, 1) <= 0.8 (== random() exactly)
+TG_HD void flip(const Level& L, Env& e, int h, Rng& rng) {
+  if (rng.random() <= 0.8) {
+    const int up = (e.f >> (F_OBJ + 3 + h)) & 1u;
+    cascade(L, e, 3 + h, !up, rng);
+  } else {
+    wiggle(e, h, rng);
+  }
+}
+
+// noisy (IM/:361-366): round() is half-to-even == rint
+TG_HD int noisy(int val, Rng& rng) {
+  const double between = val / 2.0;
+  const double u = (val < between) ? rng.uniform((double)val, between) : rng.uniform(between, (double)val);
+  return (int)rint(u);
+}
+
+// ==========================================================================================
+// Primitive tick: _TreasureGameImpl.step (IM/:290-359). Returns the tick reward.
+// ==========================================================================================
+TG_HD int tick(const Level& L, const Map& m, Env& e, int prim, Rng& rng) {
+  int xd = 0, yd = 0;
+  if (prim == P_UP) {
+    if (m.can_go_up(e)) yd = noisy(-INCR, rng);
+  } else if (prim == P_DOWN) {
+    if (m.can_go_down(e)) yd = noisy(INCR, rng);
+  } else if (prim == P_LEFT) {
+    if (m.can_go_side(e, -1)) { xd = noisy(-INCR, rng); e.f &= ~F_FACING; }
+  } else if (prim == P_RIGHT) {
+    if (m.can_go_side(e, +1)) { xd = noisy(INCR, rng); e.f |= F_FACING; }
+  } else if (prim == P_JUMP) {
+    if (!m.can_go_down(e) && m.up_clear(e)) {
+      const uint32_t jt = (rng.random() > 0.25) ? 23u : 22u;
+      e.f = (e.f & ~F_JT) | jt;
+    }
+  } else if (prim == P_INTERACT) {  // object list order: handles (3,4) before the bolt (6)
+    if (near_cell(e, L.handle_cx[0], L.handle_cy[0], R2_HANDLE)) flip(L, e, 0, rng);
+    if (near_cell(e, L.handle_cx[1], L.handle_cy[1], R2_HANDLE)) flip(L, e, 1, rng);
+    if (near_cell(e, L.bolt_cx, L.bolt_cy, R2_OBJ) && got_key(e.f)) {
+      cascade(L, e, 5, 0, rng);  // try_unlock -> bolt.unlock (IM/:430-432)
+      drop_key(e);
+    }
+  }
+  const uint32_t jt = e.f & F_JT;
+  if (jt > 0) {
+    if (m.up_clear(e)) yd = -INCR;
+    e.f = (e.f & ~F_JT) | (jt - 1);
+  } else if (m.can_fall(e)) {
+    yd = INCR;  // jump_ticker already 0
+  }
+  e.px += xd;
+  if (yd > 0 && m.can_fall(e)) {
+    while (yd > 0) {  // fall pixel by pixel (IM/:341-346)
+      e.py += 1;
+      yd -= 1;
+      if (!m.can_fall(e)) yd = 0;
+    }
+  } else {
+    e.py += yd;
+  }
+  // pickups in object order: key then goldcoin (IM/:350-354)
+  if (near_cell(e, e.kx, e.ky, R2_OBJ)) {
+    e.kx = L.W - 1 - bag_len(e.f);
+    e.ky = L.H - 1;
+    bag_push(e.f, false);
+  }
+  if (near_cell(e, e.gx, e.gy, R2_OBJ)) {
+    e.gx = L.W - 1 - bag_len(e.f);
+    e.gy = L.H - 1;
+    bag_push(e.f, true);
+  }
+  return prim == P_JUMP ? -5 : -1;  // JUMP_REWARD / STEP_REWARD (IM/:15-16)
+}
+
+// ==========================================================================================
+// Options (MO/)
+// ==========================================================================================
+TG_HD void player_cell(const Env& e, int& xc, int& yc) {  // IM/:441-445
+  xc = floordiv(e.px, S);
+  yc = floordiv(e.py + S / 2, S);
+}
+// close_enough_to / close_enough_x: |tx*48 + 24 - px| < 4 (MO/:69-72 and its copies)
+TG_HD bool close_x(const Env& e, int txc) {
+  const int d = txc * S + S / 2 - e.px;
+  return (d < 0 ? -d : d) < INCR;
+}
+// go_left / go_right is_target_cell (MO/:54-67, 126-139)
+TG_HD bool go_is_target(const Level& L, const Map& m, const Env& e, int dir, int xc, int yc) {
+  return m.cell(e.f, xc, yc - 1) == C_LADDER || m.cell(e.f, xc, yc + 1) == C_LADDER ||
+         m.cell(e.f, xc + dir, yc) == C_WALL || is_object_at(L, e, xc, yc) ||
+         is_closed_door_at(L, e, xc + dir, yc) || m.cell(e.f, xc + dir, yc + 1) == C_OPEN;
+}
+// get_target_cell (MO/:43-52; MO/:115-124 whose xc<0 test can never fire going right, and
+// terminates because OOB is WALL)
+TG_HD bool go_target(const Level& L, const Map& m, const Env& e, int dir, int xc, int yc, int& tx) {
+  int x = xc + dir;
+  while (!go_is_target(L, m, e, dir, x, yc)) {
+    x += dir;
+    if (x < 0) return false;
+  }
+  tx = x;
+  return true;
+}
+// jump landing (MO/:281-287)
+TG_HD bool landing(const Map& m, const Env& e, int xc, int yc) {
+  return m.cell(e.f, xc, yc) == C_OPEN && m.cell(e.f, xc, yc + 1) == C_WALL;
+}
+
+TG_HD bool can_run(const Level& L, const Map& m, const Env& e, int k) {
+  int xc, yc;
+  player_cell(e, xc, yc);
+  switch (k) {
+    case O_GO_LEFT:
+    case O_GO_RIGHT: {  // MO/:23-41, 95-113
+      const int dir = k == O_GO_LEFT ? -1 : 1;
+      int tc;
+      if (!go_target(L, m, e, dir, xc, yc, tc)) return false;
+      for (int x = xc; dir < 0 ? x >= tc : x <= tc; x += dir) {
+        if (m.cell(e.f, x, yc) != C_OPEN) return false;
+        if (m.cell(e.f, x, yc + 1) == C_OPEN) return false;
+      }
+      return true;
+    }
+    case O_UP_LADDER: return m.can_go_up(e);      // MO/:165-166
+    case O_DOWN_LADDER: return m.can_go_down(e);  // MO/:181-182
+    case O_INTERACT:                              // MO/:446-455
+      return near_cell(e, L.handle_cx[0], L.handle_cy[0], R2_HANDLE) ||
+             near_cell(e, L.handle_cx[1], L.handle_cy[1], R2_HANDLE) ||
+             (near_cell(e, L.bolt_cx, L.bolt_cy, R2_OBJ) && got_key(e.f));
+    case O_DOWN_LEFT:
+    case O_DOWN_RIGHT: {  // MO/:199-209, 394-404
+      const int dir = k == O_DOWN_LEFT ? -1 : 1;
+      return m.cell(e.f, xc + dir, yc) == C_OPEN && m.cell(e.f, xc + dir, yc + 1) == C_OPEN;
+    }
+    case O_JUMP_LEFT:
+    case O_JUMP_RIGHT: {  // MO/:254-267, 324-337
+      const int dir = k == O_JUMP_LEFT ? -1 : 1;
+      return m.cell(e.f, xc, yc - 1) == C_OPEN && m.cell(e.f, xc + dir, yc - 1) == C_OPEN &&
+             (landing(m, e, xc + dir, yc - 1) || landing(m, e, xc + 2 * dir, yc - 1));
+    }
+  }
+  return false;
+}
+
+TG_HD uint32_t available_mask(const Level& L, const Map& m, const Env& e) {  // TG/:83-89
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < O_COUNT; ++k) r |= (uint32_t)can_run(L, m, e, k) << k;
+  return r;
+}
+
+// option-local state (start_cell / target_cell are None between steps, MO/:80-83 etc.)
+struct Opt {
+  int k;
+  int tx;      // target cell x
+  bool init;   // target computed
+  bool done;
+};
+
+// policy_step of every option (MO/)
+TG_HD int policy(const Level& L, const Map& m, const Env& e, Opt& o) {
+  int xc, yc;
+  switch (o.k) {
+    case O_GO_LEFT:
+    case O_GO_RIGHT: {  // MO/:74-85, 146-157
+      const int dir = o.k == O_GO_LEFT ? -1 : 1;
+      if (!o.init) {
+        player_cell(e, xc, yc);
+        go_target(L, m, e, dir, xc, yc, o.tx);  // exists: can_run checked it
+        o.init = true;
+      }
+      if (close_x(e, o.tx)) o.done = true;
+      return dir < 0 ? P_LEFT : P_RIGHT;
+    }
+    case O_UP_LADDER:  // MO/:168-173
+      if (!m.can_go_up(e)) { o.done = true; return P_NOP; }
+      return P_UP;
+    case O_DOWN_LADDER:  // MO/:184-189
+      if (!m.can_go_down(e)) { o.done = true; return P_NOP; }
+      return P_DOWN;
+    case O_INTERACT:  // MO/:457-460
+      o.done = true;
+      return P_INTERACT;
+    case O_DOWN_LEFT:
+    case O_DOWN_RIGHT: {  // MO/:231-244, 426-439
+      const int dir = o.k == O_DOWN_LEFT ? -1 : 1;
+      if (!o.init) {
+        // get_target_cell (MO/:211-221, 406-416) scans down column xc+dir for the first
+        // non-open cell; only its x is ever used (close_enough_x).  It returns None only if
+        // the scan leaves the grid, after which the reference raises TypeError; the bottom
+        // row of a walled level never lets that happen.
+        player_cell(e, xc, yc);
+        o.tx = xc + dir;
+        o.init = true;
+      }
+      if (close_x(e, o.tx)) {
+        if (!m.can_fall(e)) o.done = true;
+        return P_NOP;
+      }
+      return dir < 0 ? P_LEFT : P_RIGHT;
+    }
+    default: {  // O_JUMP_LEFT / O_JUMP_RIGHT (MO/:297-314, 367-384)
+      const int dir = o.k == O_JUMP_LEFT ? -1 : 1;
+      if (!o.init) {
+        player_cell(e, xc, yc);
+        o.tx = landing(m, e, xc + dir, yc - 1) ? xc + dir : xc + 2 * dir;  // MO/:269-279
+        o.init = true;
+        return P_JUMP;
+      }
+      if (close_x(e, o.tx)) {
+        if (!m.can_fall(e)) o.done = true;
+        return P_NOP;
+      }
+      const bool back = !m.can_fall(e) && !m.can_go_side(e, dir);
+      return (back ? -dir : dir) < 0 ? P_LEFT : P_RIGHT;
+    }
+  }
+}
+
+// ==========================================================================================
+// Observation (IM/:368-378 + OB/:157-158,186-190,202-203,215-216) and done (TG/:95)
+// ==========================================================================================
+TG_HD void observe(const Level& L, const Env& e, double o[9]) {
+  const double w = (double)(L.W * S), h = (double)(L.H * S);
+  o[0] = (double)e.px / w;
+  o[1] = (double)e.py / h;
+  o[2] = e.ang0;
+  o[3] = e.ang1;
+  o[4] = (double)(e.kx * S) / w;
+  o[5] = (double)(e.ky * S) / h;
+  o[6] = ((e.f >> (F_OBJ + 5)) & 1u) ? 1.0 : 0.0;
+  o[7] = (double)(e.gx * S) / w;
+  o[8] = (double)(e.gy * S) / h;
+}
+TG_HD bool is_done(const Env& e) {
+  int xc, yc;
+  player_cell(e, xc, yc);
+  return got_gold(e.f) && yc == 0;
+}
+
+// ==========================================================================================
+// reset_game (IM/:55-73): objects re-read (handle angles, 2 draws), start position (gauss
+// pair, 2 draws), empty bag.  Keeps the error bits.
+// ==========================================================================================
+TG_HD void reset_env(const Level& L, Env& e, Rng& rng) {
+  e.f = (e.f & E_MASK) | L.init_flags | F_FACING;
+  e.ang0 = ((L.init_flags >> (F_OBJ + 3)) & 1u) ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
+  e.ang1 = ((L.init_flags >> (F_OBJ + 4)) & 1u) ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
+  e.kx = L.key_cx;
+  e.ky = L.key_cy;
+  e.gx = L.gold_cx;
+  e.gy = L.gold_cy;
+  // player_initial_position (IM/:168-178) with Random.gauss's pair (gauss_next consumed)
+  const double x2pi = rng.random() * (2.0 * 3.141592653589793);
+  const double g2rad = sqrt(-2.0 * log(1.0 - rng.random()));
+  const double zx = 0.0 + (cos(x2pi) * g2rad) * (S / 24.0);
+  const double zy = fabs(0.0 + (sin(x2pi) * g2rad) * (S / 36.0));
+  const double fx = fabs(zx) - floor(fabs(zx)), fy = zy - floor(zy);
+  if ((fabs(zx) >= 0.5 && (fx < 1e-9 || fx > 1.0 - 1e-9)) || (zy >= 0.5 && (fy < 1e-9 || fy > 1.0 - 1e-9)))
+    e.f |= E_NEARINT;
+  e.px = L.start_x * S + S / 2 + (int)zx;
+  e.py = L.start_y * S + (int)zy;
+}
+
+// ==========================================================================================
+// One env-step: TreasureGame.step (TG/:91-96) -> _Option.run (OP/:20-36)
+// ==========================================================================================
+struct StepResult {
+  int reward;  // sum of tick rewards (0 when the option could not run)
+  int ran;     // 0 == the reference returns reward None
+  int done;    // got gold and back in row 0
+  int ticks;
+};
+TG_HD StepResult env_step(const Level& L, const Map& m, Env& e, int a, Rng& rng) {
+  StepResult r{0, 0, 0, 0};
+  if (a < -O_COUNT || a >= O_COUNT) {
+    e.f |= E_ACTION;  // option_list[a] raises IndexError in the reference (TG/:92)
+  } else {
+    if (a < 0) a += O_COUNT;  // Python negative indexing
+    if (can_run(L, m, e, a)) {
+      r.ran = 1;
+      Opt o{a, 0, false, false};
+      do {
+        const int prim = policy(L, m, e, o);
+        r.reward += tick(L, m, e, prim, rng);
+        if (++r.ticks >= TICK_CAP) {
+          e.f |= E_TICKCAP;
+          break;
+        }
+      } while (!o.done);
+    }
+  }
+  r.done = is_done(e);
+  return r;
+}
+
+}  // namespace tg

@@ -1,0 +1,172 @@
+// tg_level.h — level text (the reference's three file formats) -> tg::Level + LDS grid codes.
+// Host-only C++.  Follows get_file_description / build_map / read_objects /
+// extract_interactives / player_initial_position (IM/:75-202) and door.update_map (OB/:246-253).
+#pragma once
+#include <cctype>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tg_core.h"
+
+namespace tg {
+
+constexpr int MAX_CELLS = 32 * 32;  // LDS grid capacity (default level: 14 x 13)
+
+inline int level_err(std::string& err, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+inline int level_err(std::string& err, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  err = buf;
+  return -1;
+}
+
+inline const char* const kDefaultDomain =
+    "////L/////////\n/          ///\n//////////L///\n/    /////L///\n/            / \n"
+    "/////   //////\n/     /      /\n///L//////////\n/  L         / \n/  L      ////\n"
+    "/  L     /////\n/       //////\n//////////////\n";
+inline const char* const kDefaultObjects =
+    "door 9 1 True\ndoor 9 4 False\ndoor 10 8 True\nhandle 1 1 True\nhandle 12 4 False\n"
+    "key 1 4\nbolt 1 11 True\ngold 12 8\n";
+inline const char* const kDefaultInteractions =
+    "handle 0 True door 0 True\nhandle 0 False door 0 False\nhandle 0 True door 1 False\n"
+    "handle 0 False door 1 True\nhandle 0 True handle 1 False\nhandle 0 False handle 1 True\n"
+    "handle 1 False door 0 True\nhandle 1 True door 0 False\nhandle 1 False door 1 False\n"
+    "handle 1 True door 1 True\nhandle 1 False handle 0 True\nhandle 1 True handle 0 False\n"
+    "bolt 0 True door 2 True\nbolt 0 False door 2 False\n";
+
+inline std::vector<std::string> lines_of(const char* s) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (const char* p = s; *p; ++p) {
+    if (*p == '\n') {
+      out.push_back(cur);
+      cur.clear();
+    } else {
+      cur.push_back(*p);
+    }
+  }
+  if (!cur.empty()) out.push_back(cur);
+  return out;
+}
+inline std::string strip(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && isspace((unsigned char)s[a])) ++a;
+  while (b > a && isspace((unsigned char)s[b - 1])) --b;
+  return s.substr(a, b - a);
+}
+inline std::vector<std::string> words(const std::string& s) {
+  std::vector<std::string> w;
+  std::string cur;
+  for (char c : s) {
+    if (isspace((unsigned char)c)) {
+      if (!cur.empty()) w.push_back(cur), cur.clear();
+    } else {
+      cur.push_back(c);
+    }
+  }
+  if (!cur.empty()) w.push_back(cur);
+  return w;
+}
+
+// Returns 0, or -1 with a message in `err`.
+inline int parse_level(const char* dom, const char* objs, const char* inter, Level& L,
+                       std::vector<uint8_t>& grid, std::string& err) {
+  memset(&L, 0, sizeof L);
+  std::vector<std::string> desc;
+  for (auto& l : lines_of(dom)) desc.push_back(strip(l));  // get_file_description
+  while (!desc.empty() && desc.back().empty()) desc.pop_back();
+  if (desc.empty()) return level_err(err, "level: empty domain");
+  L.W = (int)desc[0].size();
+  L.H = (int)desc.size();
+  if (L.W * L.H > MAX_CELLS || L.W > 120 || L.H > 120)
+    return level_err(err, "level: %dx%d exceeds the %d-cell LDS grid", L.W, L.H, MAX_CELLS);
+  grid.assign((size_t)L.W * L.H, C_OPEN);
+  bool found = false;
+  for (int y = 0; y < L.H; ++y) {
+    if ((int)desc[y].size() != L.W) return level_err(err, "level: ragged row %d", y);
+    for (int x = 0; x < L.W; ++x) {
+      const char c = desc[y][x];
+      grid[y * L.W + x] = c == ' ' ? C_OPEN : c == '/' ? C_WALL : c == 'L' ? C_LADDER
+                                                              : c == 'D' ? C_DOOR : C_OTHER;
+      if (!found && c != '/') {  // player_initial_position (IM/:173-176)
+        L.start_x = x;
+        L.start_y = y;
+        found = true;
+      }
+    }
+  }
+  if (!found) return level_err(err, "level: no non-wall cell for the start position");
+  // read_objects (IM/:119-166): this kernel is specialised to the reference roster, in file
+  // order door, door, door, handle, handle, key, bolt, gold
+  static const char* kRoster[8] = {"door", "door", "door", "handle", "handle", "key", "bolt", "gold"};
+  int k = 0;
+  for (auto& l : lines_of(objs)) {
+    const char* p = l.c_str();
+    const char* t = !strncmp(p, "door", 4) ? "door" : !strncmp(p, "key", 3) ? "key"
+                    : !strncmp(p, "bolt", 4) ? "bolt" : !strncmp(p, "gold", 4) ? "gold"
+                    : !strncmp(p, "handle", 6) ? "handle" : nullptr;
+    if (!t) continue;
+    auto w = words(l);
+    if (k >= 8 || strcmp(t, kRoster[k]) || w.size() < 3)
+      return level_err(err, "level: object roster must be door x3, handle x2, key, bolt, gold");
+    const int cx = atoi(w[1].c_str()), cy = atoi(w[2].c_str());
+    const bool flag = w.size() > 3 && w[3] == "True";
+    if (cx < 0 || cy < 0 || cx >= L.W || cy >= L.H)
+      return level_err(err, "level: object %d outside the grid", k);
+    if (k < 3) {
+      L.door_cx[k] = (int8_t)cx;
+      L.door_cy[k] = (int8_t)cy;
+      grid[cy * L.W + cx] = (uint8_t)(C_DOORSLOT + k);
+      if (flag) L.init_flags |= 1u << (F_OBJ + k);
+    } else if (k < 5) {
+      L.handle_cx[k - 3] = (int8_t)cx;
+      L.handle_cy[k - 3] = (int8_t)cy;
+      if (flag) L.init_flags |= 1u << (F_OBJ + k);
+    } else if (k == 5) {
+      L.key_cx = (int8_t)cx;
+      L.key_cy = (int8_t)cy;
+    } else if (k == 6) {
+      L.bolt_cx = (int8_t)cx;
+      L.bolt_cy = (int8_t)cy;
+      if (flag) L.init_flags |= 1u << (F_OBJ + 5);
+    } else {
+      L.gold_cx = (int8_t)cx;
+      L.gold_cy = (int8_t)cy;
+    }
+    ++k;
+  }
+  if (k != 8) return level_err(err, "level: object roster incomplete (%d of 8)", k);
+  for (int a = 0; a < 3; ++a)
+    for (int b = a + 1; b < 3; ++b)
+      if (L.door_cx[a] == L.door_cx[b] && L.door_cy[a] == L.door_cy[b])
+        return level_err(err, "level: two doors share a cell");
+  // extract_interactives (IM/:75-117): per-object trigger lists in file order
+  for (auto& l : lines_of(inter)) {
+    auto w = words(l);
+    if (w.empty()) continue;
+    if (w.size() != 6) return level_err(err, "level: bad interaction line '%s'", l.c_str());
+    auto id = [](const std::string& t, int idx) -> int {
+      if (t == "door" && idx >= 0 && idx < 3) return idx;
+      if (t == "handle" && idx >= 0 && idx < 2) return 3 + idx;
+      if (t == "bolt" && idx == 0) return 5;
+      return -1;
+    };
+    const int src = id(w[0], atoi(w[1].c_str())), dst = id(w[3], atoi(w[4].c_str()));
+    if (src < 0 || dst < 0) return level_err(err, "level: bad interaction '%s'", l.c_str());
+    const int pol = w[2] == "True", val = w[5] == "True";
+    uint32_t& list = L.trig[src][pol];
+    const uint32_t cnt = list & 0xFu;
+    if (cnt >= 7) return level_err(err, "level: more than 7 triggers on one object");
+    list = (list & ~0xFu) | (cnt + 1) | ((uint32_t)(dst | (val << 3)) << (4 + 4 * cnt));
+  }
+  return 0;
+}
+
+}  // namespace tg

@@ -1,0 +1,315 @@
+"""Env surfaces over the C ABI: ``TreasureGameVec`` (N envs on one GPU, torch tensors) and
+``TreasureGame`` (the N=1 drop-in for the reference ``TreasureGame``, treasure_game.py:54-114).
+
+Seeding contract: env ``g`` of a batch created with ``seed=s,
+global_offset=o`` replays, bit for bit, a reference env in a fresh process after
+``random.seed(s + o + g); env = TreasureGame(); env.reset()``.  Every env owns its own
+CPython-compatible MT19937 stream; the reference's envs share one process-global stream
+(IM/:2, OB/:9), which is the one deliberate difference.
+"""
+import ctypes
+import operator
+import os
+import random
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import TgError, check
+
+OPTION_NAMES = ["go_left_option", "go_right_option", "up_ladder_option", "down_ladder_option",
+                "interact_option", "down_left_option", "down_right_option", "jump_left_option",
+                "jump_right_option"]  # create_options order (IM/:484-498)
+STATE_NAMES = ["playerx", "playery", "handle1.angle", "handle2.angle", "key.x", "key.y",
+               "bolt.locked", "goldcoin.x", "goldcoin.y"]  # get_state_descriptors (IM/:380-400)
+LEVEL_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "levels", "default")
+
+
+# ---- spaces: gym's / gymnasium's when importable, else minimal stand-ins with the same fields
+def _spaces():
+    for mod in ("gym.spaces", "gymnasium.spaces"):
+        try:
+            m = __import__(mod, fromlist=["Discrete", "Box"])
+            return m.Discrete, m.Box
+        except Exception:  # noqa: BLE001 — absent or broken install: use the stand-ins
+            continue
+
+    class Discrete:
+        def __init__(self, n):
+            self.n = int(n)
+            self.shape = ()
+            self.dtype = np.int64
+
+        def sample(self):
+            return random.randrange(self.n)
+
+        def contains(self, x):
+            try:
+                return 0 <= int(x) < self.n
+            except (TypeError, ValueError):
+                return False
+
+        def __repr__(self):
+            return "Discrete(%d)" % self.n
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.shape = tuple(shape)
+            self.dtype = np.dtype(dtype)
+            self.low = np.full(self.shape, low, self.dtype)
+            self.high = np.full(self.shape, high, self.dtype)
+
+        def sample(self):
+            return np.random.uniform(self.low, self.high).astype(self.dtype)
+
+        def contains(self, x):
+            x = np.asarray(x)
+            return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+        def __repr__(self):
+            return "Box(%s, %s, %s, %s)" % (self.low.min(), self.high.max(), self.shape, self.dtype)
+
+    return Discrete, Box
+
+
+Discrete, Box = _spaces()
+
+
+def read_level(path=LEVEL_DIR):
+    """The three level files (reference formats, IM/:75-202) as bytes."""
+    out = []
+    for f in ("domain.txt", "domain-objects.txt", "domain-interactions.txt"):
+        with open(os.path.join(path, f), "rb") as fh:
+            out.append(fh.read())
+    return tuple(out)
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class TreasureGameVec:
+    """``num_envs`` Treasure Game envs resident in one GPU's HBM.
+
+    ``step`` takes an int32 action tensor [N] (values in [-9, 8], Python list indexing as in
+    TG/:92) and returns ``(obs f64 [N,9], reward i32 [N], valid u8 [N], done u8 [N], info)``;
+    ``valid == 0`` is the reference's ``None`` reward (OP/:22-23).  Returned tensors are the
+    env's own output buffers and are overwritten by the next call (``copy=True`` clones).
+    With ``autoreset=True`` an env that returns done is reset in the same step (the reference
+    never resets by itself; this is the equivalent of calling ``reset()`` right after), its
+    pre-reset obs goes to ``info["final_obs"]`` and its episode (return, length) to
+    ``episodes()``.
+    """
+
+    def __init__(self, num_envs, seed=0, device=None, global_offset=0, autoreset=False,
+                 level_dir=None, copy=False):
+        if not torch.cuda.is_available():
+            raise TgError("TreasureGameVec needs a ROCm GPU (gfx950); there is no CPU path")
+        self._L = _lib.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.num_envs = int(num_envs)
+        self.seed = int(seed)
+        self.global_offset = int(global_offset)
+        self.autoreset = bool(autoreset)
+        self.copy = bool(copy)
+        texts = read_level(level_dir) if level_dir else (None, None, None)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self._L.tg_create(ctypes.byref(h), self.num_envs, self.seed & (2**64 - 1),
+                                    self.global_offset, self.device.index, *texts), "tg_create")
+        self._h = h
+        n, dev = self.num_envs, self.device
+        self._obs = torch.empty((n, 9), dtype=torch.float64, device=dev)
+        self._final = torch.empty((n, 9), dtype=torch.float64, device=dev) if autoreset else None
+        self._rew = torch.empty(n, dtype=torch.int32, device=dev)
+        self._valid = torch.empty(n, dtype=torch.uint8, device=dev)
+        self._done = torch.empty(n, dtype=torch.uint8, device=dev)
+        self._act = torch.empty(n, dtype=torch.int32, device=dev)
+        self._mask = torch.empty(n, dtype=torch.int16, device=dev)
+        self.action_space = Discrete(_lib.NUM_ACTIONS)
+        self.observation_space = Box(np.float32(0.0), np.float32(1.0), shape=(_lib.OBS_DIM,))
+        self.option_names = list(OPTION_NAMES)
+
+    # -- plumbing ---------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _out(self, t):
+        return t.clone() if self.copy else t
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise TgError("env is closed")
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            torch.cuda.synchronize(self.device)
+            self._L.tg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 — interpreter teardown
+            pass
+
+    # -- reference surface --------------------------------------------------------------------
+    def reset(self, mask=None):
+        """reset() (TG/:78-81) of every env, or of those with mask[i] != 0."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+            if m.numel() != self.num_envs:
+                raise ValueError("mask must have num_envs entries")
+        check(self._L.tg_reset(self.handle, _ptr(m), _ptr(self._obs), self._stream()), "tg_reset")
+        return self._out(self._obs)
+
+    def step(self, actions):
+        """step(a) (TG/:91-96) for every env."""
+        a = actions
+        if not (isinstance(a, torch.Tensor) and a.dtype == torch.int32 and a.device == self.device
+                and a.is_contiguous()):
+            a = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
+        if a.numel() != self.num_envs:
+            raise ValueError("actions must have num_envs entries")
+        check(self._L.tg_step(self.handle, _ptr(a), _ptr(self._obs), _ptr(self._rew),
+                              _ptr(self._valid), _ptr(self._done), _ptr(self._final),
+                              _lib.TG_STEP_AUTORESET if self.autoreset else 0, self._stream()),
+              "tg_step")
+        info = {"final_obs": self._out(self._final)} if self.autoreset else {}
+        return (self._out(self._obs), self._out(self._rew), self._out(self._valid),
+                self._out(self._done), info)
+
+    def available_mask(self):
+        """available_mask (TG/:83-89) as bits: int16 [N], bit k == option k can run."""
+        check(self._L.tg_available_mask(self.handle, _ptr(self._mask), self._stream()),
+              "tg_available_mask")
+        return self._out(self._mask)
+
+    def observe(self):
+        """get_state (IM/:368-378) of every env."""
+        check(self._L.tg_observe(self.handle, _ptr(self._obs), self._stream()), "tg_observe")
+        return self._out(self._obs)
+
+    # -- batch extras -------------------------------------------------------------------------
+    def policy_actions(self, t, action_seed=0x5EED0001, policy="uniform", out=None):
+        """Counter-hash synthetic actions for step t (bench / parity), keyed by GLOBAL env id."""
+        pol = {"uniform": _lib.TG_POLICY_UNIFORM, "masked": _lib.TG_POLICY_MASKED}[policy]
+        out = self._act if out is None else out
+        check(self._L.tg_policy_actions(self.handle, action_seed, int(t), pol, _ptr(out),
+                                        self._stream()), "tg_policy_actions")
+        return out
+
+    def drain_episodes(self, out, count):
+        """Asynchronous device drain: up to out.shape[0] records -> ``out`` (int64 [cap, 2],
+        the raw 16-B tg_episode rows), their number -> ``count`` (int32 [1])."""
+        check(self._L.tg_episodes(self.handle, _ptr(out), _ptr(count), out.shape[0],
+                                  self._stream()), "tg_episodes")
+
+    @staticmethod
+    def decode_episodes(rows):
+        """raw tg_episode rows (int64 [k, 2]) -> int64 [k, 3] = (env, return, length)."""
+        packed = rows[:, 1]
+        ret = ((packed & 0xFFFFFFFF) ^ 0x80000000) - 0x80000000  # sign-extend the i32 half
+        return torch.stack([rows[:, 0], ret, packed >> 32], dim=1)
+
+    def episodes(self, cap=None):
+        """Completed (auto-reset) episodes, oldest first, up to ``cap`` of them:
+        int64 [k, 3] = (global env, return, length) on the device (synchronises)."""
+        cap = self.num_envs if cap is None else int(cap)
+        rec = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=self.device)
+        cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.drain_episodes(rec[:cap], cnt)
+        return self.decode_episodes(rec[: int(cnt.item())])
+
+    def errors(self):
+        v = ctypes.c_uint32(0)
+        check(self._L.tg_errors(self.handle, ctypes.byref(v), self._stream()), "tg_errors")
+        return int(v.value)
+
+    def set_timing(self, enable=True):
+        check(self._L.tg_set_timing(self.handle, int(bool(enable))), "tg_set_timing")
+
+    def stats(self):
+        s = _lib.Stats()
+        check(self._L.tg_get_stats(self.handle, ctypes.byref(s)), "tg_get_stats")
+        return s.as_dict()
+
+    def stats_reset(self):
+        check(self._L.tg_stats_reset(self.handle), "tg_stats_reset")
+
+    def read_state(self, mt=False):
+        """Host copy of the SoA state (checkpoints / tests)."""
+        n = self.num_envs
+        out = {"pos": np.zeros((n, 2), np.int32), "flags": np.zeros(n, np.uint32),
+               "objs": np.zeros((n, 4), np.int32), "ang": np.zeros((n, 2), np.float64),
+               "mt_pos": np.zeros(n, np.uint32)}
+        if mt:
+            out["mt"] = np.zeros((n, 624), np.uint32)
+
+        def p(k):
+            return out[k].ctypes.data_as(ctypes.c_void_p) if k in out else None
+
+        check(self._L.tg_read_state(self.handle, p("pos"), p("flags"), p("objs"), p("ang"),
+                                    p("mt"), p("mt_pos")), "tg_read_state")
+        return out
+
+
+class TreasureGame:
+    """Drop-in for the reference ``TreasureGame`` (treasure_game.py:54-114), one env on the GPU.
+
+    Same surface and Python types: ``reset() -> list[9]``, ``step(a) -> (list[9], int | None,
+    bool, {})``, ``available_mask`` (np int array [9]), ``action_space`` Discrete(9),
+    ``observation_space`` Box(0, 1, (9,), float32), ``option_names``.  ``TreasureGame(seed=s)``
+    equals ``random.seed(s); TreasureGame()`` in a fresh reference process; ``seed=None``
+    draws a seed from Python's global ``random`` (so ``random.seed`` still makes runs
+    reproducible, but not draw-for-draw identical to the reference's shared stream).
+    Pixel rendering (``render`` / ``ObservationWrapper``, TG/:38-51, 98-114) is not part of
+    this path yet and raises.
+    """
+
+    metadata = {"render.modes": ["human", "rgb_array"]}
+
+    def __init__(self, seed=None, device=None, level_dir=None):
+        if seed is None:
+            seed = random.getrandbits(64)
+        self._vec = TreasureGameVec(1, seed=seed, device=device, level_dir=level_dir)
+        self.option_list = list(range(_lib.NUM_ACTIONS))
+        self.option_names = list(OPTION_NAMES)
+        self.action_space = Discrete(_lib.NUM_ACTIONS)
+        self.observation_space = Box(np.float32(0.0), np.float32(1.0), shape=(_lib.OBS_DIM,))
+        self.viewer = None
+        self._act = torch.empty(1, dtype=torch.int32, device=self._vec.device)
+
+    def reset(self):
+        return self._vec.reset().cpu().numpy()[0].tolist()
+
+    @property
+    def available_mask(self):
+        m = int(self._vec.available_mask().cpu().item()) & 0x1FF
+        return np.array([(m >> k) & 1 for k in range(_lib.NUM_ACTIONS)])
+
+    def step(self, action):
+        a = operator.index(action)  # list indexing accepts ints only (TG/:92)
+        if not -_lib.NUM_ACTIONS <= a < _lib.NUM_ACTIONS:
+            raise IndexError("list index out of range")
+        self._act.fill_(a)
+        obs, rew, valid, done, _ = self._vec.step(self._act)
+        packed = torch.cat([obs[0], rew.to(torch.float64), valid.to(torch.float64),
+                            done.to(torch.float64)]).cpu().numpy()
+        state = packed[:9].tolist()
+        r = int(packed[9]) if packed[10] else None
+        return state, r, bool(packed[11]), {}
+
+    def render(self, mode="human"):
+        raise NotImplementedError("pixel rendering (TG/:98-110) is outside this build's hot path")
+
+    def close(self):
+        if self.viewer is not None:
+            self.viewer = None
+        self._vec.close()

@@ -48,6 +48,7 @@ def lib():
         L.tgo_internal.argtypes = [P, P]
         L.tgo_predicates.restype = ctypes.c_uint
         L.tgo_predicates.argtypes = [P, i32, i32, ctypes.c_uint]
+        L.tgo_predicate_table.argtypes = [P, i32, i32, i32, i32, ctypes.c_uint, P]
         L.tgo_run.restype = i32
         L.tgo_run.argtypes = [P, u64, i64, i64, i32, u64, i32, i32, P, P, P, P, P, P, P, P, i32]
         L.tgo_rng_words.argtypes = [u64, i32, P]
@@ -130,6 +131,11 @@ class OracleEnv:
 
     def predicates(self, px, py, door_bits):
         return int(lib().tgo_predicates(self._h, int(px), int(py), int(door_bits)))
+
+    def predicate_table(self, x0, x1, y0, y1, door_bits):
+        out = np.zeros((y1 - y0, x1 - x0), np.uint8)
+        lib().tgo_predicate_table(self._h, x0, x1, y0, y1, door_bits, _p(out))
+        return out
 
 
 def run(seed_base, g0, n, steps, action_seed, policy=0, autoreset=False, full=True,

@@ -1004,6 +1004,14 @@ unsigned tgo_predicates(tgo_env *e, int px, int py, unsigned door_bits) {
     return m;
 }
 
+void tgo_predicate_table(tgo_env *e, int x0, int x1, int y0, int y1, unsigned door_bits,
+                         uint8_t *out) {
+    for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++)
+            out[(size_t)(y - y0) * (size_t)(x1 - x0) + (size_t)(x - x0)] =
+                (uint8_t)tgo_predicates(e, x, y, door_bits);
+}
+
 /* ======================================================================================
  * Action stream + hash (same as tests/golden/make_golden.py)
  * ====================================================================================== */

@@ -48,6 +48,9 @@ void tgo_internal(const tgo_env *e, int32_t out[12]);
 /* the 6 collision predicates of IM/:232-288 at an arbitrary pixel position / door state
  * (bit order: up_clear, can_go_up, can_go_down, can_go_left, can_go_right, can_fall) */
 unsigned tgo_predicates(tgo_env *e, int px, int py, unsigned door_bits);
+/* the same over the pixel box [x0,x1) x [y0,y1), row-major u8 */
+void tgo_predicate_table(tgo_env *e, int x0, int x1, int y0, int y1, unsigned door_bits,
+                         uint8_t *out);
 
 /* --- batched driver (the CPU baseline and the parity generator) ------------------------- */
 /* Runs envs g in [g0, g0+n), env g seeded seed_base+g, for `steps` env-steps with the

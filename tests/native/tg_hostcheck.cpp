@@ -1,0 +1,138 @@
+// tg_hostcheck.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// Host-only build of the product's per-env core (gym-treasure-game_amd/csrc/tg_core.h), so
+// the exact code the gfx950 kernel runs per lane can be checked against the oracle on the
+// build machine, which has no GPU.  It replays k_step's per-lane sequence (env_step, observe,
+// optional auto-reset) one env at a time.  The product library never contains or calls this.
+// Built by tests/native/Makefile with hipcc --offload-host-only.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../gym-treasure-game_amd/csrc/tg_core.h"
+#include "../../gym-treasure-game_amd/csrc/tg_level.h"
+
+using namespace tg;
+
+namespace {
+uint64_t sm64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+uint64_t rec_hash(uint64_t h, const double o[9], int32_t r, int v, int d) {
+  for (int i = 0; i < 9; ++i) {
+    uint64_t b;
+    memcpy(&b, &o[i], 8);
+    h = sm64(h ^ b);
+  }
+  return sm64(h ^ ((uint64_t)(uint32_t)r | ((uint64_t)v << 32) | ((uint64_t)d << 40)));
+}
+}  // namespace
+
+extern "C" {
+
+static bool load_level(const char* dom, const char* objs, const char* inter, Level& L,
+                       std::vector<uint8_t>& grid) {
+  std::string err;
+  if (!dom) {
+    dom = kDefaultDomain;
+    objs = kDefaultObjects;
+    inter = kDefaultInteractions;
+  }
+  return parse_level(dom, objs, inter, L, grid, err) == 0;
+}
+
+// Level texts as tg_create takes them (NULL = built-in default).
+// obs/final_obs [n][steps+1][9], reward/valid/done [n][steps+1], hash/draws/ticks [n]
+int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_base, int64_t g0,
+           int64_t n, int steps, uint64_t a0, int policy, int autoreset, double* obs,
+           int32_t* reward, uint8_t* valid, uint8_t* done, double* final_obs, uint64_t* hash,
+           int64_t* draws, int64_t* ticks) {
+  Level Lv;
+  std::vector<uint8_t> grid;
+  if (!load_level(dom, objs, inter, Lv, grid)) return -1;
+  const Level* L = &Lv;
+  uint32_t gen[MT_N];
+  gen[0] = 19650218u;
+  for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
+  const Map m{grid.data(), L->W, L->H};
+  const int64_t T1 = (int64_t)steps + 1;
+  std::vector<uint32_t> mt(MT_N);
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t g = (uint64_t)(g0 + i);
+    seed_mt(mt.data(), gen, seed_base + g);
+    Env e{};
+    Rng rng{mt.data(), 0u, 0u};
+    reset_env(*L, e, rng);
+    reset_env(*L, e, rng);
+    double o[9], fo[9];
+    observe(*L, e, o);
+    uint64_t h = rec_hash(g, o, 0, 0, 0);
+    int64_t nt = 0;
+    if (obs) memcpy(&obs[i * T1 * 9], o, sizeof o);
+    if (final_obs) memcpy(&final_obs[i * T1 * 9], o, sizeof o);
+    if (reward) reward[i * T1] = 0;
+    if (valid) valid[i * T1] = 0;
+    if (done) done[i * T1] = 0;
+    for (int t = 0; t < steps; ++t) {
+      const uint64_t hh = sm64(sm64(a0 ^ sm64(g)) ^ (uint64_t)t);
+      int a = (int)(hh % 9ull);
+      if (policy == 1) {
+        const uint32_t mk = available_mask(*L, m, e);
+        const int c = __builtin_popcount(mk);
+        if (c) {
+          uint32_t k = (uint32_t)(hh % (uint64_t)c), mm = mk;
+          while (k--) mm &= mm - 1u;
+          a = __builtin_ctz(mm);
+        }
+      }
+      const StepResult r = env_step(*L, m, e, a, rng);
+      nt += r.ticks;
+      observe(*L, e, fo);
+      memcpy(o, fo, sizeof o);
+      if (autoreset && r.done) {
+        reset_env(*L, e, rng);
+        observe(*L, e, o);
+      }
+      h = rec_hash(h, fo, r.reward, r.ran, r.done);
+      const int64_t j = i * T1 + t + 1;
+      if (obs) memcpy(&obs[j * 9], o, sizeof o);
+      if (final_obs) memcpy(&final_obs[j * 9], fo, sizeof fo);
+      if (reward) reward[j] = r.reward;
+      if (valid) valid[j] = (uint8_t)r.ran;
+      if (done) done[j] = (uint8_t)r.done;
+    }
+    if (hash) hash[i] = h;
+    if (draws) draws[i] = rng.draws;  // includes the 8 construct + reset draws
+    if (ticks) ticks[i] = nt;
+  }
+  return 0;
+}
+
+// the six collision predicates at a pixel position / door state (same bit order as the
+// oracle's tgo_predicates)
+unsigned hc_predicates(int px, int py, unsigned door_bits) {
+  static Level L;
+  static std::vector<uint8_t> grid;
+  if (grid.empty() && !load_level(nullptr, nullptr, nullptr, L, grid)) return ~0u;
+  const Map m{grid.data(), L.W, L.H};
+  Env e{};
+  e.px = px;
+  e.py = py;
+  e.f = (door_bits & 7u) << F_OBJ;
+  return (unsigned)m.up_clear(e) | (unsigned)m.can_go_up(e) << 1 | (unsigned)m.can_go_down(e) << 2 |
+         (unsigned)m.can_go_side(e, -1) << 3 | (unsigned)m.can_go_side(e, +1) << 4 |
+         (unsigned)m.can_fall(e) << 5;
+}
+
+void hc_predicate_table(int x0, int x1, int y0, int y1, unsigned door_bits, uint8_t* out) {
+  for (int y = y0; y < y1; ++y)
+    for (int x = x0; x < x1; ++x)
+      out[(size_t)(y - y0) * (size_t)(x1 - x0) + (size_t)(x - x0)] =
+          (uint8_t)hc_predicates(x, y, door_bits);
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+"""The drop-in boundary: libtg_amd.so loads and exports every entry point include/tg_amd.h
+declares, and fails loudly (never silently) without a gfx950 device."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "tg_amd.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tg_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    names = header_functions()
+    for must in ("tg_create", "tg_reset", "tg_step", "tg_available_mask", "tg_destroy"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(tg):
+    lib = tg._lib.load()
+    names = header_functions()
+    assert sorted(tg._lib.EXPORTS) == names
+    out = subprocess.check_output(["nm", "-D", "--defined-only", tg._lib.LIB_PATH]).decode()
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    for n in names:
+        assert getattr(lib, n) is not None
+    assert lib.tg_version().decode().endswith("gfx950")
+
+
+def test_library_has_gfx950_code_object(tg):
+    blob = open(tg._lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the .hip_fatbin bundle id
+
+
+def test_bad_level_is_rejected_before_touching_a_device(tg):
+    lib = tg._lib.load()
+    h = ctypes.c_void_p()
+    rc = lib.tg_create(ctypes.byref(h), 4, 0, 0, 0, b"////\n/  /\n////\n", b"door 1 1 True\n",
+                       b"")
+    assert rc == -1  # TG_E_INVAL: roster incomplete
+    assert b"roster" in lib.tg_last_error()
+    rc = lib.tg_create(ctypes.byref(h), 4, 0, 0, 0, b"x", None, None)
+    assert rc == -1
+    rc = lib.tg_create(ctypes.byref(h), 0, 0, 0, 0, None, None, None)
+    assert rc == -1
+
+
+def test_no_device_fails_loudly(tg):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    lib = tg._lib.load()
+    h = ctypes.c_void_p()
+    rc = lib.tg_create(ctypes.byref(h), 4, 0, 0, 0, None, None, None)
+    assert rc == -4  # TG_E_NODEV
+    assert not h.value
+    with pytest.raises(tg.TgError):
+        tg.make(num_envs=8)
+    with pytest.raises(tg.TgError):
+        tg.make(seed=0)

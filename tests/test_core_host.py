@@ -1,0 +1,85 @@
+"""The product's per-env core (csrc/tg_core.h: lazy-twist MT, cell-level predicates,
+register-stack trigger cascade) compiled for the host, against the golden vectors and the
+oracle.  This is the same code every kernel lane runs; the GPU tests then check the kernels
+themselves (LDS staging, SoA packing, ballots) on the device."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+KEYS = ["obs", "reward", "valid", "done", "final_obs", "hash", "draws", "ticks"]
+
+
+def hc_run(lib, seed_base, g0, n, steps, a0, policy, autoreset):
+    t1 = steps + 1
+    o = {"obs": np.zeros((n, t1, 9)), "final_obs": np.zeros((n, t1, 9)),
+         "reward": np.zeros((n, t1), np.int32), "valid": np.zeros((n, t1), np.uint8),
+         "done": np.zeros((n, t1), np.uint8), "hash": np.zeros(n, np.uint64),
+         "draws": np.zeros(n, np.int64), "ticks": np.zeros(n, np.int64)}
+    p = {k: o[k].ctypes.data_as(ctypes.c_void_p) for k in o}
+    rc = lib.hc_run(None, None, None, seed_base, g0, n, steps, a0, policy, int(autoreset),
+                    p["obs"], p["reward"], p["valid"], p["done"], p["final_obs"], p["hash"],
+                    p["draws"], p["ticks"])
+    assert rc == 0
+    return o
+
+
+def assert_same(a, b, keys=("obs", "final_obs", "reward", "valid", "done", "hash", "draws")):
+    for k in keys:
+        x, y = a[k], b[k]
+        if x.dtype == np.float64:
+            x, y = x.view(np.uint64), y.view(np.uint64)
+        np.testing.assert_array_equal(x, y, err_msg=k)
+
+
+@pytest.mark.parametrize("name,policy,autoreset", [("traj_uniform.npz", 0, False),
+                                                   ("traj_masked.npz", 1, False),
+                                                   ("traj_autoreset.npz", 1, True)])
+def test_core_vs_golden_trajectories(hostcheck, name, policy, autoreset):
+    d = golden(name)
+    n, t1 = d["valid"].shape
+    o = hc_run(hostcheck, int(d["seed_base"]), 0, n, t1 - 1, int(d["action_seed"]), policy,
+               autoreset)
+    g = {k: d[k] for k in ("obs", "final_obs", "reward", "valid", "done")}
+    assert_same(o, g, keys=list(g))
+    np.testing.assert_array_equal(o["draws"], d["draws"][:, -1])
+
+
+@pytest.mark.parametrize("name,policy", [("hash_uniform.npz", 0), ("hash_masked.npz", 1)])
+def test_core_vs_golden_hashes(hostcheck, name, policy):
+    d = golden(name)
+    o = hc_run(hostcheck, 0, 0, len(d["hash"]), int(d["steps"]), int(d["action_seed"]), policy,
+               False)
+    np.testing.assert_array_equal(o["hash"], d["hash"])
+    np.testing.assert_array_equal(o["draws"], d["draws"])
+    np.testing.assert_array_equal(o["ticks"], d["ticks"])
+
+
+def test_core_predicates_vs_golden_and_oracle(hostcheck, oracle):
+    d = golden("predicates.npz")
+    x0, x1, y0, y1 = (int(v) for v in d["box"])
+    e = oracle.OracleEnv(0)
+    for db in range(8):  # all door states vs the oracle, the two pinned ones vs the reference
+        out = np.zeros((y1 - y0, x1 - x0), np.uint8)
+        hostcheck.hc_predicate_table(x0, x1, y0, y1, db, out.ctypes.data_as(ctypes.c_void_p))
+        np.testing.assert_array_equal(out, e.predicate_table(x0, x1, y0, y1, db), err_msg=str(db))
+        if db in (0, 7):
+            np.testing.assert_array_equal(out, d["table"][0 if db == 0 else 1])
+
+
+@pytest.mark.parametrize("seed_base,g0,n,steps,policy,autoreset", [
+    (10**9, 0, 2048, 400, 0, False),          # other seeds, uniform
+    (2**32 - 100, 0, 256, 300, 0, False),     # seeds crossing 2**32 (2-word init_by_array keys)
+    (0, 2**40, 256, 300, 1, True),            # huge global index, masked + auto-reset
+    (7, 5000, 512, 2500, 1, True),            # long masked runs: many episodes and resets
+])
+def test_core_vs_oracle(hostcheck, oracle, seed_base, g0, n, steps, policy, autoreset):
+    a0 = 0xA5A5 + policy
+    o = hc_run(hostcheck, seed_base, g0, n, steps, a0, policy, autoreset)
+    r = oracle.run(seed_base, g0, n, steps, a0, policy, autoreset)
+    assert_same(o, r)
+    np.testing.assert_array_equal(o["ticks"], r["ticks"])
+    if autoreset and steps > 1000:
+        assert r["done"].sum() > 0

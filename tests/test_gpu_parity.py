@@ -1,0 +1,245 @@
+"""GPU parity: the gfx950 kernels, called through the C ABI (libtg_amd.so), against the
+reference's golden vectors and the CPU oracle.  Bit-exact everywhere: obs compared as f64 bit
+patterns, reward / None / done exactly, draw and tick counts exactly."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def sm64(x):
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def rec_hash(h, obs, rew, valid, done):
+    """vectorised tests/golden/make_golden.py:rec_hash over envs"""
+    bits = np.ascontiguousarray(obs).view(np.uint64)
+    for k in range(9):
+        h = sm64(h ^ bits[:, k])
+    w = (rew.astype(np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)) | \
+        (valid.astype(np.uint64) << np.uint64(32)) | (done.astype(np.uint64) << np.uint64(40))
+    return sm64(h ^ w)
+
+
+def run_gpu(tg, seed_base, g0, n, steps, a0, policy, autoreset, rows=None, hash_only=False,
+            drain_every=0):
+    """Drive a TreasureGameVec like tgo_run drives the oracle; returns env-major arrays.
+    drain_every > 0 collects the auto-reset episode records every that many steps."""
+    pol = "masked" if policy else "uniform"
+    vec = tg.TreasureGameVec(n, seed=seed_base, global_offset=g0, autoreset=autoreset)
+    idx = None if rows is None else torch.as_tensor(rows, device=vec.device)
+    pick = (lambda t: t) if idx is None else (lambda t: t.index_select(0, idx))
+    obs0 = pick(vec.reset()).cpu().numpy()
+    m = obs0.shape[0]
+    h = (np.arange(g0, g0 + n, dtype=np.uint64) if rows is None
+         else (np.uint64(g0) + np.asarray(rows, dtype=np.uint64)))
+    h = rec_hash(h, obs0, np.zeros(m, np.int32), np.zeros(m, np.uint8), np.zeros(m, np.uint8))
+    out = None
+    if not hash_only:
+        out = {"obs": np.zeros((m, steps + 1, 9)), "final_obs": np.zeros((m, steps + 1, 9)),
+               "reward": np.zeros((m, steps + 1), np.int32),
+               "valid": np.zeros((m, steps + 1), np.uint8),
+               "done": np.zeros((m, steps + 1), np.uint8)}
+        out["obs"][:, 0] = obs0
+        out["final_obs"][:, 0] = obs0
+    eps = []
+    for t in range(steps):
+        a = vec.policy_actions(t, a0, pol)
+        o, r, v, d, info = vec.step(a)
+        if drain_every and (t + 1) % drain_every == 0:
+            eps.append(vec.episodes(cap=n).cpu().numpy())
+        fo = info["final_obs"] if autoreset else o
+        o, r, v, d, fo = (pick(x).cpu().numpy() for x in (o, r, v, d, fo))
+        h = rec_hash(h, fo, r, v, d)
+        if out is not None:
+            out["obs"][:, t + 1] = o
+            out["final_obs"][:, t + 1] = fo
+            out["reward"][:, t + 1] = r
+            out["valid"][:, t + 1] = v
+            out["done"][:, t + 1] = d
+    res = out or {}
+    res["hash"] = h
+    if drain_every:
+        eps.append(vec.episodes().cpu().numpy())
+        res["episodes"] = np.concatenate(eps)
+    res["stats"] = vec.stats()
+    res["errors"] = vec.errors()
+    res["vec"] = vec
+    return res
+
+
+def assert_bits(a, b, what):
+    if a.dtype == np.float64:
+        a, b = a.view(np.uint64), b.view(np.uint64)
+    bad = np.argwhere(a != b)
+    assert len(bad) == 0, "%s differs first at %s (%d cells)" % (what, bad[0].tolist(), len(bad))
+
+
+@pytest.mark.parametrize("name,policy,autoreset", [("traj_uniform.npz", 0, False),
+                                                   ("traj_masked.npz", 1, False),
+                                                   ("traj_autoreset.npz", 1, True)])
+def test_golden_trajectories(tg, name, policy, autoreset):
+    d = golden(name)
+    n, t1 = d["valid"].shape
+    o = run_gpu(tg, int(d["seed_base"]), 0, n, t1 - 1, int(d["action_seed"]), policy, autoreset)
+    for k in ("obs", "final_obs", "reward", "valid", "done"):
+        assert_bits(o[k], d[k], k)
+    st = o["stats"]
+    assert st["draws"] == int((d["draws"][:, -1] - 8).sum())  # auto-resets draw in k_step
+    assert o["errors"] == 0
+
+
+@pytest.mark.parametrize("name,policy", [("hash_uniform.npz", 0), ("hash_masked.npz", 1)])
+def test_golden_hashes(tg, name, policy):
+    """4,096 envs x 1,000 uniform steps (config C2) and 1,024 x 600 masked, vs the reference."""
+    d = golden(name)
+    o = run_gpu(tg, 0, 0, len(d["hash"]), int(d["steps"]), int(d["action_seed"]), policy, False,
+                hash_only=True)
+    np.testing.assert_array_equal(o["hash"], d["hash"])
+    st = o["stats"]
+    assert st["draws"] == int((d["draws"] - 8).sum())
+    assert st["ticks"] == int(d["ticks"].sum())
+    assert st["valid_steps"] == int(d["valid_steps"].sum())
+    assert st["steps"] == len(d["hash"]) * int(d["steps"])
+
+
+def test_full_size_sampled_vs_oracle(tg, oracle):
+    """1,048,576 envs (config C3) with auto-reset: 8 blocks of 256 envs spread over the batch
+    replayed exactly by the oracle (every env is independent and seeded by its global index)."""
+    n, steps, a0 = 1 << 20, 40, 0xC3
+    rng = np.random.default_rng(5)
+    starts = np.sort(rng.choice(np.arange(0, n - 256, 256), 8, replace=False))
+    starts[0], starts[-1] = 0, n - 256
+    rows = np.concatenate([np.arange(s, s + 256) for s in starts])
+    o = run_gpu(tg, 11, 0, n, steps, a0, 0, True, rows=rows)
+    for bi, s in enumerate(starts):
+        r = oracle.run(11, int(s), 256, steps, a0, 0, True)
+        sl = slice(bi * 256, (bi + 1) * 256)
+        for k in ("obs", "final_obs", "reward", "valid", "done"):
+            assert_bits(o[k][sl], r[k], "%s block %d" % (k, s))
+    assert o["stats"]["steps"] == n * steps
+    assert o["errors"] == 0
+
+
+def test_masked_autoreset_long_vs_oracle(tg, oracle):
+    """Many episodes: masked policy, auto-reset, 3,000 steps; episode records == oracle's."""
+    n, steps, a0 = 512, 3000, 0x77
+    o = run_gpu(tg, 0, 10**6, n, steps, a0, 1, True, hash_only=True, drain_every=250)
+    r = oracle.run(0, 10**6, n, steps, a0, 1, True)
+    np.testing.assert_array_equal(o["hash"], r["hash"])
+    # the episodes the kernel compacted with its ballots == the oracle's (env, return, length)
+    eps = o["episodes"]
+    exp = []
+    for i in range(n):
+        ret, ln = 0, 0
+        for t in range(1, steps + 1):
+            ret += int(r["reward"][i, t])
+            ln += 1
+            if r["done"][i, t]:
+                exp.append((10**6 + i, ret, ln))
+                ret, ln = 0, 0
+    assert len(exp) > 100
+    assert sorted(map(tuple, eps.tolist())) == sorted(exp)
+    assert o["stats"]["episodes"] == len(exp)
+    assert o["stats"]["episodes_dropped"] == 0
+
+
+def test_sharding_is_invisible(tg):
+    """One 4,096-env batch == two 2,048-env batches at global offsets 0 and 2,048."""
+    full = run_gpu(tg, 5, 0, 4096, 200, 9, 1, True, hash_only=True)["hash"]
+    a = run_gpu(tg, 5, 0, 2048, 200, 9, 1, True, hash_only=True)["hash"]
+    b = run_gpu(tg, 5, 2048, 2048, 200, 9, 1, True, hash_only=True)["hash"]
+    np.testing.assert_array_equal(np.concatenate([a, b]), full)
+
+
+def test_available_mask_matches_oracle(tg, oracle):
+    n, a0 = 256, 0x31
+    vec = tg.TreasureGameVec(n, seed=3, autoreset=False)
+    vec.reset()
+    envs = [oracle.OracleEnv(3 + g) for g in range(n)]
+    for t in range(60):
+        m = vec.available_mask().cpu().numpy().astype(np.uint16)
+        exp = np.array([e.mask() for e in envs], np.uint16)
+        np.testing.assert_array_equal(m & 0x1FF, exp)
+        a = vec.policy_actions(t, a0, "masked").cpu().numpy()
+        for g, e in enumerate(envs):
+            assert a[g] == oracle.pick_action(a0, g, t, True, int(exp[g]))
+            e.step(int(a[g]))
+        vec.step(torch.as_tensor(a, device=vec.device))
+
+
+def test_dropin_single_env(tg, oracle):
+    """TreasureGame(seed=s) == random.seed(s); TreasureGame() of the reference, with the
+    reference's Python types (TG/:91-96): list of floats, int or None, bool, {}."""
+    for seed in (0, 1, 2**33 + 1):
+        env = tg.TreasureGame(seed=seed)
+        ref = oracle.OracleEnv(seed)
+        s = env.reset()
+        assert isinstance(s, list) and len(s) == 9 and all(type(v) is float for v in s)
+        np.testing.assert_array_equal(np.array(s).view(np.uint64), ref.obs.view(np.uint64))
+        for t in range(300):
+            mask = env.available_mask
+            assert mask.tolist() == [(ref.mask() >> k) & 1 for k in range(9)]
+            a = oracle.pick_action(0xD1, seed, t, True, ref.mask())
+            if t % 7 == 3:
+                a = a - 9  # negative indices wrap like option_list[a]
+            st, r, d, info = env.step(a)
+            rs, rr, rd, _ = ref.step(a)
+            assert type(st) is list and info == {} and type(d) is bool
+            assert r is None or type(r) is int
+            np.testing.assert_array_equal(np.array(st).view(np.uint64), rs.view(np.uint64))
+            assert (r, d) == (rr, rd)
+        with pytest.raises(IndexError):
+            env.step(9)
+        with pytest.raises(IndexError):
+            env.step(-10)
+        with pytest.raises(TypeError):
+            env.step(1.0)
+        env.close()
+
+
+def test_step_before_reset_is_the_constructed_state(tg):
+    """tg_create == TreasureGame.__init__ (4 draws): reset() then equals a 2nd build."""
+    vec = tg.TreasureGameVec(64, seed=0)
+    o1 = vec.observe().clone()
+    o2 = vec.reset().clone()
+    d = golden("resets.npz")
+    np.testing.assert_array_equal(o2.cpu().numpy().view(np.uint64), d["obs"][:64].view(np.uint64))
+    assert not torch.equal(o1, o2)
+
+
+def test_bad_action_flags_error(tg):
+    vec = tg.TreasureGameVec(128, seed=0)
+    vec.reset()
+    a = torch.zeros(128, dtype=torch.int32, device=vec.device)
+    a[17] = 42
+    o, r, v, d, _ = vec.step(a)
+    assert int(v[17]) == 0
+    assert vec.errors() & tg._lib.TG_ERR_ACTION
+
+
+def test_reset_mask(tg, oracle):
+    vec = tg.TreasureGameVec(32, seed=0)
+    vec.reset()
+    for t in range(20):
+        vec.step(vec.policy_actions(t, 1, "masked"))
+    before = vec.observe().clone()
+    mask = torch.zeros(32, dtype=torch.uint8, device=vec.device)
+    mask[::3] = 1
+    after = vec.reset(mask).clone()
+    keep = mask.cpu().numpy() == 0
+    np.testing.assert_array_equal(after.cpu().numpy()[keep], before.cpu().numpy()[keep])
+    for g in np.flatnonzero(~keep):
+        e = oracle.OracleEnv(g)
+        for t in range(20):
+            e.step(oracle.pick_action(1, g, t, True, e.mask()))
+        np.testing.assert_array_equal(after[g].cpu().numpy().view(np.uint64),
+                                      e.reset().view(np.uint64))

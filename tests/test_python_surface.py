@@ -1,0 +1,50 @@
+"""The Python surface mirrors the reference's (treasure_game.py:54-114, __init__.py:3-6)."""
+import numpy as np
+import pytest
+
+
+def test_names_match_reference(tg):
+    # create_options order and class names (IM/:484-498); state descriptors (IM/:380-400)
+    assert tg.OPTION_NAMES == ["go_left_option", "go_right_option", "up_ladder_option",
+                               "down_ladder_option", "interact_option", "down_left_option",
+                               "down_right_option", "jump_left_option", "jump_right_option"]
+    assert tg.STATE_NAMES == ["playerx", "playery", "handle1.angle", "handle2.angle", "key.x",
+                              "key.y", "bolt.locked", "goldcoin.x", "goldcoin.y"]
+
+
+def test_spaces(tg):
+    from gym_treasure_game_amd.envs import Box, Discrete
+    d = Discrete(9)
+    assert d.n == 9 and all(d.contains(d.sample()) for _ in range(50))
+    b = Box(np.float32(0.0), np.float32(1.0), shape=(9,))
+    assert b.shape == (9,) and b.dtype == np.float32
+
+
+def test_make_rejects_unknown_id(tg):
+    with pytest.raises(KeyError):
+        tg.make("CartPole-v1")
+
+
+def test_level_files_are_the_reference_level(tg):
+    dom, objs, inter = tg.read_level()
+    rows = [r.strip() for r in dom.decode().splitlines() if r.strip()]
+    assert len(rows) == 13 and all(len(r) == 14 for r in rows)
+    assert objs.decode().split("\n")[0] == "door 9 1 True"
+    assert len([ln for ln in inter.decode().splitlines() if ln.strip()]) == 14
+
+
+def test_register_is_harmless_without_gym(tg):
+    assert isinstance(tg.register(), list)
+
+
+def test_no_oracle_in_the_product_package():
+    """The product must never route through the oracle or any CPU restatement."""
+    import os
+    import re
+    from conftest import ROOT
+    pkg = os.path.join(ROOT, "gym-treasure-game_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                src = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"import oracle|from oracle|\btgo_[a-z]|libtg_oracle|libtg_hostcheck|\bhc_run", src), f
