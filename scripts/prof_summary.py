@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Summarise a gpu_profile.sh session into profiles/<tag>_summary.json (+ traffic_step.json).
+
+    python scripts/prof_summary.py --tag r01 [--out gpurun_out] [--envs 1048576]
+
+Reads the rocprofv3 kernel-trace stats (same command as bench.py) and the separate PMC passes
+(FETCH_SIZE, WRITE_SIZE, SQ_*).  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE /
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts a wide coalesced 128-B read request as 64 B,
+so it is calibrated here on k_errors, which reads exactly 16 B per env (one uint4) in fully
+coalesced 16-B lanes and nothing else.  The calibration factor is applied to k_step's
+FETCH_SIZE and reported beside the raw value.
+"""
+import argparse
+import csv
+import json
+import os
+import re
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    m = re.search(r"(k_[a-z_]+)(<[^>]*>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name.split("(")[0][:60]
+
+
+def kernel_stats(path):
+    out = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            out[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                     "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
+                                     "pct": float(r["Percentage"])}
+    return out
+
+
+def counters(path):
+    per = defaultdict(lambda: defaultdict(list))
+    meta = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            k = short(r["Kernel_Name"])
+            per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta[k] = {"grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),
+                       "sgpr": int(r["SGPR_Count"]), "lds": int(r["LDS_Block_Size"])}
+    avg = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in per.items()}
+    return avg, meta
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default="r01")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--envs", type=int, default=1 << 20)
+    ap.add_argument("--policy", default="uniform")
+    a = ap.parse_args()
+    res = {"tag": a.tag, "envs": a.envs, "policy": a.policy}
+    ks = kernel_stats(os.path.join(a.out, "trace_" + a.tag, "run_kernel_stats.csv"))
+    res["kernel_trace"] = ks
+    pm = {}
+    meta = {}
+    for p in ("fetch", "write", "sq1", "sq2"):
+        path = os.path.join(a.out, "pmc_%s_%s" % (p, a.tag), "run_counter_collection.csv")
+        if os.path.exists(path):
+            avg, m = counters(path)
+            meta.update(m)
+            for k, d in avg.items():
+                pm.setdefault(k, {}).update(d)
+    res["pmc_avg_per_dispatch"] = pm
+    res["dispatch_meta"] = meta
+    step = next((k for k in pm if k.startswith("k_step")), None)
+    if step and "k_errors" in pm and "FETCH_SIZE" in pm[step]:
+        known = 16.0 * a.envs  # k_errors: one 16-B uint4 per env
+        raw_err = pm["k_errors"]["FETCH_SIZE"] * 1024.0
+        cal = known / raw_err if raw_err > 0 else None
+        fetch_raw = pm[step]["FETCH_SIZE"] * 1024.0
+        write = pm[step].get("WRITE_SIZE", 0.0) * 1024.0
+        fetch = fetch_raw * (cal or 1.0)
+        res["hbm"] = {"kernel": step, "fetch_bytes_raw": fetch_raw, "fetch_calibration": cal,
+                      "fetch_bytes": fetch, "write_bytes": write,
+                      "hbm_bytes_per_launch": fetch + write,
+                      "calibration_note": "k_errors reads %d B; FETCH_SIZE reported %.0f B" %
+                                          (known, raw_err)}
+        sq = pm[step]
+        if "SQ_INSTS_VALU" in sq and "SQ_WAVES" in sq:
+            res["per_wave"] = {c: sq[c] / sq["SQ_WAVES"] for c in sq if c.startswith("SQ_INSTS")}
+        if "GRBM_GUI_ACTIVE" in sq and step in ks:
+            # GRBM_GUI_ACTIVE sums over the 8 XCDs (MI355X_MICROARCH.md DVFS note)
+            res["effective_clock_ghz"] = sq["GRBM_GUI_ACTIVE"] / 8 / (ks[step]["avg_ns"])
+        tj = {"envs": a.envs, "policy": a.policy, "kernel": step,
+              "hbm_bytes_per_launch": fetch + write, "source": "profiles/%s_summary.json" % a.tag}
+        with open(os.path.join(ROOT, "profiles", "traffic_step.json"), "w") as f:
+            json.dump(tj, f, indent=1)
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    with open(os.path.join(ROOT, "profiles", "%s_summary.json" % a.tag), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps({k: res[k] for k in res if k in ("hbm", "per_wave", "effective_clock_ghz")},
+                     indent=1))
+    print(json.dumps(ks.get(step or "", {}), indent=1))
+
+
+if __name__ == "__main__":
+    main()
