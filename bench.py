@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--envs", type=int, default=1 << 20, help="envs per GPU")
     ap.add_argument("--policy", default="uniform", choices=["uniform", "masked"])
     ap.add_argument("--no-autoreset", action="store_true")
+    ap.add_argument("--mode", default="compact", choices=["compact", "direct"],
+                    help="step implementation (bit-identical): two-pass compacted or one-pass")
+    ap.add_argument("--run-blocks", type=int, default=0, help="k_run workgroups (0 = default)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU-baseline sample (0 disables it)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_step.json"),
@@ -101,6 +104,7 @@ def main():
     offset, count = D.shard(total, rank, world)
     autoreset = not args.no_autoreset
     vec = tg.TreasureGameVec(count, seed=0, global_offset=offset, autoreset=False, device=dev)
+    vec.set_mode(args.mode, args.run_blocks)
     vec.autoreset = autoreset  # final_obs is not requested: obs/reward/valid/done only
     vec.reset()
     ep_rows = torch.empty((EP_CAP, 2), dtype=torch.int64, device=dev)
@@ -164,7 +168,8 @@ def main():
         traffic = None
         if os.path.exists(args.traffic_json):
             tj = json.load(open(args.traffic_json))
-            if tj.get("envs") == args.envs and tj.get("policy") == args.policy:
+            if (tj.get("envs") == args.envs and tj.get("policy") == args.policy
+                    and tj.get("mode", "direct") == args.mode):
                 traffic = tj.get("hbm_bytes_per_launch")
         line = {
             "metric": METRIC, "value": env_steps / dt, "unit": "env-steps/s", "n_gpus": world,
@@ -176,12 +181,15 @@ def main():
                                    % (args.envs, args.policy,
                                       " + RCCL episode gather" if world > 1 else ""),
                        "envs_per_gpu": args.envs, "total_envs": total, "policy": args.policy,
-                       "autoreset": autoreset, "parallelism": "env-shard x%d" % world},
+                       "autoreset": autoreset, "step_mode": args.mode,
+                       "parallelism": "env-shard x%d" % world},
             "ticks_per_s": node["ticks"] / dt,
             "valid_step_frac": node["valid_steps"] / max(node["steps"], 1),
             "draws_per_step": node["draws"] / max(node["steps"], 1),
             "episodes": node["episodes"], "error_flags": errs,
-            "roofline": {"bound": "hbm", "kernel": "k_step", "achieved": achieved,
+            "roofline": {"bound": "hbm",
+                         "kernel": "k_classify+k_run" if args.mode == "compact" else "k_step",
+                         "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel_ms": kern_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes},

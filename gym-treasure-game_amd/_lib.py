@@ -14,6 +14,8 @@ TG_OK = 0
 TG_STEP_AUTORESET = 1
 TG_POLICY_UNIFORM = 0
 TG_POLICY_MASKED = 1
+TG_MODE_DIRECT = 0
+TG_MODE_COMPACT = 1
 TG_ERR_TICKCAP = 1 << 24
 TG_ERR_BAG = 1 << 25
 TG_ERR_ACTION = 1 << 26
@@ -23,7 +25,7 @@ NUM_ACTIONS = 9
 
 # every symbol include/tg_amd.h declares (tests check the library exports all of them)
 EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_available_mask",
-           "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_timing",
+           "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing",
            "tg_get_stats", "tg_stats_reset", "tg_read_state", "tg_last_error", "tg_version")
 
 
@@ -72,6 +74,7 @@ def load():
         "tg_policy_actions": (i32, [P, u64, i64, i32, P, P]),
         "tg_episodes": (i32, [P, P, P, i32, P]),
         "tg_errors": (i32, [P, ctypes.POINTER(u32), P]),
+        "tg_set_mode": (i32, [P, i32, i32]),
         "tg_set_timing": (i32, [P, i32]),
         "tg_get_stats": (i32, [P, ctypes.POINTER(Stats)]),
         "tg_stats_reset": (i32, [P]),

@@ -49,7 +49,7 @@ int fail(int code, const char* fmt, ...) {
 // ------------------------------------------------------------------------------------------
 // SoA pack / unpack
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void unpack(const uint4 s, const double2 a, Env& e) {
+__device__ __forceinline__ void unpack_st4(const uint4 s, Env& e) {
   e.px = (int)(int16_t)(s.x & 0xFFFFu);
   e.py = (int)(int16_t)(s.x >> 16);
   e.f = s.y;
@@ -58,6 +58,9 @@ __device__ __forceinline__ void unpack(const uint4 s, const double2 a, Env& e) {
   e.gx = (int)(int8_t)((s.z >> 16) & 0xFF);
   e.gy = (int)(int8_t)(s.z >> 24);
   e.mti = s.w;
+}
+__device__ __forceinline__ void unpack(const uint4 s, const double2 a, Env& e) {
+  unpack_st4(s, e);
   e.ang0 = a.x;
   e.ang1 = a.y;
 }
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(BLOCK) void k_create(Soa S, int64_t n, Level L, uin
   seed_mt(mt, genrand, seed0 + (uint64_t)i);
   Env e{};
   e.f = 0;
-  Rng rng{mt, 0u, 0u};
+  Rng rng(mt, 0u);
   reset_env(L, e, rng);
   e.mti = rng.pos;
   S.st4[i] = pack(e);
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
   Env e;
   unpack(S.st4[i], S.ang[i], e);
   if (!mask || mask[i]) {
-    Rng rng{S.mt + i * MT_N, e.mti, 0u};
+    Rng rng(S.mt + i * MT_N, e.mti);
     reset_env(L, e, rng);
     e.mti = rng.pos;
     S.st4[i] = pack(e);
@@ -141,17 +144,94 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
   }
 }
 
+struct StepIO {
+  const int32_t* __restrict__ actions;
+  double* __restrict__ obs;
+  int32_t* __restrict__ reward;
+  uint8_t* __restrict__ valid;
+  uint8_t* __restrict__ done;
+  double* __restrict__ final_obs;  // may be null
+};
+struct EpQueue {
+  tg_episode* __restrict__ eps;
+  int32_t* count;
+  int32_t cap;
+};
+
+// Completed episodes (auto-reset): wavefront ballot, popcount prefix, one atomic per wave.
+// Must be reached by every lane of the wave.
+__device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, const EpQueue& q,
+                                                unsigned long long* stats) {
+  const unsigned long long b = __ballot(mine);
+  if (!b) return;
+  const int lane = threadIdx.x & 63;
+  const int first = __ffsll((long long)b) - 1;
+  int base = 0;
+  if (lane == first) base = atomicAdd(q.count, __popcll(b));
+  base = __shfl(base, first, 64);
+  if (mine) {
+    const int slot = base + __popcll(b & ((1ull << lane) - 1ull));
+    if (slot < q.cap) {
+      tg_episode r;
+      r.env = g;
+      r.ret = ep.x;
+      r.len = ep.y;
+      q.eps[slot] = r;
+    } else {
+      atomicAdd(&stats[ST_EP_OVERFLOW], 1ull);  // rare: block 0's slot
+    }
+    ep = make_int2(0, 0);
+  }
+}
+
+// Launch counters without global atomics: the block reduces its waves' sums in LDS and its
+// thread 0 adds them into the block's own slot of `part` ([grid][ST_COUNT]); every step
+// kernel uses the same grid, so slots never race.  The host sums the slots on demand.
+// (One counter word per launch took ~32k same-line atomics: ~370 us at ~88 atomics/us.)
+// Must be reached by every thread of the block.
+__device__ __forceinline__ void block_stats(unsigned long long* __restrict__ part, int steps,
+                                            int valid, int ticks, int draws, int episodes) {
+  __shared__ int acc[5];
+  if (threadIdx.x < 5) acc[threadIdx.x] = 0;
+  __syncthreads();
+  const int s0 = wave_sum(steps), s1 = wave_sum(valid), s2 = wave_sum(ticks),
+            s3 = wave_sum(draws), s4 = wave_sum(episodes);
+  if ((threadIdx.x & 63) == 0) {
+    if (s0) atomicAdd(&acc[0], s0);
+    if (s1) atomicAdd(&acc[1], s1);
+    if (s2) atomicAdd(&acc[2], s2);
+    if (s3) atomicAdd(&acc[3], s3);
+    if (s4) atomicAdd(&acc[4], s4);
+  }
+  __syncthreads();
+  if (threadIdx.x < 5 && acc[threadIdx.x])
+    part[(size_t)blockIdx.x * ST_COUNT + threadIdx.x] += (unsigned long long)acc[threadIdx.x];
+}
+
+// finish one env-step: obs/reward/valid/done rows, episode counters, optional auto-reset
+template <bool AUTORESET, bool FINAL>
+__device__ __forceinline__ void finish_step(const Level& L, Env& e, Rng& rng, int64_t i,
+                                            const StepResult& r, int2& ep, const StepIO& io) {
+  double o[9];
+  observe(L, e, o);  // get_state (TG/:94)
+  io.reward[i] = r.reward;
+  io.valid[i] = (uint8_t)r.ran;
+  io.done[i] = (uint8_t)r.done;
+  ep.x += r.reward;
+  ep.y += 1;
+  if (FINAL) store_obs(io.final_obs, i, o);
+  if (AUTORESET && r.done) {
+    reset_env(L, e, rng);
+    observe(L, e, o);
+  }
+  store_obs(io.obs, i, o);
+}
+
+// ---- one-pass step: one lane per env, the option runs in place (TG_MODE_DIRECT) ----------
 template <bool AUTORESET, bool FINAL>
 __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
-                                                 const uint8_t* __restrict__ grid,
-                                                 const int32_t* __restrict__ actions,
-                                                 double* __restrict__ obs,
-                                                 int32_t* __restrict__ reward,
-                                                 uint8_t* __restrict__ valid,
-                                                 uint8_t* __restrict__ done_out,
-                                                 double* __restrict__ final_obs,
-                                                 tg_episode* __restrict__ eps, int32_t* eps_count,
-                                                 int32_t eps_cap, int64_t g0,
+                                                 const uint8_t* __restrict__ grid, StepIO io,
+                                                 EpQueue q, int64_t g0,
                                                  unsigned long long* __restrict__ stats,
                                                  uint32_t* __restrict__ err_or) {
   __shared__ uint8_t lgrid[MAX_CELLS];
@@ -159,76 +239,178 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
   const Map m{lgrid, L.W, L.H};
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
-
-  int ticks = 0, ran = 0, dn = 0;
+  StepResult r{0, 0, 0, 0};
   uint32_t draws = 0;
   Env e;
   int2 ep = make_int2(0, 0);
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
-    Rng rng{S.mt + i * MT_N, e.mti, 0u};
-    const StepResult r = env_step(L, m, e, actions[i], rng);
-    ticks = r.ticks;
-    ran = r.ran;
-    dn = r.done;
-    double o[9];
-    observe(L, e, o);  // get_state (TG/:94)
-    reward[i] = r.reward;
-    valid[i] = (uint8_t)ran;
-    done_out[i] = (uint8_t)dn;
-    ep.x += r.reward;
-    ep.y += 1;
-    if (FINAL) store_obs(final_obs, i, o);
-    if (AUTORESET && dn) {
-      reset_env(L, e, rng);
-      observe(L, e, o);
-    }
-    store_obs(obs, i, o);
+    Rng rng(S.mt + i * MT_N, e.mti);
+    r = env_step(L, m, e, io.actions[i], rng);
+    finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.pos;
     draws = rng.draws;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
-  // completed episodes: wavefront ballot + one atomic per wave
-  if (AUTORESET) {
-    const unsigned long long b = __ballot(live && dn);
-    if (b) {
-      const int lane = threadIdx.x & 63;
-      const int cnt = __popcll(b);
-      const int first = __ffsll((long long)b) - 1;
-      int base = 0;
-      if (lane == first) base = atomicAdd(eps_count, cnt);
-      base = __shfl(base, first, 64);
-      if (live && dn) {
-        const int slot = base + __popcll(b & ((1ull << lane) - 1ull));
-        if (slot < eps_cap) {
-          tg_episode r;
-          r.env = g0 + i;
-          r.ret = ep.x;
-          r.len = ep.y;
-          eps[slot] = r;
-        } else {
-          atomicAdd(&stats[ST_EP_OVERFLOW], 1ull);
-        }
-        ep = make_int2(0, 0);
-      }
-    }
-  }
+  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
   if (live) {
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
     S.ep[i] = ep;
   }
-  // launch counters for the roofline (one atomic per wave and counter)
-  const int s_steps = wave_sum(live ? 1 : 0), s_valid = wave_sum(ran), s_ticks = wave_sum(ticks),
-            s_draws = wave_sum((int)draws), s_dn = wave_sum(AUTORESET ? dn : 0);
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&stats[ST_STEPS], (unsigned long long)s_steps);
-    atomicAdd(&stats[ST_VALID], (unsigned long long)s_valid);
-    atomicAdd(&stats[ST_TICKS], (unsigned long long)s_ticks);
-    atomicAdd(&stats[ST_DRAWS], (unsigned long long)s_draws);
-    if (AUTORESET && s_dn) atomicAdd(&stats[ST_EPISODES], (unsigned long long)s_dn);
+  block_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0);
+}
+
+// ---- two-pass compacted step (TG_MODE_COMPACT) -------------------------------------------
+// Pass 1, k_classify: one lane per env (coalesced).  Evaluates option_list[a].can_run();
+// envs whose option cannot run finish here (reward None, obs/done rows written, state
+// unchanged); the rest are appended to per-option worklists.  Appends are aggregated per
+// workgroup in LDS and the counters are sharded 8 ways (blockIdx % 8) across cache lines, so
+// each counter word sees ~1/72 of the workgroups (one word alone saturates at ~88 atomics/us,
+// MI355X_MICROARCH.md "dequeue").
+// Pass 2, k_run: wave w runs chunk w (64 envs) of the worklists concatenated in
+// longest-option-first order, so a wavefront holds only envs that tick, mostly of one option
+// (uniform control flow, similar lengths); low chunk ids dispatch first.
+constexpr int SHARDS = 8;
+constexpr int NSEG = O_COUNT * SHARDS;
+constexpr int CTR_STRIDE = 32;  // counters 128 B apart
+struct Work {
+  int32_t* __restrict__ lists;  // [NSEG][shard_cap], segment = option * SHARDS + shard
+  int32_t* __restrict__ ctr;    // [NSEG * CTR_STRIDE]
+  int64_t shard_cap;
+};
+// worklist order: longest options first (mean ticks, uniform policy: go 56, jumps 36, drops
+// 30, ladders 26, interact 1 — DESIGN.md §3)
+__constant__ int kOrder[O_COUNT] = {O_GO_LEFT,   O_GO_RIGHT,   O_JUMP_LEFT,   O_JUMP_RIGHT,
+                                    O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
+                                    O_INTERACT};
+
+template <bool AUTORESET, bool FINAL>
+__global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
+                                                     const uint8_t* __restrict__ grid,
+                                                     StepIO io, EpQueue q, Work w, int64_t g0,
+                                                     unsigned long long* __restrict__ stats,
+                                                     uint32_t* __restrict__ err_or) {
+  __shared__ uint8_t lgrid[MAX_CELLS];
+  __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
+  if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
+  stage_grid(lgrid, grid, L.W * L.H);  // includes the barrier
+  const Map m{lgrid, L.W, L.H};
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = i < n;
+  const int lane = threadIdx.x & 63;
+  int k = -1;
+  bool runs = false, dn = false;
+  Env e;
+  uint4 s4 = make_uint4(0, 0, 0, 0);
+  if (live) {
+    s4 = S.st4[i];
+    unpack_st4(s4, e);  // the angles are only needed if the env finishes here
+    k = option_index(io.actions[i]);
+    runs = k >= 0 && can_run(L, m, e, k);
   }
+  // workgroup-local slots: one LDS atomic per wave and option
+  int slot = 0;
+#pragma unroll
+  for (int kk = 0; kk < O_COUNT; ++kk) {
+    const bool mine = runs && k == kk;
+    const unsigned long long b = __ballot(mine);
+    if (b) {
+      const int first = __ffsll((long long)b) - 1;
+      int base = 0;
+      if (lane == first) base = atomicAdd(&bcnt[kk], __popcll(b));
+      base = __shfl(base, first, 64);
+      if (mine) slot = base + __popcll(b & ((1ull << lane) - 1ull));
+    }
+  }
+  __syncthreads();
+  const int shard = blockIdx.x % SHARDS;
+  if (threadIdx.x < O_COUNT) {
+    const int c = bcnt[threadIdx.x];
+    bbase[threadIdx.x] = c ? atomicAdd(&w.ctr[(threadIdx.x * SHARDS + shard) * CTR_STRIDE], c) : 0;
+  }
+  __syncthreads();
+  if (runs) w.lists[(int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot] = (int32_t)i;
+
+  int2 ep = make_int2(0, 0);
+  if (live && !runs) {  // reward None: state unchanged, rows written here
+    if (k < 0) e.f |= E_ACTION;
+    const double2 a2 = S.ang[i];
+    e.ang0 = a2.x;
+    e.ang1 = a2.y;
+    ep = S.ep[i];
+    dn = is_done(e);
+    Rng rng(S.mt + i * MT_N, e.mti);
+    StepResult r{0, 0, (int)dn, 0};
+    finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
+    e.mti = rng.pos;
+    if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+  }
+  if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, q, stats);
+  if (live && !runs) {
+    const uint4 s4n = pack(e);
+    if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w) {  // reset / error
+      S.st4[i] = s4n;
+      S.ang[i] = make_double2(e.ang0, e.ang1);
+    }
+    S.ep[i] = ep;
+  }
+  block_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, AUTORESET ? (live && !runs && dn) : 0);
+}
+
+template <bool AUTORESET, bool FINAL>
+__global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
+                                                const uint8_t* __restrict__ grid, StepIO io,
+                                                EpQueue q, Work w, int64_t g0,
+                                                unsigned long long* __restrict__ stats,
+                                                uint32_t* __restrict__ err_or) {
+  __shared__ uint8_t lgrid[MAX_CELLS];
+  __shared__ int pre[NSEG + 1];  // exclusive prefix of the segments in run order
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 0; b < O_COUNT; ++b)
+      for (int sh = 0; sh < SHARDS; ++sh) {
+        pre[b * SHARDS + sh] = acc;
+        acc += w.ctr[(kOrder[b] * SHARDS + sh) * CTR_STRIDE];
+      }
+    pre[NSEG] = acc;
+  }
+  stage_grid(lgrid, grid, L.W * L.H);  // includes the barrier
+  const int total = pre[NSEG];
+  const int j = blockIdx.x * BLOCK + threadIdx.x;  // wave w runs chunk w
+  const Map m{lgrid, L.W, L.H};
+  const bool live = j < total;
+  int64_t i = 0;
+  StepResult r{0, 0, 0, 0};
+  Env e;
+  int2 ep = make_int2(0, 0);
+  uint32_t draws = 0;
+  if (live) {
+    int lo = 0, hi = NSEG;  // segment: pre[lo] <= j < pre[lo + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pre[mid] <= j) lo = mid; else hi = mid;
+    }
+    const int k = kOrder[lo / SHARDS], sh = lo % SHARDS;
+    i = w.lists[(int64_t)(k * SHARDS + sh) * w.shard_cap + (j - pre[lo])];
+    unpack(S.st4[i], S.ang[i], e);
+    ep = S.ep[i];
+    Rng rng(S.mt + i * MT_N, e.mti);
+    run_option(L, m, e, k, rng, r);
+    r.done = is_done(e);
+    finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
+    e.mti = rng.pos;
+    draws = rng.draws;
+    if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+  }
+  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
+  if (live) {
+    S.st4[i] = pack(e);
+    S.ang[i] = make_double2(e.ang0, e.ang1);
+    S.ep[i] = ep;
+  }
+  block_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
@@ -341,6 +523,10 @@ struct tg_batch {
   int32_t eps_cap = 0;
   unsigned long long* stats = nullptr;  // ST_COUNT
   uint32_t* err = nullptr;
+  int mode = TG_MODE_COMPACT;
+  int32_t* wl = nullptr;   // per-(option, shard) worklists (compact mode)
+  int32_t* wctr = nullptr; // sharded counters
+  int64_t shard_cap = 0;
   bool timing = false;
   std::vector<hipEvent_t> ev;  // (start, stop) pairs
   size_t ev_used = 0;
@@ -433,13 +619,17 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->S.mt, sizeof(uint32_t) * MT_N * (size_t)n);
   ALLOC(h->eps, sizeof(tg_episode) * (size_t)h->eps_cap);
   ALLOC(h->eps_count, sizeof(int32_t));
-  ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT);
+  ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT * (size_t)grid_for(n));
   ALLOC(h->err, sizeof(uint32_t));
+  // a shard holds the envs of every SHARDS-th workgroup
+  h->shard_cap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK;
+  ALLOC(h->wl, sizeof(int32_t) * NSEG * (size_t)h->shard_cap);
+  ALLOC(h->wctr, sizeof(int32_t) * NSEG * CTR_STRIDE);
 #undef ALLOC
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
-      hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT) != hipSuccess ||
+      hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)grid_for(n)) != hipSuccess ||
       hipMemset(h->err, 0, sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail(TG_E_HIP, "tg_create: upload failed"));
   hipLaunchKernelGGL(k_create, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, h->L,
@@ -456,8 +646,8 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   for (auto ev : h->ev) (void)hipEventDestroy(ev);
-  void* bufs[] = {h->grid, h->genrand, h->S.st4, h->S.ang, h->S.ep, h->S.mt,
-                  h->eps,  h->eps_count, h->stats, h->err};
+  void* bufs[] = {h->grid, h->genrand, h->S.st4, h->S.ang,   h->S.ep, h->S.mt,
+                  h->eps,  h->eps_count, h->stats, h->err, h->wl,   h->wctr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -487,11 +677,27 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
     }
     HIP_TRY(hipEventRecord(h->ev[h->ev_used], st));
   }
-  auto kern = ar ? (fo ? k_step<true, true> : k_step<true, false>)
-                 : (fo ? k_step<false, true> : k_step<false, false>);
-  hipLaunchKernelGGL(kern, dim3(grid_for(h->n)), dim3(BLOCK), 0, st, h->S, h->n, h->L, h->grid,
-                     actions, obs, reward, valid, done, final_obs, h->eps, h->eps_count,
-                     h->eps_cap, h->g0, h->stats, h->err);
+  const StepIO io{actions, obs, reward, valid, done, final_obs};
+  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
+  const dim3 grid(grid_for(h->n)), block(BLOCK);
+  if (h->mode == TG_MODE_DIRECT) {
+    auto kern = ar ? (fo ? k_step<true, true> : k_step<true, false>)
+                   : (fo ? k_step<false, true> : k_step<false, false>);
+    hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, h->g0,
+                       h->stats, h->err);
+  } else {
+    const Work w{h->wl, h->wctr, h->shard_cap};
+    HIP_TRY(hipMemsetAsync(h->wctr, 0, sizeof(int32_t) * NSEG * CTR_STRIDE, st));
+    auto kc = ar ? (fo ? k_classify<true, true> : k_classify<true, false>)
+                 : (fo ? k_classify<false, true> : k_classify<false, false>);
+    auto kr = ar ? (fo ? k_run<true, true> : k_run<true, false>)
+                 : (fo ? k_run<false, true> : k_run<false, false>);
+    hipLaunchKernelGGL(kc, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, w, h->g0,
+                       h->stats, h->err);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(kr, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, w, h->g0,
+                       h->stats, h->err);
+  }
   HIP_TRY(hipGetLastError());
   if (h->timing) {
     HIP_TRY(hipEventRecord(h->ev[h->ev_used + 1], st));
@@ -552,6 +758,15 @@ int tg_errors(tg_batch* h, uint32_t* out, void* stream) {
   return TG_OK;
 }
 
+int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
+  BIND(h);
+  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT)
+    return fail(TG_E_INVAL, "tg_set_mode: unknown mode %d", mode);
+  h->mode = mode;
+  (void)run_blocks;  // reserved
+  return TG_OK;
+}
+
 int tg_set_timing(tg_batch* h, int enable) {
   BIND(h);
   h->timing = enable != 0;
@@ -564,8 +779,13 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   HIP_TRY(hipDeviceSynchronize());
   int rc = flush_timing(h);
   if (rc) return rc;
-  unsigned long long s[ST_COUNT];
-  HIP_TRY(hipMemcpy(s, h->stats, sizeof s, hipMemcpyDeviceToHost));
+  const size_t nb = (size_t)grid_for(h->n);
+  std::vector<unsigned long long> part(nb * ST_COUNT);
+  HIP_TRY(hipMemcpy(part.data(), h->stats, sizeof(unsigned long long) * part.size(),
+                    hipMemcpyDeviceToHost));
+  unsigned long long s[ST_COUNT] = {};
+  for (size_t b = 0; b < nb; ++b)
+    for (int k = 0; k < ST_COUNT; ++k) s[k] += part[b * ST_COUNT + k];
   out->steps = (int64_t)s[ST_STEPS];
   out->valid_steps = (int64_t)s[ST_VALID];
   out->ticks = (int64_t)s[ST_TICKS];
@@ -580,7 +800,7 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
 int tg_stats_reset(tg_batch* h) {
   BIND(h);
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT));
+  HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)grid_for(h->n)));
   h->ev_used = 0;
   h->kernel_ms_done = 0.0;
   return TG_OK;

@@ -85,33 +85,69 @@ TG_HD int floordiv(int a, int b) {  // Python // for b > 0
 //   mt[p-227] (already new), and mt[0] (new) for p = 623.  Generating word p in place right
 //   before it is consumed therefore produces the identical stream: positions < p are new,
 //   positions >= p old.  A freshly seeded state (CPython index = 624) is position 0.
-//   No 624-iteration loop, hence no wavefront divergence on the twist.
+//   No 624-iteration loop, hence no wavefront divergence on the twist.  Words are consumed in
+//   pairs (random() is the only consumer), so the position is always even and each draw is
+//   one aligned 8-byte store plus three prefetched loads for the next draw.
 // ==========================================================================================
 struct Rng {
-  uint32_t* mt;   // this env's 624 words (HBM on device)
-  uint32_t pos;
+  uint32_t* mt;    // this env's 624 words (HBM on device)
+  uint32_t pos;    // always even: random() is the only consumer and takes words in pairs
   uint32_t draws;  // random() calls (instrumentation for the roofline)
+  // register cache, filled on first use and refreshed one draw ahead (prefetch):
+  //   p0 = mt[pos], mt[pos+1]; p1 = mt[pos+2], mt[pos+3] (mod 624);
+  //   c0, c1 = the partners mt[pos+397 | pos-227] of words pos, pos+1
+  uint2 p0, p1;
+  uint32_t c0, c1;
+  bool primed;
 
-  TG_HD uint32_t next_u32() {
-    const uint32_t p = pos;
-    const uint32_t p1 = (p == MT_N - 1) ? 0u : p + 1;
-    const uint32_t pm = (p < MT_N - MT_M) ? p + MT_M : p - (MT_N - MT_M);
-    const uint32_t a = mt[p], b = mt[p1], c = mt[pm];
-    const uint32_t y0 = (a & 0x80000000u) | (b & 0x7fffffffu);
-    uint32_t y = c ^ (y0 >> 1) ^ ((y0 & 1u) ? 0x9908b0dfu : 0u);
-    mt[p] = y;
-    pos = p1;
+  TG_HD Rng(uint32_t* m, uint32_t p) : mt(m), pos(p), draws(0u), p0{}, p1{}, c0(0u), c1(0u),
+                                        primed(false) {}
+
+  static TG_HD uint32_t partner(uint32_t q) { return q < MT_N - MT_M ? q + MT_M : q - (MT_N - MT_M); }
+  static TG_HD uint32_t twist(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+  static TG_HD uint32_t temper(uint32_t y) {
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
     return y;
   }
-  // random_random (53-bit): exact in double, FMA-safe
+  TG_HD void fetch_ahead() {  // inputs of the draw at `pos` (p0 already in registers)
+    const uint32_t q = (pos + 2 == MT_N) ? 0u : pos + 2;
+    p1 = *reinterpret_cast<const uint2*>(mt + q);
+    c0 = mt[partner(pos)];
+    c1 = mt[partner(pos + 1)];
+  }
+  TG_HD void prime() {
+    p0 = *reinterpret_cast<const uint2*>(mt + pos);
+    fetch_ahead();
+    primed = true;
+  }
+  // genrand_uint32 twice + random_random (53-bit), exact in double (FMA-safe).  Words pos and
+  // pos+1 of the next generation are twisted in place (lazy twist): word 623's successor is
+  // the already-new mt[0], which is exactly what p1 holds when pos = 622.
   TG_HD double random() {
-    const uint32_t a = next_u32() >> 5;
-    const uint32_t b = next_u32() >> 6;
+#ifdef TG_DIAG_NORNG
+    // DIAGNOSTIC BUILD ONLY (scripts/diag_ablation.py): words from a register hash instead
+    // of the MT state, to price the MT memory traffic.  Never part of the product library.
+    uint32_t z = (pos * 0x9E3779B9u) ^ (uint32_t)(uintptr_t)mt;
+    pos = (pos + 2 == MT_N) ? 0u : pos + 2;
+    z ^= z >> 16; z *= 0x85EBCA6Bu; z ^= z >> 13; z *= 0xC2B2AE35u; z ^= z >> 16;
     ++draws;
+    return (double)(z >> 5) * (1.0 / 134217728.0);
+#endif
+    if (!primed) prime();
+    const uint32_t w0 = twist(p0.x, p0.y, c0);
+    const uint32_t w1 = twist(p0.y, p1.x, c1);
+    *reinterpret_cast<uint2*>(mt + pos) = make_uint2(w0, w1);
+    pos = (pos + 2 == MT_N) ? 0u : pos + 2;
+    p0 = p1;
+    fetch_ahead();
+    ++draws;
+    const uint32_t a = temper(w0) >> 5, b = temper(w1) >> 6;
     return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
   }
   // Random.uniform = a + (b-a)*random(); built with -ffp-contract=off (no FMA)
@@ -597,25 +633,29 @@ struct StepResult {
   int done;    // got gold and back in row 0
   int ticks;
 };
+// the while-not-done loop of _Option.run (OP/:28-31) for an option whose can_run held
+TG_HD void run_option(const Level& L, const Map& m, Env& e, int k, Rng& rng, StepResult& r) {
+  r.ran = 1;
+  Opt o{k, 0, false, false};
+  do {
+    const int prim = policy(L, m, e, o);
+    r.reward += tick(L, m, e, prim, rng);
+    if (++r.ticks >= TICK_CAP) {
+      e.f |= E_TICKCAP;
+      break;
+    }
+  } while (!o.done);
+}
+// option_list[a] (TG/:92): -1 for an out-of-range action (the reference raises IndexError)
+TG_HD int option_index(int a) {
+  if (a < -O_COUNT || a >= O_COUNT) return -1;
+  return a < 0 ? a + O_COUNT : a;  // Python negative indexing
+}
 TG_HD StepResult env_step(const Level& L, const Map& m, Env& e, int a, Rng& rng) {
   StepResult r{0, 0, 0, 0};
-  if (a < -O_COUNT || a >= O_COUNT) {
-    e.f |= E_ACTION;  // option_list[a] raises IndexError in the reference (TG/:92)
-  } else {
-    if (a < 0) a += O_COUNT;  // Python negative indexing
-    if (can_run(L, m, e, a)) {
-      r.ran = 1;
-      Opt o{a, 0, false, false};
-      do {
-        const int prim = policy(L, m, e, o);
-        r.reward += tick(L, m, e, prim, rng);
-        if (++r.ticks >= TICK_CAP) {
-          e.f |= E_TICKCAP;
-          break;
-        }
-      } while (!o.done);
-    }
-  }
+  const int k = option_index(a);
+  if (k < 0) e.f |= E_ACTION;
+  else if (can_run(L, m, e, k)) run_option(L, m, e, k, rng, r);  // OP/:22-23 gate
   r.done = is_done(e);
   return r;
 }

@@ -103,7 +103,7 @@ class TreasureGameVec:
     """
 
     def __init__(self, num_envs, seed=0, device=None, global_offset=0, autoreset=False,
-                 level_dir=None, copy=False):
+                 level_dir=None, copy=False, mode="compact"):
         if not torch.cuda.is_available():
             raise TgError("TreasureGameVec needs a ROCm GPU (gfx950); there is no CPU path")
         self._L = _lib.load()
@@ -132,6 +132,8 @@ class TreasureGameVec:
         self.action_space = Discrete(_lib.NUM_ACTIONS)
         self.observation_space = Box(np.float32(0.0), np.float32(1.0), shape=(_lib.OBS_DIM,))
         self.option_names = list(OPTION_NAMES)
+        if mode != "compact":
+            self.set_mode(mode)
 
     # -- plumbing ---------------------------------------------------------------------------
     def _stream(self):
@@ -231,6 +233,12 @@ class TreasureGameVec:
         v = ctypes.c_uint32(0)
         check(self._L.tg_errors(self.handle, ctypes.byref(v), self._stream()), "tg_errors")
         return int(v.value)
+
+    def set_mode(self, mode="compact", run_blocks=0):
+        """Step implementation: "compact" (two-pass, default) or "direct" (one lane per env
+        runs in place); both are bit-identical."""
+        m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT}[mode]
+        check(self._L.tg_set_mode(self.handle, m, int(run_blocks)), "tg_set_mode")
 
     def set_timing(self, enable=True):
         check(self._L.tg_set_timing(self.handle, int(bool(enable))), "tg_set_timing")

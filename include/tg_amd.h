@@ -123,7 +123,17 @@ int tg_episodes(tg_batch *h, tg_episode *out, int32_t *count, int32_t cap, void 
 /* OR of all per-env error bits (host, synchronises the handle's stream). */
 int tg_errors(tg_batch *h, uint32_t *or_of_flags, void *stream);
 
-/* Enable HIP-event timing of every step-kernel launch (adds two event records per step). */
+/* Step implementation (both bit-identical):
+ *   TG_MODE_COMPACT (default): k_classify finishes envs whose option cannot run and appends
+ *     the rest to per-option worklists; k_run's waves run them in 64-env chunks,
+ *     longest-option-first (run_blocks is reserved, pass 0).
+ *   TG_MODE_DIRECT: one k_step lane per env runs its option in place. */
+#define TG_MODE_DIRECT 0
+#define TG_MODE_COMPACT 1
+int tg_set_mode(tg_batch *h, int mode, int run_blocks);
+
+/* Enable HIP-event timing of every tg_step (adds two event records per step; the measured
+ * interval covers all of the step's kernels). */
 int tg_set_timing(tg_batch *h, int enable);
 /* Counters (host, synchronises). */
 int tg_get_stats(tg_batch *h, tg_stats *out);

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""A/B timing of step variants on one GPU (diagnostics; not the bench).
+
+Builds (if needed) and times, per variant, ms per batched step at 1,048,576 envs with the
+bench's workload: the product library in both step modes, and a DIAGNOSTIC build
+(-DTG_DIAG_NORNG: MT words from a register hash, no MT memory traffic; results are NOT
+reference-exact) to price the RNG's memory traffic.  Interleaved, best of 3 rounds.
+"""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import gym_treasure_game_amd as tg  # noqa: E402
+from gym_treasure_game_amd import _lib  # noqa: E402
+
+DIAG = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_diag.so")
+
+
+def build_diag():
+    src = os.path.join(ROOT, "gym-treasure-game_amd", "csrc", "tg_amd.hip")
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                           "-ffp-contract=off", "-fPIC", "-shared", "-DTG_DIAG_NORNG", "-o", DIAG,
+                           src])
+
+
+def time_variant(lib_path, mode, n, steps, warmup):
+    _lib._lib = None
+    _lib.LIB_PATH = lib_path
+    vec = tg.TreasureGameVec(n, seed=0, mode=mode)
+    vec.reset()
+    for t in range(warmup):
+        vec.step(vec.policy_actions(t))
+    torch.cuda.synchronize()
+    vec.stats_reset()
+    vec.set_timing(True)
+    t0 = time.perf_counter()
+    for t in range(warmup, warmup + steps):
+        vec.step(vec.policy_actions(t))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = vec.stats()
+    vec.close()
+    return {"ms_step": dt / steps * 1e3, "kernel_ms": st["kernel_ms"] / steps,
+            "ticks": st["ticks"] / steps}
+
+
+def main():
+    n = int(os.environ.get("N", 1 << 20))
+    steps, warmup = 60, 10
+    if not os.path.exists(DIAG):
+        build_diag()
+    prod = _lib.LIB_PATH
+    variants = [("prod", prod, "compact"), ("prod", prod, "direct"), ("norng", DIAG, "compact"),
+                ("norng", DIAG, "direct")]
+    best = {}
+    for _ in range(3):
+        for name, path, mode in variants:
+            r = time_variant(path, mode, n, steps, warmup)
+            k = "%s/%s" % (name, mode)
+            if k not in best or r["kernel_ms"] < best[k]["kernel_ms"]:
+                best[k] = r
+    _lib._lib = None
+    _lib.LIB_PATH = prod
+    print(json.dumps(best, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -65,7 +65,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
     const uint64_t g = (uint64_t)(g0 + i);
     seed_mt(mt.data(), gen, seed_base + g);
     Env e{};
-    Rng rng{mt.data(), 0u, 0u};
+    Rng rng(mt.data(), 0u);
     reset_env(*L, e, rng);
     reset_env(*L, e, rng);
     double o[9], fo[9];

@@ -29,12 +29,15 @@ def rec_hash(h, obs, rew, valid, done):
     return sm64(h ^ w)
 
 
+MODES = ["compact", "direct"]
+
+
 def run_gpu(tg, seed_base, g0, n, steps, a0, policy, autoreset, rows=None, hash_only=False,
-            drain_every=0):
+            drain_every=0, mode="compact"):
     """Drive a TreasureGameVec like tgo_run drives the oracle; returns env-major arrays.
     drain_every > 0 collects the auto-reset episode records every that many steps."""
     pol = "masked" if policy else "uniform"
-    vec = tg.TreasureGameVec(n, seed=seed_base, global_offset=g0, autoreset=autoreset)
+    vec = tg.TreasureGameVec(n, seed=seed_base, global_offset=g0, autoreset=autoreset, mode=mode)
     idx = None if rows is None else torch.as_tensor(rows, device=vec.device)
     pick = (lambda t: t) if idx is None else (lambda t: t.index_select(0, idx))
     obs0 = pick(vec.reset()).cpu().numpy()
@@ -83,13 +86,15 @@ def assert_bits(a, b, what):
     assert len(bad) == 0, "%s differs first at %s (%d cells)" % (what, bad[0].tolist(), len(bad))
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("name,policy,autoreset", [("traj_uniform.npz", 0, False),
                                                    ("traj_masked.npz", 1, False),
                                                    ("traj_autoreset.npz", 1, True)])
-def test_golden_trajectories(tg, name, policy, autoreset):
+def test_golden_trajectories(tg, name, policy, autoreset, mode):
     d = golden(name)
     n, t1 = d["valid"].shape
-    o = run_gpu(tg, int(d["seed_base"]), 0, n, t1 - 1, int(d["action_seed"]), policy, autoreset)
+    o = run_gpu(tg, int(d["seed_base"]), 0, n, t1 - 1, int(d["action_seed"]), policy, autoreset,
+                mode=mode)
     for k in ("obs", "final_obs", "reward", "valid", "done"):
         assert_bits(o[k], d[k], k)
     st = o["stats"]
@@ -97,12 +102,13 @@ def test_golden_trajectories(tg, name, policy, autoreset):
     assert o["errors"] == 0
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("name,policy", [("hash_uniform.npz", 0), ("hash_masked.npz", 1)])
-def test_golden_hashes(tg, name, policy):
+def test_golden_hashes(tg, name, policy, mode):
     """4,096 envs x 1,000 uniform steps (config C2) and 1,024 x 600 masked, vs the reference."""
     d = golden(name)
     o = run_gpu(tg, 0, 0, len(d["hash"]), int(d["steps"]), int(d["action_seed"]), policy, False,
-                hash_only=True)
+                hash_only=True, mode=mode)
     np.testing.assert_array_equal(o["hash"], d["hash"])
     st = o["stats"]
     assert st["draws"] == int((d["draws"] - 8).sum())
@@ -111,7 +117,8 @@ def test_golden_hashes(tg, name, policy):
     assert st["steps"] == len(d["hash"]) * int(d["steps"])
 
 
-def test_full_size_sampled_vs_oracle(tg, oracle):
+@pytest.mark.parametrize("mode", MODES)
+def test_full_size_sampled_vs_oracle(tg, oracle, mode):
     """1,048,576 envs (config C3) with auto-reset: 8 blocks of 256 envs spread over the batch
     replayed exactly by the oracle (every env is independent and seeded by its global index)."""
     n, steps, a0 = 1 << 20, 40, 0xC3
@@ -119,7 +126,7 @@ def test_full_size_sampled_vs_oracle(tg, oracle):
     starts = np.sort(rng.choice(np.arange(0, n - 256, 256), 8, replace=False))
     starts[0], starts[-1] = 0, n - 256
     rows = np.concatenate([np.arange(s, s + 256) for s in starts])
-    o = run_gpu(tg, 11, 0, n, steps, a0, 0, True, rows=rows)
+    o = run_gpu(tg, 11, 0, n, steps, a0, 0, True, rows=rows, mode=mode)
     for bi, s in enumerate(starts):
         r = oracle.run(11, int(s), 256, steps, a0, 0, True)
         sl = slice(bi * 256, (bi + 1) * 256)
@@ -129,10 +136,11 @@ def test_full_size_sampled_vs_oracle(tg, oracle):
     assert o["errors"] == 0
 
 
-def test_masked_autoreset_long_vs_oracle(tg, oracle):
+@pytest.mark.parametrize("mode", MODES)
+def test_masked_autoreset_long_vs_oracle(tg, oracle, mode):
     """Many episodes: masked policy, auto-reset, 3,000 steps; episode records == oracle's."""
     n, steps, a0 = 512, 3000, 0x77
-    o = run_gpu(tg, 0, 10**6, n, steps, a0, 1, True, hash_only=True, drain_every=250)
+    o = run_gpu(tg, 0, 10**6, n, steps, a0, 1, True, hash_only=True, drain_every=250, mode=mode)
     r = oracle.run(0, 10**6, n, steps, a0, 1, True)
     np.testing.assert_array_equal(o["hash"], r["hash"])
     # the episodes the kernel compacted with its ballots == the oracle's (env, return, length)
@@ -216,8 +224,9 @@ def test_step_before_reset_is_the_constructed_state(tg):
     assert not torch.equal(o1, o2)
 
 
-def test_bad_action_flags_error(tg):
-    vec = tg.TreasureGameVec(128, seed=0)
+@pytest.mark.parametrize("mode", MODES)
+def test_bad_action_flags_error(tg, mode):
+    vec = tg.TreasureGameVec(128, seed=0, mode=mode)
     vec.reset()
     a = torch.zeros(128, dtype=torch.int32, device=vec.device)
     a[17] = 42
@@ -243,3 +252,21 @@ def test_reset_mask(tg, oracle):
             e.step(oracle.pick_action(1, g, t, True, e.mask()))
         np.testing.assert_array_equal(after[g].cpu().numpy().view(np.uint64),
                                       e.reset().view(np.uint64))
+
+
+def test_modes_identical_full_outputs(tg):
+    """compact and direct modes write identical rows for every env, incl. invalid steps."""
+    n = 1 << 16
+    outs = []
+    for mode in MODES:
+        vec = tg.TreasureGameVec(n, seed=2, autoreset=True, mode=mode)
+        vec.reset()
+        acc = []
+        for t in range(30):
+            o, r, v, d, info = vec.step(vec.policy_actions(t, 0x44, "uniform"))
+            acc.append(torch.cat([o.view(torch.int64).flatten(), r.to(torch.int64), v.to(torch.int64),
+                                  d.to(torch.int64), info["final_obs"].view(torch.int64).flatten()]).cpu())
+        outs.append((torch.stack(acc), vec.stats()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for k in ("steps", "valid_steps", "ticks", "draws", "episodes"):
+        assert outs[0][1][k] == outs[1][1][k], k
