@@ -16,7 +16,7 @@ DEPS = [SRC, os.path.join(HERE, "csrc", "tg_core.h"), os.path.join(HERE, "csrc",
 OUT = os.path.join(HERE, "libtg_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-         "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
+         "-fPIC", "-shared", "-Wall", "-Wno-unused-function", "-Wno-bitwise-instead-of-logical"]
 
 
 def needs_build():

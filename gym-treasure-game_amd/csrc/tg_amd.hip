@@ -81,10 +81,25 @@ struct Soa {
   uint32_t* mt;
 };
 
-__device__ __forceinline__ void stage_grid(uint8_t* lds, const uint8_t* grid, int ncell) {
-  for (int i = threadIdx.x; i < ncell; i += BLOCK) lds[i] = grid[i];
+// The level in LDS: the bordered cell grid (per-lane indexed probes) and the trigger table
+// (indexed per lane by the cascade; kernel arguments indexed per lane would be vector loads
+// from the kernarg segment).
+struct LdsLevel {
+  uint32_t trig[12];
+  uint32_t grid[MAX_CELLS / 4];
+};
+__device__ __forceinline__ void stage_level(LdsLevel& lv, const uint32_t* __restrict__ grid,
+                                            const Level& L) {
+  const int nwords = ((L.W + 2 * PAD) * (L.H + 2 * PAD) + 3) / 4;
+  for (int i = threadIdx.x; i < nwords; i += BLOCK) lv.grid[i] = grid[i];
+  if (threadIdx.x < 12) lv.trig[threadIdx.x] = L.trig[threadIdx.x >> 1][threadIdx.x & 1];
   __syncthreads();
 }
+#define LEVEL_IN_LDS()                   \
+  __shared__ LdsLevel lv;                \
+  stage_level(lv, grid, L);              \
+  const uint32_t* const trig = lv.trig;  \
+  const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H}
 
 __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o[9]) {
   double* p = out + i * 9;
@@ -116,7 +131,7 @@ __global__ __launch_bounds__(BLOCK) void k_create(Soa S, int64_t n, Level L, uin
   e.f = 0;
   Rng rng(mt, 0u);
   reset_env(L, e, rng);
-  e.mti = rng.pos;
+  e.mti = rng.finish();
   S.st4[i] = pack(e);
   S.ang[i] = make_double2(e.ang0, e.ang1);
   S.ep[i] = make_int2(0, 0);
@@ -132,7 +147,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
   if (!mask || mask[i]) {
     Rng rng(S.mt + i * MT_N, e.mti);
     reset_env(L, e, rng);
-    e.mti = rng.pos;
+    e.mti = rng.finish();
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
     S.ep[i] = make_int2(0, 0);
@@ -230,13 +245,11 @@ __device__ __forceinline__ void finish_step(const Level& L, Env& e, Rng& rng, in
 // ---- one-pass step: one lane per env, the option runs in place (TG_MODE_DIRECT) ----------
 template <bool AUTORESET, bool FINAL>
 __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
-                                                 const uint8_t* __restrict__ grid, StepIO io,
+                                                 const uint32_t* __restrict__ grid, StepIO io,
                                                  EpQueue q, int64_t g0,
                                                  unsigned long long* __restrict__ stats,
                                                  uint32_t* __restrict__ err_or) {
-  __shared__ uint8_t lgrid[MAX_CELLS];
-  stage_grid(lgrid, grid, L.W * L.H);
-  const Map m{lgrid, L.W, L.H};
+  LEVEL_IN_LDS();
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
   StepResult r{0, 0, 0, 0};
@@ -247,9 +260,9 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
     Rng rng(S.mt + i * MT_N, e.mti);
-    r = env_step(L, m, e, io.actions[i], rng);
+    r = env_step(L, trig, m, e, io.actions[i], rng);
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
-    e.mti = rng.pos;
+    e.mti = rng.finish();
     draws = rng.draws;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
@@ -288,15 +301,14 @@ __constant__ int kOrder[O_COUNT] = {O_GO_LEFT,   O_GO_RIGHT,   O_JUMP_LEFT,   O_
 
 template <bool AUTORESET, bool FINAL>
 __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
-                                                     const uint8_t* __restrict__ grid,
+                                                     const uint32_t* __restrict__ grid,
                                                      StepIO io, EpQueue q, Work w, int64_t g0,
                                                      unsigned long long* __restrict__ stats,
                                                      uint32_t* __restrict__ err_or) {
-  __shared__ uint8_t lgrid[MAX_CELLS];
   __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
   if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
-  stage_grid(lgrid, grid, L.W * L.H);  // includes the barrier
-  const Map m{lgrid, L.W, L.H};
+  LEVEL_IN_LDS();  // includes the barrier
+  (void)trig;
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
   const int lane = threadIdx.x & 63;
@@ -344,7 +356,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     Rng rng(S.mt + i * MT_N, e.mti);
     StepResult r{0, 0, (int)dn, 0};
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
-    e.mti = rng.pos;
+    e.mti = rng.finish();
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, q, stats);
@@ -359,48 +371,71 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   block_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, AUTORESET ? (live && !runs && dn) : 0);
 }
 
+#ifdef TG_DIAG_STAMPS
+// DIAGNOSTIC BUILD ONLY (scripts/diag_stamps.py): per-wave s_memtime stamps of k_run
+__device__ unsigned long long g_stamps[(1 << 16) * 4];
+#define TG_STAMP(v) v = __builtin_amdgcn_s_memtime()
+#else
+#define TG_STAMP(v) (void)0
+#endif
+
 template <bool AUTORESET, bool FINAL>
 __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
-                                                const uint8_t* __restrict__ grid, StepIO io,
+                                                const uint32_t* __restrict__ grid, StepIO io,
                                                 EpQueue q, Work w, int64_t g0,
                                                 unsigned long long* __restrict__ stats,
                                                 uint32_t* __restrict__ err_or) {
-  __shared__ uint8_t lgrid[MAX_CELLS];
-  __shared__ int pre[NSEG + 1];  // exclusive prefix of the segments in run order
+  // segments padded to whole chunks so that every wave holds ONE option (wave-uniform k
+  // selects a loop specialised to that option's primitive actions)
+  __shared__ int pre[NSEG + 1];  // exclusive prefix of the padded segments in run order
   if (threadIdx.x == 0) {
     int acc = 0;
     for (int b = 0; b < O_COUNT; ++b)
       for (int sh = 0; sh < SHARDS; ++sh) {
         pre[b * SHARDS + sh] = acc;
-        acc += w.ctr[(kOrder[b] * SHARDS + sh) * CTR_STRIDE];
+        acc += (w.ctr[(kOrder[b] * SHARDS + sh) * CTR_STRIDE] + 63) & ~63;
       }
     pre[NSEG] = acc;
   }
-  stage_grid(lgrid, grid, L.W * L.H);  // includes the barrier
+  LEVEL_IN_LDS();  // includes the barrier
   const int total = pre[NSEG];
-  const int j = blockIdx.x * BLOCK + threadIdx.x;  // wave w runs chunk w
-  const Map m{lgrid, L.W, L.H};
-  const bool live = j < total;
+  const int base = (blockIdx.x * BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
+  int seg = 0;  // pre[seg] <= base < pre[seg + 1] (wave-uniform)
+  if (base < total) {
+    int lo = 0, hi = NSEG;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pre[mid] <= base) lo = mid; else hi = mid;
+    }
+    seg = lo;
+  }
+  seg = __builtin_amdgcn_readfirstlane(seg);
+  const int k = kOrder[seg / SHARDS], sh = seg % SHARDS;
+  const int idx = base + (threadIdx.x & 63) - pre[seg];
+  const bool live = base < total && idx < w.ctr[(k * SHARDS + sh) * CTR_STRIDE];
   int64_t i = 0;
   StepResult r{0, 0, 0, 0};
   Env e;
   int2 ep = make_int2(0, 0);
   uint32_t draws = 0;
+  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  TG_STAMP(t0);
+  (void)t0; (void)t1; (void)t2; (void)t3;
   if (live) {
-    int lo = 0, hi = NSEG;  // segment: pre[lo] <= j < pre[lo + 1]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (pre[mid] <= j) lo = mid; else hi = mid;
-    }
-    const int k = kOrder[lo / SHARDS], sh = lo % SHARDS;
-    i = w.lists[(int64_t)(k * SHARDS + sh) * w.shard_cap + (j - pre[lo])];
+    i = w.lists[(int64_t)(k * SHARDS + sh) * w.shard_cap + idx];
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
     Rng rng(S.mt + i * MT_N, e.mti);
-    run_option(L, m, e, k, rng, r);
+    rng.prime();  // issue the window loads now; the first draw comes after the policy setup
+#ifdef TG_DIAG_STAMPS
+    (void)*(volatile uint32_t*)&rng.c0.x;
+#endif
+    TG_STAMP(t1);
+    run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform: one specialised loop
+    TG_STAMP(t2);
     r.done = is_done(e);
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
-    e.mti = rng.pos;
+    e.mti = rng.finish();
     draws = rng.draws;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
@@ -411,16 +446,34 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     S.ep[i] = ep;
   }
   block_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0);
+#ifdef TG_DIAG_STAMPS
+  TG_STAMP(t3);
+  {
+    int mx = r.ticks;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+    const int sum = wave_sum(r.ticks);
+    const unsigned long long bl = __ballot(live);
+    const int src = bl ? __ffsll((long long)bl) - 1 : 0;
+    const unsigned long long a1 = __shfl(t1, src, 64);
+    const unsigned long long a2 = __shfl(t2, src, 64);
+    const int wv = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0 && bl && wv < (1 << 16)) {
+      g_stamps[wv * 4 + 0] = a1 - t0;
+      g_stamps[wv * 4 + 1] = a2 - a1;
+      g_stamps[wv * 4 + 2] = t3 - a2;
+      g_stamps[wv * 4 + 3] = (unsigned long long)mx | ((unsigned long long)sum << 32);
+    }
+  }
+#endif
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
-                                                 const uint8_t* __restrict__ grid,
+                                                 const uint32_t* __restrict__ grid,
                                                  uint16_t* __restrict__ out) {
-  __shared__ uint8_t lgrid[MAX_CELLS];
-  stage_grid(lgrid, grid, L.W * L.H);
+  LEVEL_IN_LDS();
+  (void)trig;
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
-  const Map m{lgrid, L.W, L.H};
   Env e;
   unpack(S.st4[i], S.ang[i], e);
   out[i] = (uint16_t)available_mask(L, m, e);
@@ -446,17 +499,17 @@ __device__ __forceinline__ uint64_t sm64(uint64_t x) {
 
 // a[t, g] = h(a0, g, t) % 9, or the k-th set bit of available_mask (masked-uniform)
 __global__ __launch_bounds__(BLOCK) void k_actions(Soa S, int64_t n, Level L,
-                                                    const uint8_t* __restrict__ grid,
+                                                    const uint32_t* __restrict__ grid,
                                                     uint64_t a0, int64_t g0, int64_t t,
                                                     int policy, int32_t* __restrict__ out) {
-  __shared__ uint8_t lgrid[MAX_CELLS];
-  if (policy == TG_POLICY_MASKED) stage_grid(lgrid, grid, L.W * L.H);
+  __shared__ LdsLevel lv;
+  if (policy == TG_POLICY_MASKED) stage_level(lv, grid, L);  // uniform branch
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
   const uint64_t h = sm64(sm64(a0 ^ sm64((uint64_t)(g0 + i))) ^ (uint64_t)t);
   int a = (int)(h % 9ull);
   if (policy == TG_POLICY_MASKED) {
-    const Map m{lgrid, L.W, L.H};
+    const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
     Env e;
     unpack(S.st4[i], S.ang[i], e);
     const uint32_t mk = available_mask(L, m, e);
@@ -515,7 +568,7 @@ struct tg_batch {
   int64_t g0 = 0;
   uint64_t seed0 = 0;
   Level L{};
-  uint8_t* grid = nullptr;
+  uint32_t* grid = nullptr;  // bordered cell grid, padded to whole words
   uint32_t* genrand = nullptr;
   Soa S{};
   tg_episode* eps = nullptr;
@@ -535,6 +588,10 @@ struct tg_batch {
 
 namespace {
 int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
+// k_run needs one wave per 64-lane chunk of the padded worklists: at most n/64 + NSEG chunks
+int run_grid_for(int64_t n) { return grid_for(n) + (NSEG * 64 + BLOCK - 1) / BLOCK; }
+// per-block launch-counter slots cover the largest step grid
+int stat_slots(int64_t n) { return run_grid_for(n); }
 
 int bind(const tg_batch* h) {
   int cur = -1;
@@ -611,6 +668,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
 #define ALLOC(ptr, bytes)                                                                   \
   if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess)                                    \
     return cleanup(fail(TG_E_NOMEM, "hipMalloc %zu B for " #ptr, (size_t)(bytes)));
+  grid.resize((grid.size() + 3) & ~(size_t)3, 0);
   ALLOC(h->grid, grid.size());
   ALLOC(h->genrand, sizeof gen);
   ALLOC(h->S.st4, sizeof(uint4) * n);
@@ -619,7 +677,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->S.mt, sizeof(uint32_t) * MT_N * (size_t)n);
   ALLOC(h->eps, sizeof(tg_episode) * (size_t)h->eps_cap);
   ALLOC(h->eps_count, sizeof(int32_t));
-  ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT * (size_t)grid_for(n));
+  ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n));
   ALLOC(h->err, sizeof(uint32_t));
   // a shard holds the envs of every SHARDS-th workgroup
   h->shard_cap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK;
@@ -629,7 +687,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
-      hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)grid_for(n)) != hipSuccess ||
+      hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)) != hipSuccess ||
       hipMemset(h->err, 0, sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail(TG_E_HIP, "tg_create: upload failed"));
   hipLaunchKernelGGL(k_create, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, h->L,
@@ -695,8 +753,8 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
     hipLaunchKernelGGL(kc, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, w, h->g0,
                        h->stats, h->err);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(kr, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, w, h->g0,
-                       h->stats, h->err);
+    hipLaunchKernelGGL(kr, dim3(run_grid_for(h->n)), block, 0, st, h->S, h->n, h->L, h->grid, io,
+                       q, w, h->g0, h->stats, h->err);
   }
   HIP_TRY(hipGetLastError());
   if (h->timing) {
@@ -779,7 +837,7 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   HIP_TRY(hipDeviceSynchronize());
   int rc = flush_timing(h);
   if (rc) return rc;
-  const size_t nb = (size_t)grid_for(h->n);
+  const size_t nb = (size_t)stat_slots(h->n);
   std::vector<unsigned long long> part(nb * ST_COUNT);
   HIP_TRY(hipMemcpy(part.data(), h->stats, sizeof(unsigned long long) * part.size(),
                     hipMemcpyDeviceToHost));
@@ -800,7 +858,7 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
 int tg_stats_reset(tg_batch* h) {
   BIND(h);
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)grid_for(h->n)));
+  HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(h->n)));
   h->ev_used = 0;
   h->kernel_ms_done = 0.0;
   return TG_OK;
@@ -834,5 +892,14 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
   if (mt) HIP_TRY(hipMemcpy(mt, h->S.mt, sizeof(uint32_t) * MT_N * (size_t)n, hipMemcpyDeviceToHost));
   return TG_OK;
 }
+
+#ifdef TG_DIAG_STAMPS
+int tg_diag_stamps(unsigned long long* out, int n_waves) {
+  if (n_waves > (1 << 16)) n_waves = 1 << 16;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * n_waves));
+  return TG_OK;
+}
+#endif
 
 }  // extern "C"

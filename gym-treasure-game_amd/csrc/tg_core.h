@@ -1,18 +1,21 @@
 // tg_core.h — per-env Treasure Game step physics for the MI355X kernel (gfx950).
 //
-// Everything here is `__host__ __device__` straight-line integer code operating on one env
-// held in registers.  tg_amd.hip wraps it in the batched kernels (one wavefront lane per env,
-// level grid in LDS, struct-of-arrays state in HBM).  The host instantiation exists only so
-// the test harness (tests/native/) can run the exact same code on the build machine, which
-// has no GPU; the product API never executes it on the CPU.
+// Everything here is `__host__ __device__` integer code operating on one env held in
+// registers.  tg_amd.hip wraps it in the batched kernels (one wavefront lane per env, level
+// grid in LDS, struct-of-arrays state in HBM).  The host instantiation exists only so the
+// test harness (tests/native/) can run the exact same code on the build machine, which has
+// no GPU; the product API never executes it on the CPU.
 //
 // Differences in FORM from the reference (not in results — parity is pinned by the oracle):
-//   * collision predicates (IM/:232-288) are evaluated on the 48x48-cell grid with at most 6
-//     cell lookups instead of up to 104 pixel probes: the reference pixel map is constant per
-//     cell (build_map IM/:204-216, door.update_map OB/:246-253) and OOB is WALL (IM/:218-225);
+//   * collision predicates (IM/:232-288) are evaluated on the 48x48-cell grid with a handful
+//     of branch-free cell lookups instead of up to 104 pixel probes: the reference pixel map
+//     is constant per cell (build_map IM/:204-216, door.update_map OB/:246-253) and OOB is
+//     WALL (IM/:218-225) — here a 2-cell WALL border around the grid plus clamping;
 //   * near_enough (OB/:46-53) is the exact integer test d^2 < r^2 (inputs are integers);
 //   * the trigger cascade (OB/:76-94) is an explicit 8-bit-frame stack in one u64 register;
-//   * MT19937 twists lazily, one word at the point of consumption (see Rng below).
+//   * MT19937 twists lazily, one word pair at the point of consumption (see Rng below);
+//   * each option's policy/tick loop is specialised at compile time to the primitive actions
+//     that option can issue (a wave runs one option in the compacted kernel).
 // Prefixes: TG/ treasure_game.py, IM/ _treasure_game_impl.py, OB/ _objects.py,
 // MO/ _move_options.py, OP/ _option.py under gym_treasure_game/envs/.
 #pragma once
@@ -27,11 +30,12 @@ constexpr int S = 48;          // xscale == yscale (_scale.py:8-9)
 constexpr int INCR = S / 10;   // x_incr / y_incr (IM/:46-47)
 constexpr int HALFW = S / 4;   // player_width // 2 (IM/:49)
 constexpr int MT_N = 624, MT_M = 397;
-constexpr int MAX_W = 64, MAX_H = 64;
 constexpr int TICK_CAP = 1 << 14;  // the reference has no cap (OP/:28-31); observed max 105
+constexpr int PAD = 2;             // WALL cells around the grid in LDS (probes reach <= 60 px out)
 
-// cell codes in the LDS grid; a door object's cell holds DOORSLOT+i and resolves per env
-enum : int { C_OPEN = 0, C_WALL = 1, C_LADDER = 2, C_DOOR = 3, C_OTHER = 4, C_DOORSLOT = 8 };
+// Cell bits in the LDS grid.  A door object's cell carries only its one-hot door bit: its type
+// is 'D' or ' ' by the door's state (update_map overwrites whatever the file had there).
+enum : uint32_t { B_OPEN = 1, B_LADDER = 2, B_WALL = 4, B_DOOR = 8, B_DOOROBJ = 16 /* << i */ };
 // primitive actions (_actions.py:7-13)
 enum : int { P_NOP = 0, P_UP, P_DOWN, P_LEFT, P_RIGHT, P_JUMP, P_INTERACT };
 // options in create_options order (IM/:495)
@@ -53,15 +57,15 @@ constexpr uint32_t E_NEARINT = 1u << 27;  // a reset's gauss landed within 1e-9 
                                           // boundary (device libm vs glibc watch)
 constexpr uint32_t E_MASK = 0xFF000000u;
 
-// ---- level (kernel argument; the grid itself is staged in LDS) ----------------------------
+// ---- level (kernel argument; the grid and the trigger table are staged in LDS) -------------
 struct Level {
-  int32_t W, H;            // cells (IM/:196-197)
+  int32_t W, H;              // cells (IM/:196-197)
   int32_t start_x, start_y;  // first non-WALL description cell (IM/:173-176)
   int8_t door_cx[3], door_cy[3];
   int8_t handle_cx[2], handle_cy[2];
   int8_t key_cx, key_cy, bolt_cx, bolt_cy, gold_cx, gold_cy;
-  uint32_t init_flags;     // door/handle/bolt initial booleans at their F_OBJ bits
-  uint32_t trig[6][2];     // trigger lists [object][polarity]: count(4b) + 7 x (target 3b, val 1b)
+  uint32_t init_flags;       // door/handle/bolt initial booleans at their F_OBJ bits
+  uint32_t trig[6][2];       // trigger lists [object][polarity]: count(4b) + 7 x (target 3b, val 1b)
 };
 
 // ---- per-env state (registers) -------------------------------------------------------------
@@ -70,13 +74,14 @@ struct Env {
   uint32_t f;            // flags above
   int kx, ky, gx, gy;    // key / goldcoin cell (OB/:34-38)
   double ang0, ang1;     // handle angles (OB/:111-114)
-  uint32_t mti;          // lazy-twist MT position (0..623)
+  uint32_t mti;          // lazy-twist MT position (0..622, even)
 };
 
 TG_HD int floordiv(int a, int b) {  // Python // for b > 0
   int q = a / b;
   return (a % b != 0 && a < 0) ? q - 1 : q;
 }
+TG_HD int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // ==========================================================================================
 // CPython random, lazily twisted.
@@ -86,24 +91,31 @@ TG_HD int floordiv(int a, int b) {  // Python // for b > 0
 //   before it is consumed therefore produces the identical stream: positions < p are new,
 //   positions >= p old.  A freshly seeded state (CPython index = 624) is position 0.
 //   No 624-iteration loop, hence no wavefront divergence on the twist.  Words are consumed in
-//   pairs (random() is the only consumer), so the position is always even and each draw is
-//   one aligned 8-byte store plus three prefetched loads for the next draw.
+//   pairs (random() is the only consumer), so the position is always even; see the register
+//   window below for how the words reach registers.
 // ==========================================================================================
 struct Rng {
-  uint32_t* mt;    // this env's 624 words (HBM on device)
+  uint32_t* mt;    // this env's 624 words (HBM on device), 16-B aligned
   uint32_t pos;    // always even: random() is the only consumer and takes words in pairs
   uint32_t draws;  // random() calls (instrumentation for the roofline)
-  // register cache, filled on first use and refreshed one draw ahead (prefetch):
-  //   p0 = mt[pos], mt[pos+1]; p1 = mt[pos+2], mt[pos+3] (mod 624);
-  //   c0, c1 = the partners mt[pos+397 | pos-227] of words pos, pos+1
-  uint2 p0, p1;
-  uint32_t c0, c1;
+  // Register window over three 16-B chunks of each stream, refilled two chunks (4 draws)
+  // ahead so the gathered loads' L2-miss latency hides behind the ticks in between:
+  //   c0, c1, c2 = mt[pos & ~3 .. +12)                   (the words being twisted)
+  //   d0, d1, d2 = mt[q & ~3 .. +12), q = (pos + 397) % 624  (partners: pos+397 | pos-227)
+  // 624 = 4 * 156 and 397 = 1 (mod 4), so both streams walk the same 156 chunks cyclically:
+  // a pair at pos = 0 (mod 4) uses c0.xy(+c0.z) and d0.yz, a pair at pos = 2 (mod 4) uses
+  // c0.zw(+c1.x) and d0.w, d1.x and then shifts both windows by a chunk.  Each draw costs
+  // half a 16-B load per stream and half a 16-B store.  finish() flushes a half-rewritten c0.
+  // Prefetched chunks hold old words: the twist only rewrites position pos, and the partner
+  // stream runs 397 words ahead (old) or 227 behind (new long ago).
+  uint4 c0, c1, c2, d0, d1, d2;
   bool primed;
 
-  TG_HD Rng(uint32_t* m, uint32_t p) : mt(m), pos(p), draws(0u), p0{}, p1{}, c0(0u), c1(0u),
-                                        primed(false) {}
+  TG_HD Rng(uint32_t* m, uint32_t p)
+      : mt(m), pos(p), draws(0u), c0{}, c1{}, c2{}, d0{}, d1{}, d2{}, primed(false) {}
 
-  static TG_HD uint32_t partner(uint32_t q) { return q < MT_N - MT_M ? q + MT_M : q - (MT_N - MT_M); }
+  static TG_HD uint32_t wrap(uint32_t q) { return q >= (uint32_t)MT_N ? q - MT_N : q; }
+  TG_HD uint4 chunk(uint32_t q) const { return *reinterpret_cast<const uint4*>(mt + q); }
   static TG_HD uint32_t twist(uint32_t a, uint32_t b, uint32_t c) {
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
     return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
@@ -115,20 +127,19 @@ struct Rng {
     y ^= (y >> 18);
     return y;
   }
-  TG_HD void fetch_ahead() {  // inputs of the draw at `pos` (p0 already in registers)
-    const uint32_t q = (pos + 2 == MT_N) ? 0u : pos + 2;
-    p1 = *reinterpret_cast<const uint2*>(mt + q);
-    c0 = mt[partner(pos)];
-    c1 = mt[partner(pos + 1)];
-  }
   TG_HD void prime() {
-    p0 = *reinterpret_cast<const uint2*>(mt + pos);
-    fetch_ahead();
+    const uint32_t cb = pos & ~3u, db = wrap(pos + MT_M) & ~3u;
+    c0 = chunk(cb);
+    c1 = chunk(wrap(cb + 4));
+    c2 = chunk(wrap(cb + 8));
+    d0 = chunk(db);
+    d1 = chunk(wrap(db + 4));
+    d2 = chunk(wrap(db + 8));
     primed = true;
   }
   // genrand_uint32 twice + random_random (53-bit), exact in double (FMA-safe).  Words pos and
   // pos+1 of the next generation are twisted in place (lazy twist): word 623's successor is
-  // the already-new mt[0], which is exactly what p1 holds when pos = 622.
+  // the already-new mt[0], which is what c1.x holds when pos = 622.
   TG_HD double random() {
 #ifdef TG_DIAG_NORNG
     // DIAGNOSTIC BUILD ONLY (scripts/diag_ablation.py): words from a register hash instead
@@ -140,18 +151,41 @@ struct Rng {
     return (double)(z >> 5) * (1.0 / 134217728.0);
 #endif
     if (!primed) prime();
-    const uint32_t w0 = twist(p0.x, p0.y, c0);
-    const uint32_t w1 = twist(p0.y, p1.x, c1);
-    *reinterpret_cast<uint2*>(mt + pos) = make_uint2(w0, w1);
-    pos = (pos + 2 == MT_N) ? 0u : pos + 2;
-    p0 = p1;
-    fetch_ahead();
+    uint32_t w0, w1;
+    if ((pos & 2u) == 0u) {
+      w0 = twist(c0.x, c0.y, d0.y);
+      w1 = twist(c0.y, c0.z, d0.z);
+      c0.x = w0;
+      c0.y = w1;
+      pos += 2;
+    } else {
+      w0 = twist(c0.z, c0.w, d0.w);
+      w1 = twist(c0.w, c1.x, d1.x);
+      c0.z = w0;
+      c0.w = w1;
+      *reinterpret_cast<uint4*>(mt + (pos & ~3u)) = c0;  // chunk fully rewritten
+      pos = wrap(pos + 2);
+      c0 = c1;
+      c1 = c2;
+      c2 = chunk(wrap(pos + 8));
+      d0 = d1;
+      d1 = d2;
+      d2 = chunk(wrap((wrap(pos + MT_M) & ~3u) + 8));
+    }
     ++draws;
     const uint32_t a = temper(w0) >> 5, b = temper(w1) >> 6;
     return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
   }
   // Random.uniform = a + (b-a)*random(); built with -ffp-contract=off (no FMA)
   TG_HD double uniform(double a, double b) { return a + (b - a) * random(); }
+  // write back a half-rewritten chunk; returns the position to store with the env
+  TG_HD uint32_t finish() {
+#ifndef TG_DIAG_NORNG
+    if (primed && (pos & 2u)) *reinterpret_cast<uint4*>(mt + (pos & ~3u)) = c0;
+#endif
+    primed = false;
+    return pos;
+  }
 };
 
 // init_by_array([seed lo, seed hi?]) into this env's words; position 0 (see above)
@@ -188,72 +222,84 @@ TG_HD void seed_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed)
 }
 
 // ==========================================================================================
-// Map probes
+// Map probes.  Every probe is a clamped index into the bordered grid plus one LDS byte read;
+// predicates combine probes with bitwise &/| so their LDS reads issue back to back.
 // ==========================================================================================
 struct Map {
-  const uint8_t* g;  // LDS on device
+  const uint8_t* g;  // LDS on device: (H + 2*PAD) rows of (W + 2*PAD) cells
   int W, H;
 
-  TG_HD int cell(uint32_t f, int cx, int cy) const {  // object_type_at_cell (IM/:227-230)
-    if ((unsigned)cx >= (unsigned)W || (unsigned)cy >= (unsigned)H) return C_WALL;
-    int c = g[cy * W + cx];
-    if (c & C_DOORSLOT) c = ((f >> (F_OBJ + (c & 7))) & 1u) ? C_DOOR : C_OPEN;
-    return c;
+  TG_HD int pw() const { return W + 2 * PAD; }
+  // object_type_at_cell (IM/:227-230) as cell bits; anything outside the grid is WALL
+  TG_HD uint32_t cellb(int cx, int cy) const {
+    cx = clampi(cx, -PAD, W + PAD - 1);
+    cy = clampi(cy, -PAD, H + PAD - 1);
+    return g[(cy + PAD) * pw() + cx + PAD];
   }
-  TG_HD int at(uint32_t f, int x, int y) const {  // object_type_at (IM/:218-225)
-    if (x < 0 || y < 0 || x >= W * S || y >= H * S) return C_WALL;
-    return cell(f, x / S, y / S);
+  // object_type_at (IM/:218-225) as cell bits
+  TG_HD uint32_t atb(int x, int y) const {
+    x = clampi(x, -PAD * S, (W + PAD) * S - 1) + PAD * S;
+    y = clampi(y, -PAD * S, (H + PAD) * S - 1) + PAD * S;
+    return g[(int)((unsigned)y / S) * pw() + (int)((unsigned)x / S)];
   }
+  // door state -> type: `dc` = closed-door bits (f >> F_OBJ) & 7
+  static TG_HD bool is_open(uint32_t c, uint32_t dc) {
+    return ((c & B_OPEN) | ((c >> 4) & ~dc & 7u)) != 0;
+  }
+  static TG_HD bool is_ladder(uint32_t c) { return (c & B_LADDER) != 0; }
+  static TG_HD bool is_wall(uint32_t c) { return (c & B_WALL) != 0; }
+  static TG_HD bool is_door(uint32_t c, uint32_t dc) {
+    return ((c & B_DOOR) | ((c >> 4) & dc)) != 0;
+  }
+  static TG_HD uint32_t dc_of(uint32_t f) { return (f >> F_OBJ) & 7u; }
 
-  // up_clear (IM/:232-238): xs {px-4, px, px+4} x ys [py-4, py-1] all OPEN
+  TG_HD bool open_at(uint32_t dc, int x, int y) const { return is_open(atb(x, y), dc); }
+  TG_HD bool open_cell(uint32_t dc, int cx, int cy) const { return is_open(cellb(cx, cy), dc); }
+
+  // up_clear (IM/:232-238): xs {px-4, px, px+4} x ys [py-4, py-1] all OPEN; the three xs
+  // span at most two columns and the four ys at most two rows
   TG_HD bool up_clear(const Env& e) const {
+    const uint32_t dc = dc_of(e.f);
     const int x0 = e.px - INCR, x1 = e.px + INCR, y0 = e.py - INCR, y1 = e.py - 1;
-    if (x0 < 0 || y0 < 0 || x1 >= W * S || y1 >= H * S) return false;
-    const int c0 = x0 / S, c1 = x1 / S, r0 = y0 / S, r1 = y1 / S;
-    return cell(e.f, c0, r0) == C_OPEN && cell(e.f, c1, r0) == C_OPEN &&
-           cell(e.f, c0, r1) == C_OPEN && cell(e.f, c1, r1) == C_OPEN;
+    return open_at(dc, x0, y0) & open_at(dc, x1, y0) & open_at(dc, x0, y1) & open_at(dc, x1, y1);
   }
   // can_go_up (IM/:240-250): ys {py-4, py, py+44} x xs {px-12, px+12}, any LADDER
   TG_HD bool can_go_up(const Env& e) const {
-    if (e.py <= 1) return false;
     const int xa = e.px - HALFW, xb = e.px + HALFW;
-    const int ys[3] = {e.py - INCR, e.py, e.py + S - INCR};
-    bool any = false;
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      any |= (int)(at(e.f, xa, ys[j]) == C_LADDER) | (int)(at(e.f, xb, ys[j]) == C_LADDER);
-    return any;
+    const int y0 = e.py - INCR, y1 = e.py, y2 = e.py + S - INCR;
+    const uint32_t any = atb(xa, y0) | atb(xb, y0) | atb(xa, y1) | atb(xb, y1) | atb(xa, y2) |
+                         atb(xb, y2);
+    return (e.py > 1) & is_ladder(any);
   }
-  // can_go_down (IM/:252-257): ys [py, py+51] x xs {px-12, px+12}, any LADDER
+  // can_go_down (IM/:252-257): ys [py, py+51] x xs {px-12, px+12}, any LADDER.  The 52 ys span
+  // at most three rows; rows outside the grid are WALL, so probing the clamped rows
+  // y, y+24, y+51 (every row of the span contains one of them) is exact.
   TG_HD bool can_go_down(const Env& e) const {
-    const int y0 = e.py < 0 ? 0 : e.py;
-    const int y1 = (e.py + S + INCR - 1 >= H * S) ? H * S - 1 : e.py + S + INCR - 1;
-    if (y0 > y1) return false;
-    const int r0 = y0 / S, r1 = y1 / S;  // r1 - r0 <= 2
-    bool any = false;
-    const int xs[2] = {e.px - HALFW, e.px + HALFW};
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int x = xs[i];
-      if (x < 0 || x >= W * S) continue;
-      const int c = x / S;
-      any |= cell(e.f, c, r0) == C_LADDER;
-      if (r0 + 1 <= r1) any |= cell(e.f, c, r0 + 1) == C_LADDER;
-      if (r0 + 2 <= r1) any |= cell(e.f, c, r0 + 2) == C_LADDER;
-    }
-    return any;
+    const int xa = e.px - HALFW, xb = e.px + HALFW;
+    const int y0 = e.py, y1 = e.py + S / 2, y2 = e.py + S + INCR - 1;
+    const uint32_t any = atb(xa, y0) | atb(xb, y0) | atb(xa, y1) | atb(xb, y1) | atb(xa, y2) |
+                         atb(xb, y2);
+    return is_ladder(any);
   }
   // can_go_left / can_go_right (IM/:259-281): x = px -/+ 16 at ys {py+4, py+44}
   TG_HD bool can_go_side(const Env& e, int dir) const {
+    const uint32_t dc = dc_of(e.f);
     const int x = e.px + dir * (HALFW + INCR);
-    const int ta = at(e.f, x, e.py + INCR), tb = at(e.f, x, e.py + S - INCR);
-    return !(ta == C_WALL || ta == C_DOOR || tb == C_WALL || tb == C_DOOR);
+    const uint32_t ta = atb(x, e.py + INCR), tb = atb(x, e.py + S - INCR);
+    return !(is_wall(ta | tb) | is_door(ta, dc) | is_door(tb, dc));
   }
   // can_fall (IM/:283-288): xs {px-10, px+10} x ys {py, py+50} all OPEN
-  TG_HD bool can_fall(const Env& e) const {
-    const int xa = e.px - HALFW + 2, xb = e.px + HALFW - 2, ya = e.py, yb = e.py + S + 2;
-    return at(e.f, xa, ya) == C_OPEN && at(e.f, xa, yb) == C_OPEN && at(e.f, xb, ya) == C_OPEN &&
-           at(e.f, xb, yb) == C_OPEN;
+  TG_HD bool can_fall_at(uint32_t dc, int px, int py) const {
+    const int xa = px - HALFW + 2, xb = px + HALFW - 2, ya = py, yb = py + S + 2;
+    return open_at(dc, xa, ya) & open_at(dc, xa, yb) & open_at(dc, xb, ya) & open_at(dc, xb, yb);
+  }
+  TG_HD bool can_fall(const Env& e) const { return can_fall_at(dc_of(e.f), e.px, e.py); }
+  // can_fall at (px, py + k) for k = 0..3 as bits 0..3, one batch of lookups
+  TG_HD uint32_t can_fall4(uint32_t dc, int px, int py) const {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r |= (uint32_t)can_fall_at(dc, px, py + k) << k;
+    return r;
   }
 };
 
@@ -301,13 +347,13 @@ TG_HD void drop_key(Env& e) {
 
 // is_object_at (IM/:402-409): handles, closed doors, bolt, gold, key at the cell
 TG_HD bool is_object_at(const Level& L, const Env& e, int xc, int yc) {
-  bool r = (xc == L.handle_cx[0] && yc == L.handle_cy[0]) |
-           (xc == L.handle_cx[1] && yc == L.handle_cy[1]) |
-           (xc == L.bolt_cx && yc == L.bolt_cy) | (xc == e.gx && yc == e.gy) |
-           (xc == e.kx && yc == e.ky);
+  bool r = ((xc == L.handle_cx[0]) & (yc == L.handle_cy[0])) |
+           ((xc == L.handle_cx[1]) & (yc == L.handle_cy[1])) |
+           ((xc == L.bolt_cx) & (yc == L.bolt_cy)) | ((xc == e.gx) & (yc == e.gy)) |
+           ((xc == e.kx) & (yc == e.ky));
 #pragma unroll
   for (int i = 0; i < 3; ++i)
-    r |= (xc == L.door_cx[i] && yc == L.door_cy[i] && ((e.f >> (F_OBJ + i)) & 1u));
+    r |= (xc == L.door_cx[i]) & (yc == L.door_cy[i]) & (((e.f >> (F_OBJ + i)) & 1u) != 0);
   return r;
 }
 // is_closed_door_at (IM/:411-416)
@@ -315,7 +361,7 @@ TG_HD bool is_closed_door_at(const Level& L, const Env& e, int xc, int yc) {
   bool r = false;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
-    r |= (xc == L.door_cx[i] && yc == L.door_cy[i] && ((e.f >> (F_OBJ + i)) & 1u));
+    r |= (xc == L.door_cx[i]) & (yc == L.door_cy[i]) & (((e.f >> (F_OBJ + i)) & 1u) != 0);
   return r;
 }
 
@@ -334,8 +380,9 @@ TG_HD bool set_val(Env& e, int o, int v, Rng& rng) {
   return true;
 }
 // set_val(o0, v0) followed by the process_trigger cascade (OB/:76-94), depth-first in file
-// order with the previously_triggered guard; frames are 8 bits of one u64.
-TG_HD void cascade(const Level& L, Env& e, int o0, int v0, Rng& rng) {
+// order with the previously_triggered guard; frames are 8 bits of one u64.  `trig` is the
+// level's [6][2] trigger table (LDS on device).
+TG_HD void cascade(const uint32_t* trig, Env& e, int o0, int v0, Rng& rng) {
   if (!set_val(e, o0, v0, rng)) return;
   uint64_t stack = (uint64_t)(o0 | (v0 << 3));
   uint32_t prev = 1u << o0;
@@ -343,7 +390,7 @@ TG_HD void cascade(const Level& L, Env& e, int o0, int v0, Rng& rng) {
   while (depth > 0) {
     const uint32_t fr = (uint32_t)(stack & 0xFFu);
     const int o = fr & 7, v = (fr >> 3) & 1, ei = fr >> 4;
-    const uint32_t list = L.trig[o][v];
+    const uint32_t list = trig[o * 2 + v];
     if (ei < (int)(list & 0xFu)) {
       stack += 0x10u;
       const uint32_t edge = (list >> (4 + 4 * ei)) & 0xFu;
@@ -361,48 +408,59 @@ TG_HD void cascade(const Level& L, Env& e, int o0, int v0, Rng& rng) {
   }
 }
 // handle.flip (OB/:117-122): uniform(0, 1) <= 0.8 (== random() exactly)
-TG_HD void flip(const Level& L, Env& e, int h, Rng& rng) {
+TG_HD void flip(const uint32_t* trig, Env& e, int h, Rng& rng) {
   if (rng.random() <= 0.8) {
     const int up = (e.f >> (F_OBJ + 3 + h)) & 1u;
-    cascade(L, e, 3 + h, !up, rng);
+    cascade(trig, e, 3 + h, !up, rng);
   } else {
     wiggle(e, h, rng);
   }
 }
 
-// noisy (IM/:361-366): round() is half-to-even == rint
-TG_HD int noisy(int val, Rng& rng) {
-  const double between = val / 2.0;
-  const double u = (val < between) ? rng.uniform((double)val, between) : rng.uniform(between, (double)val);
-  return (int)rint(u);
-}
+// ==========================================================================================
+// Primitive tick: _TreasureGameImpl.step (IM/:290-359).  PM is the set of primitive actions
+// the caller can issue (a compile-time mask); the others compile away.
+// ==========================================================================================
+constexpr uint32_t PM_ALL = 0x7Fu;
+template <uint32_t PM>
+TG_HD bool may(int prim, int p) { return ((PM >> p) & 1u) && prim == p; }
 
-// ==========================================================================================
-// Primitive tick: _TreasureGameImpl.step (IM/:290-359). Returns the tick reward.
-// ==========================================================================================
-TG_HD int tick(const Level& L, const Map& m, Env& e, int prim, Rng& rng) {
+template <uint32_t PM>
+TG_HD int tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, int prim, Rng& rng) {
   int xd = 0, yd = 0;
-  if (prim == P_UP) {
-    if (m.can_go_up(e)) yd = noisy(-INCR, rng);
-  } else if (prim == P_DOWN) {
-    if (m.can_go_down(e)) yd = noisy(INCR, rng);
-  } else if (prim == P_LEFT) {
-    if (m.can_go_side(e, -1)) { xd = noisy(-INCR, rng); e.f &= ~F_FACING; }
-  } else if (prim == P_RIGHT) {
-    if (m.can_go_side(e, +1)) { xd = noisy(INCR, rng); e.f |= F_FACING; }
-  } else if (prim == P_JUMP) {
-    if (!m.can_go_down(e) && m.up_clear(e)) {
-      const uint32_t jt = (rng.random() > 0.25) ? 23u : 22u;
-      e.f = (e.f & ~F_JT) | jt;
+  // the action's precondition (IM/:297-319); moves and the jump share one draw site
+  bool ok = false;
+  if (may<PM>(prim, P_UP)) ok = m.can_go_up(e);
+  else if (may<PM>(prim, P_DOWN)) ok = m.can_go_down(e);
+  else if (may<PM>(prim, P_LEFT)) ok = m.can_go_side(e, -1);
+  else if (may<PM>(prim, P_RIGHT)) ok = m.can_go_side(e, +1);
+  else if (may<PM>(prim, P_JUMP)) ok = !m.can_go_down(e) && m.up_clear(e);
+  if (ok) {
+    const double r = rng.random();
+    if (may<PM>(prim, P_JUMP)) {  // jump_ticker = 22, or 23 if random() > 0.25 (IM/:317-319)
+      e.f = (e.f & ~F_JT) | ((r > 0.25) ? 23u : 22u);
+    } else {
+      // noisy(+-4) (IM/:361-366): int(round(uniform(-4, -2.0))) or int(round(uniform(2.0, 4))),
+      // uniform = a + (b-a)*r with b-a = 2.0 exactly; round() half-to-even == rint
+      const bool neg = may<PM>(prim, P_UP) | may<PM>(prim, P_LEFT);
+      const int d = (int)rint((neg ? -4.0 : 2.0) + 2.0 * r);
+      if (may<PM>(prim, P_LEFT) | may<PM>(prim, P_RIGHT)) {
+        xd = d;
+        e.f = may<PM>(prim, P_RIGHT) ? (e.f | F_FACING) : (e.f & ~F_FACING);
+      } else {
+        yd = d;
+      }
     }
-  } else if (prim == P_INTERACT) {  // object list order: handles (3,4) before the bolt (6)
-    if (near_cell(e, L.handle_cx[0], L.handle_cy[0], R2_HANDLE)) flip(L, e, 0, rng);
-    if (near_cell(e, L.handle_cx[1], L.handle_cy[1], R2_HANDLE)) flip(L, e, 1, rng);
+  }
+  if (may<PM>(prim, P_INTERACT)) {  // object list order: handles (3,4) before the bolt (6)
+    if (near_cell(e, L.handle_cx[0], L.handle_cy[0], R2_HANDLE)) flip(trig, e, 0, rng);
+    if (near_cell(e, L.handle_cx[1], L.handle_cy[1], R2_HANDLE)) flip(trig, e, 1, rng);
     if (near_cell(e, L.bolt_cx, L.bolt_cy, R2_OBJ) && got_key(e.f)) {
-      cascade(L, e, 5, 0, rng);  // try_unlock -> bolt.unlock (IM/:430-432)
+      cascade(trig, e, 5, 0, rng);  // try_unlock -> bolt.unlock (IM/:430-432)
       drop_key(e);
     }
   }
+  // jump ticker / gravity (IM/:331-337), both at the pre-move x
   const uint32_t jt = e.f & F_JT;
   if (jt > 0) {
     if (m.up_clear(e)) yd = -INCR;
@@ -411,15 +469,18 @@ TG_HD int tick(const Level& L, const Map& m, Env& e, int prim, Rng& rng) {
     yd = INCR;  // jump_ticker already 0
   }
   e.px += xd;
-  if (yd > 0 && m.can_fall(e)) {
-    while (yd > 0) {  // fall pixel by pixel (IM/:341-346)
-      e.py += 1;
-      yd -= 1;
-      if (!m.can_fall(e)) yd = 0;
+  // integrate y (IM/:341-348): with yd > 0 and can_fall, fall pixel by pixel while can_fall
+  // holds: the distance is the first k in 1..yd-1 with !can_fall(py + k), else yd (yd <= 4)
+  if (yd > 0) {
+    const uint32_t cf = m.can_fall4(Map::dc_of(e.f), e.px, e.py);
+    if (cf & 1u) {
+      int dist = yd;
+      for (int k = yd - 1; k >= 1; --k)
+        if (!((cf >> k) & 1u)) dist = k;
+      yd = dist;
     }
-  } else {
-    e.py += yd;
   }
+  e.py += yd;
   // pickups in object order: key then goldcoin (IM/:350-354)
   if (near_cell(e, e.kx, e.ky, R2_OBJ)) {
     e.kx = L.W - 1 - bag_len(e.f);
@@ -431,7 +492,7 @@ TG_HD int tick(const Level& L, const Map& m, Env& e, int prim, Rng& rng) {
     e.gy = L.H - 1;
     bag_push(e.f, true);
   }
-  return prim == P_JUMP ? -5 : -1;  // JUMP_REWARD / STEP_REWARD (IM/:15-16)
+  return may<PM>(prim, P_JUMP) ? -5 : -1;  // JUMP_REWARD / STEP_REWARD (IM/:15-16)
 }
 
 // ==========================================================================================
@@ -448,9 +509,11 @@ TG_HD bool close_x(const Env& e, int txc) {
 }
 // go_left / go_right is_target_cell (MO/:54-67, 126-139)
 TG_HD bool go_is_target(const Level& L, const Map& m, const Env& e, int dir, int xc, int yc) {
-  return m.cell(e.f, xc, yc - 1) == C_LADDER || m.cell(e.f, xc, yc + 1) == C_LADDER ||
-         m.cell(e.f, xc + dir, yc) == C_WALL || is_object_at(L, e, xc, yc) ||
-         is_closed_door_at(L, e, xc + dir, yc) || m.cell(e.f, xc + dir, yc + 1) == C_OPEN;
+  const uint32_t dc = Map::dc_of(e.f);
+  const uint32_t up = m.cellb(xc, yc - 1), dn = m.cellb(xc, yc + 1), sd = m.cellb(xc + dir, yc),
+                 sdn = m.cellb(xc + dir, yc + 1);
+  return Map::is_ladder(up | dn) | Map::is_wall(sd) | is_object_at(L, e, xc, yc) |
+         is_closed_door_at(L, e, xc + dir, yc) | Map::is_open(sdn, dc);
 }
 // get_target_cell (MO/:43-52; MO/:115-124 whose xc<0 test can never fire going right, and
 // terminates because OOB is WALL)
@@ -465,12 +528,13 @@ TG_HD bool go_target(const Level& L, const Map& m, const Env& e, int dir, int xc
 }
 // jump landing (MO/:281-287)
 TG_HD bool landing(const Map& m, const Env& e, int xc, int yc) {
-  return m.cell(e.f, xc, yc) == C_OPEN && m.cell(e.f, xc, yc + 1) == C_WALL;
+  return m.open_cell(Map::dc_of(e.f), xc, yc) & Map::is_wall(m.cellb(xc, yc + 1));
 }
 
 TG_HD bool can_run(const Level& L, const Map& m, const Env& e, int k) {
   int xc, yc;
   player_cell(e, xc, yc);
+  const uint32_t dc = Map::dc_of(e.f);
   switch (k) {
     case O_GO_LEFT:
     case O_GO_RIGHT: {  // MO/:23-41, 95-113
@@ -478,8 +542,8 @@ TG_HD bool can_run(const Level& L, const Map& m, const Env& e, int k) {
       int tc;
       if (!go_target(L, m, e, dir, xc, yc, tc)) return false;
       for (int x = xc; dir < 0 ? x >= tc : x <= tc; x += dir) {
-        if (m.cell(e.f, x, yc) != C_OPEN) return false;
-        if (m.cell(e.f, x, yc + 1) == C_OPEN) return false;
+        if (!m.open_cell(dc, x, yc)) return false;
+        if (m.open_cell(dc, x, yc + 1)) return false;
       }
       return true;
     }
@@ -492,13 +556,13 @@ TG_HD bool can_run(const Level& L, const Map& m, const Env& e, int k) {
     case O_DOWN_LEFT:
     case O_DOWN_RIGHT: {  // MO/:199-209, 394-404
       const int dir = k == O_DOWN_LEFT ? -1 : 1;
-      return m.cell(e.f, xc + dir, yc) == C_OPEN && m.cell(e.f, xc + dir, yc + 1) == C_OPEN;
+      return m.open_cell(dc, xc + dir, yc) & m.open_cell(dc, xc + dir, yc + 1);
     }
     case O_JUMP_LEFT:
     case O_JUMP_RIGHT: {  // MO/:254-267, 324-337
       const int dir = k == O_JUMP_LEFT ? -1 : 1;
-      return m.cell(e.f, xc, yc - 1) == C_OPEN && m.cell(e.f, xc + dir, yc - 1) == C_OPEN &&
-             (landing(m, e, xc + dir, yc - 1) || landing(m, e, xc + 2 * dir, yc - 1));
+      return m.open_cell(dc, xc, yc - 1) & m.open_cell(dc, xc + dir, yc - 1) &
+             (landing(m, e, xc + dir, yc - 1) | landing(m, e, xc + 2 * dir, yc - 1));
     }
   }
   return false;
@@ -513,69 +577,75 @@ TG_HD uint32_t available_mask(const Level& L, const Map& m, const Env& e) {  // 
 
 // option-local state (start_cell / target_cell are None between steps, MO/:80-83 etc.)
 struct Opt {
-  int k;
   int tx;      // target cell x
   bool init;   // target computed
   bool done;
 };
 
-// policy_step of every option (MO/)
+// primitive actions each option's policy can return
+constexpr uint32_t prims_of(int k) {
+  return k == O_GO_LEFT ? (1u << P_LEFT)
+       : k == O_GO_RIGHT ? (1u << P_RIGHT)
+       : k == O_UP_LADDER ? (1u << P_UP) | (1u << P_NOP)
+       : k == O_DOWN_LADDER ? (1u << P_DOWN) | (1u << P_NOP)
+       : k == O_INTERACT ? (1u << P_INTERACT)
+       : k == O_DOWN_LEFT ? (1u << P_LEFT) | (1u << P_NOP)
+       : k == O_DOWN_RIGHT ? (1u << P_RIGHT) | (1u << P_NOP)
+       : (1u << P_JUMP) | (1u << P_LEFT) | (1u << P_RIGHT) | (1u << P_NOP);
+}
+
+// policy_step of option K (MO/)
+template <int K>
 TG_HD int policy(const Level& L, const Map& m, const Env& e, Opt& o) {
   int xc, yc;
-  switch (o.k) {
-    case O_GO_LEFT:
-    case O_GO_RIGHT: {  // MO/:74-85, 146-157
-      const int dir = o.k == O_GO_LEFT ? -1 : 1;
-      if (!o.init) {
-        player_cell(e, xc, yc);
-        go_target(L, m, e, dir, xc, yc, o.tx);  // exists: can_run checked it
-        o.init = true;
-      }
-      if (close_x(e, o.tx)) o.done = true;
-      return dir < 0 ? P_LEFT : P_RIGHT;
+  if (K == O_GO_LEFT || K == O_GO_RIGHT) {  // MO/:74-85, 146-157
+    constexpr int dir = K == O_GO_LEFT ? -1 : 1;
+    if (!o.init) {
+      player_cell(e, xc, yc);
+      go_target(L, m, e, dir, xc, yc, o.tx);  // exists: can_run checked it
+      o.init = true;
     }
-    case O_UP_LADDER:  // MO/:168-173
-      if (!m.can_go_up(e)) { o.done = true; return P_NOP; }
-      return P_UP;
-    case O_DOWN_LADDER:  // MO/:184-189
-      if (!m.can_go_down(e)) { o.done = true; return P_NOP; }
-      return P_DOWN;
-    case O_INTERACT:  // MO/:457-460
-      o.done = true;
-      return P_INTERACT;
-    case O_DOWN_LEFT:
-    case O_DOWN_RIGHT: {  // MO/:231-244, 426-439
-      const int dir = o.k == O_DOWN_LEFT ? -1 : 1;
-      if (!o.init) {
-        // get_target_cell (MO/:211-221, 406-416) scans down column xc+dir for the first
-        // non-open cell; only its x is ever used (close_enough_x).  It returns None only if
-        // the scan leaves the grid, after which the reference raises TypeError; the bottom
-        // row of a walled level never lets that happen.
-        player_cell(e, xc, yc);
-        o.tx = xc + dir;
-        o.init = true;
-      }
-      if (close_x(e, o.tx)) {
-        if (!m.can_fall(e)) o.done = true;
-        return P_NOP;
-      }
-      return dir < 0 ? P_LEFT : P_RIGHT;
+    if (close_x(e, o.tx)) o.done = true;
+    return dir < 0 ? P_LEFT : P_RIGHT;
+  } else if (K == O_UP_LADDER) {  // MO/:168-173
+    if (!m.can_go_up(e)) { o.done = true; return P_NOP; }
+    return P_UP;
+  } else if (K == O_DOWN_LADDER) {  // MO/:184-189
+    if (!m.can_go_down(e)) { o.done = true; return P_NOP; }
+    return P_DOWN;
+  } else if (K == O_INTERACT) {  // MO/:457-460
+    o.done = true;
+    return P_INTERACT;
+  } else if (K == O_DOWN_LEFT || K == O_DOWN_RIGHT) {  // MO/:231-244, 426-439
+    constexpr int dir = K == O_DOWN_LEFT ? -1 : 1;
+    if (!o.init) {
+      // get_target_cell (MO/:211-221, 406-416) scans down column xc+dir for the first
+      // non-open cell; only its x is ever used (close_enough_x).  It returns None only if
+      // the scan leaves the grid, after which the reference raises TypeError; the bottom
+      // row of a walled level never lets that happen.
+      player_cell(e, xc, yc);
+      o.tx = xc + dir;
+      o.init = true;
     }
-    default: {  // O_JUMP_LEFT / O_JUMP_RIGHT (MO/:297-314, 367-384)
-      const int dir = o.k == O_JUMP_LEFT ? -1 : 1;
-      if (!o.init) {
-        player_cell(e, xc, yc);
-        o.tx = landing(m, e, xc + dir, yc - 1) ? xc + dir : xc + 2 * dir;  // MO/:269-279
-        o.init = true;
-        return P_JUMP;
-      }
-      if (close_x(e, o.tx)) {
-        if (!m.can_fall(e)) o.done = true;
-        return P_NOP;
-      }
-      const bool back = !m.can_fall(e) && !m.can_go_side(e, dir);
-      return (back ? -dir : dir) < 0 ? P_LEFT : P_RIGHT;
+    if (close_x(e, o.tx)) {
+      if (!m.can_fall(e)) o.done = true;
+      return P_NOP;
     }
+    return dir < 0 ? P_LEFT : P_RIGHT;
+  } else {  // O_JUMP_LEFT / O_JUMP_RIGHT (MO/:297-314, 367-384)
+    constexpr int dir = K == O_JUMP_LEFT ? -1 : 1;
+    if (!o.init) {
+      player_cell(e, xc, yc);
+      o.tx = landing(m, e, xc + dir, yc - 1) ? xc + dir : xc + 2 * dir;  // MO/:269-279
+      o.init = true;
+      return P_JUMP;
+    }
+    if (close_x(e, o.tx)) {
+      if (!m.can_fall(e)) o.done = true;
+      return P_NOP;
+    }
+    const bool back = !m.can_fall(e) && !m.can_go_side(e, dir);
+    return (back ? -dir : dir) < 0 ? P_LEFT : P_RIGHT;
   }
 }
 
@@ -633,29 +703,46 @@ struct StepResult {
   int done;    // got gold and back in row 0
   int ticks;
 };
-// the while-not-done loop of _Option.run (OP/:28-31) for an option whose can_run held
-TG_HD void run_option(const Level& L, const Map& m, Env& e, int k, Rng& rng, StepResult& r) {
+// the while-not-done loop of _Option.run (OP/:28-31) for option K, whose can_run held
+template <int K>
+TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env& e, Rng& rng,
+                        StepResult& r) {
   r.ran = 1;
-  Opt o{k, 0, false, false};
+  Opt o{0, false, false};
   do {
-    const int prim = policy(L, m, e, o);
-    r.reward += tick(L, m, e, prim, rng);
+    const int prim = policy<K>(L, m, e, o);
+    r.reward += tick<prims_of(K)>(L, trig, m, e, prim, rng);
     if (++r.ticks >= TICK_CAP) {
       e.f |= E_TICKCAP;
       break;
     }
   } while (!o.done);
 }
+TG_HD void run_option(const Level& L, const uint32_t* trig, const Map& m, Env& e, int k,
+                      Rng& rng, StepResult& r) {
+  switch (k) {
+    case O_GO_LEFT: run_option_k<O_GO_LEFT>(L, trig, m, e, rng, r); break;
+    case O_GO_RIGHT: run_option_k<O_GO_RIGHT>(L, trig, m, e, rng, r); break;
+    case O_UP_LADDER: run_option_k<O_UP_LADDER>(L, trig, m, e, rng, r); break;
+    case O_DOWN_LADDER: run_option_k<O_DOWN_LADDER>(L, trig, m, e, rng, r); break;
+    case O_INTERACT: run_option_k<O_INTERACT>(L, trig, m, e, rng, r); break;
+    case O_DOWN_LEFT: run_option_k<O_DOWN_LEFT>(L, trig, m, e, rng, r); break;
+    case O_DOWN_RIGHT: run_option_k<O_DOWN_RIGHT>(L, trig, m, e, rng, r); break;
+    case O_JUMP_LEFT: run_option_k<O_JUMP_LEFT>(L, trig, m, e, rng, r); break;
+    default: run_option_k<O_JUMP_RIGHT>(L, trig, m, e, rng, r); break;
+  }
+}
 // option_list[a] (TG/:92): -1 for an out-of-range action (the reference raises IndexError)
 TG_HD int option_index(int a) {
   if (a < -O_COUNT || a >= O_COUNT) return -1;
   return a < 0 ? a + O_COUNT : a;  // Python negative indexing
 }
-TG_HD StepResult env_step(const Level& L, const Map& m, Env& e, int a, Rng& rng) {
+TG_HD StepResult env_step(const Level& L, const uint32_t* trig, const Map& m, Env& e, int a,
+                          Rng& rng) {
   StepResult r{0, 0, 0, 0};
   const int k = option_index(a);
   if (k < 0) e.f |= E_ACTION;
-  else if (can_run(L, m, e, k)) run_option(L, m, e, k, rng, r);  // OP/:22-23 gate
+  else if (can_run(L, m, e, k)) run_option(L, trig, m, e, k, rng, r);  // OP/:22-23 gate
   r.done = is_done(e);
   return r;
 }

@@ -14,7 +14,7 @@
 
 namespace tg {
 
-constexpr int MAX_CELLS = 32 * 32;  // LDS grid capacity (default level: 14 x 13)
+constexpr int MAX_CELLS = 48 * 48;  // LDS grid capacity incl. the border (default level: 18 x 17)
 
 inline int level_err(std::string& err, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 inline int level_err(std::string& err, const char* fmt, ...) {
@@ -85,16 +85,20 @@ inline int parse_level(const char* dom, const char* objs, const char* inter, Lev
   if (desc.empty()) return level_err(err, "level: empty domain");
   L.W = (int)desc[0].size();
   L.H = (int)desc.size();
-  if (L.W * L.H > MAX_CELLS || L.W > 120 || L.H > 120)
-    return level_err(err, "level: %dx%d exceeds the %d-cell LDS grid", L.W, L.H, MAX_CELLS);
-  grid.assign((size_t)L.W * L.H, C_OPEN);
+  const int PW = L.W + 2 * PAD, PH = L.H + 2 * PAD;
+  if (PW * PH > MAX_CELLS || L.W > 120 || L.H > 120)
+    return level_err(err, "level: %dx%d (+%d-cell border) exceeds the %d-cell LDS grid", L.W,
+                     L.H, PAD, MAX_CELLS);
+  // bordered grid of cell bits (tg_core.h B_*): the border is WALL, like the reference's
+  // out-of-bounds probes (IM/:218-225)
+  grid.assign((size_t)PW * PH, (uint8_t)B_WALL);
   bool found = false;
   for (int y = 0; y < L.H; ++y) {
     if ((int)desc[y].size() != L.W) return level_err(err, "level: ragged row %d", y);
     for (int x = 0; x < L.W; ++x) {
       const char c = desc[y][x];
-      grid[y * L.W + x] = c == ' ' ? C_OPEN : c == '/' ? C_WALL : c == 'L' ? C_LADDER
-                                                              : c == 'D' ? C_DOOR : C_OTHER;
+      grid[(y + PAD) * PW + x + PAD] = c == ' ' ? B_OPEN : c == '/' ? B_WALL : c == 'L' ? B_LADDER
+                                       : c == 'D' ? B_DOOR : 0;
       if (!found && c != '/') {  // player_initial_position (IM/:173-176)
         L.start_x = x;
         L.start_y = y;
@@ -123,7 +127,7 @@ inline int parse_level(const char* dom, const char* objs, const char* inter, Lev
     if (k < 3) {
       L.door_cx[k] = (int8_t)cx;
       L.door_cy[k] = (int8_t)cy;
-      grid[cy * L.W + cx] = (uint8_t)(C_DOORSLOT + k);
+      grid[(cy + PAD) * PW + cx + PAD] = (uint8_t)(B_DOOROBJ << k);  // type from the door state
       if (flag) L.init_flags |= 1u << (F_OBJ + k);
     } else if (k < 5) {
       L.handle_cx[k - 3] = (int8_t)cx;

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-wave k_run timing from a DIAGNOSTIC build (-DTG_DIAG_STAMPS): for each active wave,
+cycles spent loading its envs (+ RNG window), running the option loop and in the epilogue,
+with the loop's iteration count (max ticks over its lanes).  Not the product library."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import gym_treasure_game_amd as tg  # noqa: E402
+from gym_treasure_game_amd import _lib  # noqa: E402
+
+SO = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_stamps.so")
+
+
+def main():
+    if not os.path.exists(SO):
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                               "-ffp-contract=off", "-fPIC", "-shared", "-DTG_DIAG_STAMPS", "-o", SO,
+                               os.path.join(ROOT, "gym-treasure-game_amd", "csrc", "tg_amd.hip")])
+    _lib._lib = None
+    _lib.LIB_PATH = SO
+    L = _lib.load()
+    L.tg_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    n = int(os.environ.get("N", 1 << 20))
+    vec = tg.TreasureGameVec(n, seed=0, autoreset=True)
+    vec.reset()
+    for t in range(int(os.environ.get("STEPS", 30))):
+        vec.step(vec.policy_actions(t))
+    torch.cuda.synchronize()
+    nw = n // 64
+    buf = np.zeros((nw, 4), np.uint64)
+    vec.stats_reset()
+    vec.step(vec.policy_actions(999))
+    torch.cuda.synchronize()
+    _lib.check(L.tg_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), nw), "stamps")
+    act = buf[:, 3] > 0
+    b = buf[act].astype(np.float64)
+    mx = (buf[act, 3] & 0xFFFFFFFF).astype(np.float64)
+    sm = (buf[act, 3] >> 32).astype(np.float64)
+    print("active waves", act.sum(), "of", nw)
+    for name, v in (("load", b[:, 0]), ("loop", b[:, 1]), ("epilogue", b[:, 2]),
+                    ("loop/iter", b[:, 1] / np.maximum(mx, 1)), ("max ticks", mx),
+                    ("lane eff", sm / 64 / np.maximum(mx, 1))):
+        print("%-10s mean %10.1f p50 %10.1f p90 %10.1f max %10.1f" % (
+            name, v.mean(), np.median(v), np.percentile(v, 90), v.max()))
+    w = np.flatnonzero(act)
+    for lo, hi in ((0, 100), (len(w) // 2, len(w) // 2 + 5), (len(w) - 5, len(w))):
+        for k in range(lo, min(hi, len(w)), max(1, (hi - lo) // 5)):
+            print("  wave %6d load %8d loop %9d epi %8d iters %4d" % (
+                w[k], buf[w[k], 0], buf[w[k], 1], buf[w[k], 2], buf[w[k], 3] & 0xFFFFFFFF))
+    vec.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -59,15 +59,23 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
   gen[0] = 19650218u;
   for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
   const Map m{grid.data(), L->W, L->H};
+  const uint32_t* trig = &L->trig[0][0];
   const int64_t T1 = (int64_t)steps + 1;
   std::vector<uint32_t> mt(MT_N);
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t g = (uint64_t)(g0 + i);
     seed_mt(mt.data(), gen, seed_base + g);
     Env e{};
-    Rng rng(mt.data(), 0u);
-    reset_env(*L, e, rng);
-    reset_env(*L, e, rng);
+    int64_t ndraws = 0;
+    {  // construct + reset, each a separate launch on the device (k_create, k_reset)
+      Rng rng(mt.data(), 0u);
+      reset_env(*L, e, rng);
+      e.mti = rng.finish();
+      Rng rng2(mt.data(), e.mti);
+      reset_env(*L, e, rng2);
+      e.mti = rng2.finish();
+      ndraws += rng.draws + rng2.draws;
+    }
     double o[9], fo[9];
     observe(*L, e, o);
     uint64_t h = rec_hash(g, o, 0, 0, 0);
@@ -89,7 +97,8 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
           a = __builtin_ctz(mm);
         }
       }
-      const StepResult r = env_step(*L, m, e, a, rng);
+      Rng rng(mt.data(), e.mti);  // per step, as each launch rebuilds the register window
+      const StepResult r = env_step(*L, trig, m, e, a, rng);
       nt += r.ticks;
       observe(*L, e, fo);
       memcpy(o, fo, sizeof o);
@@ -97,6 +106,8 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
         reset_env(*L, e, rng);
         observe(*L, e, o);
       }
+      e.mti = rng.finish();
+      ndraws += rng.draws;
       h = rec_hash(h, fo, r.reward, r.ran, r.done);
       const int64_t j = i * T1 + t + 1;
       if (obs) memcpy(&obs[j * 9], o, sizeof o);
@@ -106,7 +117,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
       if (done) done[j] = (uint8_t)r.done;
     }
     if (hash) hash[i] = h;
-    if (draws) draws[i] = rng.draws;  // includes the 8 construct + reset draws
+    if (draws) draws[i] = ndraws;  // includes the 8 construct + reset draws
     if (ticks) ticks[i] = nt;
   }
   return 0;
