@@ -107,6 +107,157 @@ __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o
   for (int k = 0; k < 9; ++k) p[k] = o[k];
 }
 
+// ------------------------------------------------------------------------------------------
+// CPython random for the option loops (k_run, k_step): tg::Rng's read-only consumption of the
+// two pre-twisted generations, with a 16-B chunk window in LDS.
+//   Each wave owns a ring [slot 4][lane 64] x 16 B (4 KiB).  Chunk c (words 4c..4c+3, 312
+//   chunks over both halves) sits in slot c % 4 (312 = 4 * 78, so the ring survives the
+//   wrap).  A lane holds chunks c..c+3; when its draw finishes chunk c it fetches chunk c+4
+//   into the freed slot with global_load_lds_dwordx4 (LDS-DMA: no VGPR destination).
+//   Why not a register window: one that rotates (c0 = c1; c1 = c2; c2 = load) makes the
+//   compiler copy the freshly loaded chunk at once, i.e. wait for the load it has just issued
+//   (ISA: s_waitcnt vmcnt(1)/(0) after each prefetch), so every shift paid a full HBM
+//   latency.  The DMAs are issued from inline asm, invisible to the compiler's waitcnt pass,
+//   and ordered by hand: "s_waitcnt vmcnt(RING_SLOTS - 2)" before each draw's LDS read.  Why
+//   it suffices: a draw reads chunk c and, at o = 2, nothing else — chunk c was fetched when
+//   the lane finished chunk c-4 (or in prime()), and finishing c-3 and c-2 issued two more
+//   DMAs since; vmcnt counts every VMEM op of the wave in issue order (loads, stores, DMA:
+//   MI355X_MICROARCH.md §vmcnt), so "all but the two youngest done" covers chunk c.
+// ------------------------------------------------------------------------------------------
+constexpr int RING_SLOTS = 4;
+constexpr int RING_SLOT_BYTES = 64 * 16;
+constexpr int RING_WAVE_BYTES = RING_SLOTS * RING_SLOT_BYTES;  // 4 KiB per wave
+constexpr uint32_t MT_CHUNKS = MT_WORDS / 4;                    // 312
+static_assert(MT_CHUNKS % RING_SLOTS == 0, "ring slot of a chunk must survive the wrap");
+static_assert(RING_WAVE_BYTES >= MT_N * 4, "wave_refill reuses the ring as scratch");
+
+typedef __attribute__((address_space(1))) uint32_t glb_u32;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 lds_u2;
+
+// LDS-DMA of one 16-B chunk per active lane into LDS [m0 + lane * 16]; M0 is saved/restored
+__device__ __forceinline__ void glds16(uint32_t m0, const uint32_t* gptr) {
+  uint32_t save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(save)
+      : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
+      : "memory");
+}
+// chunk -> its slot of the wave's ring; M0 must be wave-uniform, so one DMA per slot value
+__device__ __forceinline__ void ring_fetch(uint32_t m0_slot0, uint32_t slot, const uint32_t* g) {
+  if (slot == 0u) glds16(m0_slot0, g);
+  else if (slot == 1u) glds16(m0_slot0 + RING_SLOT_BYTES, g);
+  else if (slot == 2u) glds16(m0_slot0 + 2 * RING_SLOT_BYTES, g);
+  else glds16(m0_slot0 + 3 * RING_SLOT_BYTES, g);
+}
+
+// the rare second crossing (RngRing::fetch), out of line so that the draw sites stay small
+__device__ __noinline__ void regen_half(uint32_t* mt, uint32_t h) {
+  twist_gen(mt + (MT_N - h), mt + h);
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+}
+
+struct RngRing {
+  uint32_t* mt;    // this env's MT_WORDS words (HBM)
+  lds_u8* cell;    // this lane's 16-B cell in slot 0 of the wave's ring
+  uint32_t m0;     // LDS address of slot 0 of the wave's ring (wave-uniform)
+  uint32_t pos;    // [0, MT_WORDS), even
+  uint32_t draws;
+  bool primed, crossed;
+
+  __device__ __forceinline__ RngRing(uint32_t* m, uint32_t p, lds_u8* wave_ring)
+      : mt(m), cell(wave_ring + (threadIdx.x & 63) * 16),
+        m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_ring)), pos(p), draws(0u),
+        primed(false), crossed(false) {}
+
+  __device__ __forceinline__ void fetch(uint32_t c) {
+    if (c >= MT_CHUNKS) c -= MT_CHUNKS;
+    if (crossed && (c == 0u || c == MT_CHUNKS / 2)) {
+      // the lane will enter a second half in this launch: it is stale, regenerate it from
+      // the half the lane is in before any of its chunks is fetched (per lane, rare)
+      regen_half(mt, c * 4u);
+    }
+    ring_fetch(m0, c & (RING_SLOTS - 1), mt + c * 4u);
+  }
+  __device__ __forceinline__ void prime() {
+    const uint32_t c = pos >> 2;
+#pragma unroll
+    for (int j = 0; j < RING_SLOTS; ++j) fetch(c + j);
+    primed = true;
+  }
+  __device__ __forceinline__ double random() {
+    if (!primed) prime();
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    static_assert(RING_SLOTS - 2 == 2, "the vmcnt above");
+    const uint32_t c = pos >> 2, o = pos & 2u;
+    const u32x2 w = *(const lds_u2*)((const lds_u32*)(cell + (c & (RING_SLOTS - 1)) * RING_SLOT_BYTES) + o);
+    if (o) fetch(c + RING_SLOTS);  // chunk c done: its slot takes chunk c + 4
+    pos += 2;
+    if (pos == (uint32_t)MT_WORDS) pos = 0u;
+    if (pos == 0u || pos == (uint32_t)MT_N) crossed = true;
+    ++draws;
+    return mt_double(w.x, w.y);
+  }
+  __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
+  // drain the DMAs (the ring is reused as scratch); returns the position to store
+  __device__ __forceinline__ uint32_t finish() {
+    if (primed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    primed = false;
+    return pos;
+  }
+};
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+// After a launch, every lane in `need` has left one half of its MT buffer: the wave
+// regenerates it (twist_gen of the half the lane is in), one env at a time, all 64 lanes
+// coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which
+// an earlier 64-word round wrote into the wave's LDS scratch (rounds are >= 3 apart).
+// Must be reached by all 64 lanes of the wave.
+__device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* env_mt, uint32_t pos,
+                                            lds_u32* scratch) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t src_l = (uint64_t)(uintptr_t)(env_mt + mt_half(pos));
+  const uint64_t dst_l = (uint64_t)(uintptr_t)(env_mt + (MT_N - mt_half(pos)));
+  constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
+  while (need) {
+    const int L = __ffsll((long long)need) - 1;
+    need &= need - 1;
+    const glb_u32* src = (const glb_u32*)(uintptr_t)readlane64(src_l, L);
+    glb_u32* dst = (glb_u32*)(uintptr_t)readlane64(dst_l, L);
+    uint32_t a[ROUNDS], b[ROUNDS], c[4];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+      const int p = r * 64 + lane;
+      a[r] = p < MT_N ? src[p] : 0u;
+      b[r] = p + 1 < MT_N ? src[p + 1] : 0u;
+      if (r < 4) c[r] = p < MT_N - MT_M ? src[p + MT_M] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+      const int p = r * 64 + lane;
+      if (p < MT_N) {
+        const uint32_t bb = p + 1 < MT_N ? b[r] : scratch[0];
+        const uint32_t cc = p < MT_N - MT_M ? c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
+        const uint32_t w = mt_twist(a[r], bb, cc);
+        scratch[p] = w;
+        dst[p] = w;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // round r visible to later rounds
+    }
+  }
+}
+
 // 64-lane sum (wave64)
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
@@ -119,44 +270,56 @@ enum { ST_STEPS, ST_VALID, ST_TICKS, ST_DRAWS, ST_EPISODES, ST_EP_OVERFLOW, ST_C
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
-// random.seed(seed0 + i); TreasureGame() — the constructor builds the game once
-// (_TreasureGameImpl.__init__, IM/:31-53: 4 draws); env.reset() is a separate call
-__global__ __launch_bounds__(BLOCK) void k_create(Soa S, int64_t n, Level L, uint64_t seed0,
+// random.seed(seed0 + i): init_by_array into the second half of the env's MT buffer; two
+// k_gen_twist launches then make generations 1 and 2, and k_reset (mask NULL) performs the
+// constructor's game build (_TreasureGameImpl.__init__, IM/:31-53: 4 draws) — tg_create.
+__global__ __launch_bounds__(BLOCK) void k_create(Soa S, int64_t n, uint64_t seed0,
                                                    const uint32_t* __restrict__ genrand) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
-  uint32_t* mt = S.mt + i * MT_N;
-  seed_mt(mt, genrand, seed0 + (uint64_t)i);
+  seed_mt(S.mt + i * MT_WORDS + MT_N, genrand, seed0 + (uint64_t)i);
   Env e{};
-  e.f = 0;
-  Rng rng(mt, 0u);
-  reset_env(L, e, rng);
-  e.mti = rng.finish();
+  e.mti = 0u;
   S.st4[i] = pack(e);
-  S.ang[i] = make_double2(e.ang0, e.ang1);
+  S.ang[i] = make_double2(0.0, 0.0);
   S.ep[i] = make_int2(0, 0);
+}
+// one generation for every env: the half at from_pos -> the other half
+__global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t from_pos) {
+  __shared__ uint32_t scratch[BLOCK / 64][MT_N];
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = i < n;
+  wave_refill(__ballot(live), S.mt + (live ? i : 0) * MT_WORDS, from_pos,
+              (lds_u32*)scratch[threadIdx.x >> 6]);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
                                                   const uint8_t* __restrict__ mask,
                                                   double* __restrict__ obs) {
+  __shared__ uint32_t scratch[BLOCK / 64][MT_N];
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  if (i >= n) return;
+  const bool live = i < n;
+  bool crossed = false;
   Env e;
-  unpack(S.st4[i], S.ang[i], e);
-  if (!mask || mask[i]) {
-    Rng rng(S.mt + i * MT_N, e.mti);
-    reset_env(L, e, rng);
-    e.mti = rng.finish();
-    S.st4[i] = pack(e);
-    S.ang[i] = make_double2(e.ang0, e.ang1);
-    S.ep[i] = make_int2(0, 0);
+  if (live) {
+    unpack(S.st4[i], S.ang[i], e);
+    if (!mask || mask[i]) {
+      Rng rng(S.mt + i * MT_WORDS, e.mti);
+      reset_env(L, e, rng);
+      e.mti = rng.finish();
+      crossed = rng.crossed;
+      S.st4[i] = pack(e);
+      S.ang[i] = make_double2(e.ang0, e.ang1);
+      S.ep[i] = make_int2(0, 0);
+    }
+    if (obs) {
+      double o[9];
+      observe(L, e, o);
+      store_obs(obs, i, o);
+    }
   }
-  if (obs) {
-    double o[9];
-    observe(L, e, o);
-    store_obs(obs, i, o);
-  }
+  wave_refill(__ballot(crossed), S.mt + (live ? i : 0) * MT_WORDS, live ? e.mti : 0u,
+              (lds_u32*)scratch[threadIdx.x >> 6]);
 }
 
 struct StepIO {
@@ -224,8 +387,8 @@ __device__ __forceinline__ void block_stats(unsigned long long* __restrict__ par
 }
 
 // finish one env-step: obs/reward/valid/done rows, episode counters, optional auto-reset
-template <bool AUTORESET, bool FINAL>
-__device__ __forceinline__ void finish_step(const Level& L, Env& e, Rng& rng, int64_t i,
+template <bool AUTORESET, bool FINAL, class R>
+__device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int64_t i,
                                             const StepResult& r, int2& ep, const StepIO& io) {
   double o[9];
   observe(L, e, o);  // get_state (TG/:94)
@@ -249,23 +412,29 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
                                                  EpQueue q, int64_t g0,
                                                  unsigned long long* __restrict__ stats,
                                                  uint32_t* __restrict__ err_or) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[(BLOCK / 64) * RING_WAVE_BYTES];
   LEVEL_IN_LDS();
+  lds_u8* const wring = (lds_u8*)ring + (threadIdx.x >> 6) * RING_WAVE_BYTES;
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
   StepResult r{0, 0, 0, 0};
   uint32_t draws = 0;
+  bool crossed = false;
   Env e;
+  e.mti = 0u;
   int2 ep = make_int2(0, 0);
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
-    Rng rng(S.mt + i * MT_N, e.mti);
+    RngRing rng(S.mt + i * MT_WORDS, e.mti, wring);
     r = env_step(L, trig, m, e, io.actions[i], rng);
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish();
     draws = rng.draws;
+    crossed = rng.crossed;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
+  wave_refill(__ballot(crossed), S.mt + (live ? i : 0) * MT_WORDS, e.mti, (lds_u32*)wring);
   if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
   if (live) {
     S.st4[i] = pack(e);
@@ -306,6 +475,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      unsigned long long* __restrict__ stats,
                                                      uint32_t* __restrict__ err_or) {
   __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
+  __shared__ uint32_t scratch[BLOCK / 64][MT_N];
   if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
   LEVEL_IN_LDS();  // includes the barrier
   (void)trig;
@@ -346,6 +516,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   if (runs) w.lists[(int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot] = (int32_t)i;
 
   int2 ep = make_int2(0, 0);
+  bool crossed = false;
   if (live && !runs) {  // reward None: state unchanged, rows written here
     if (k < 0) e.f |= E_ACTION;
     const double2 a2 = S.ang[i];
@@ -353,12 +524,16 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     e.ang1 = a2.y;
     ep = S.ep[i];
     dn = is_done(e);
-    Rng rng(S.mt + i * MT_N, e.mti);
+    Rng rng(S.mt + i * MT_WORDS, e.mti);
     StepResult r{0, 0, (int)dn, 0};
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish();
+    crossed = rng.crossed;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
+  if (AUTORESET)
+    wave_refill(__ballot(crossed), S.mt + (live ? i : 0) * MT_WORDS, live ? e.mti : 0u,
+                (lds_u32*)scratch[threadIdx.x >> 6]);
   if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, q, stats);
   if (live && !runs) {
     const uint4 s4n = pack(e);
@@ -397,6 +572,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
       }
     pre[NSEG] = acc;
   }
+  __shared__ __attribute__((aligned(16))) uint8_t ring[(BLOCK / 64) * RING_WAVE_BYTES];
   LEVEL_IN_LDS();  // includes the barrier
   const int total = pre[NSEG];
   const int base = (blockIdx.x * BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
@@ -416,8 +592,11 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   int64_t i = 0;
   StepResult r{0, 0, 0, 0};
   Env e;
+  e.mti = 0u;
   int2 ep = make_int2(0, 0);
   uint32_t draws = 0;
+  bool crossed = false;
+  lds_u8* const wring = (lds_u8*)ring + (threadIdx.x >> 6) * RING_WAVE_BYTES;
   unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   TG_STAMP(t0);
   (void)t0; (void)t1; (void)t2; (void)t3;
@@ -425,11 +604,8 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     i = w.lists[(int64_t)(k * SHARDS + sh) * w.shard_cap + idx];
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
-    Rng rng(S.mt + i * MT_N, e.mti);
-    rng.prime();  // issue the window loads now; the first draw comes after the policy setup
-#ifdef TG_DIAG_STAMPS
-    (void)*(volatile uint32_t*)&rng.c0.x;
-#endif
+    RngRing rng(S.mt + i * MT_WORDS, e.mti, wring);
+    rng.prime();  // issue the ring DMAs now; the first draw comes after the policy setup
     TG_STAMP(t1);
     run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform: one specialised loop
     TG_STAMP(t2);
@@ -437,8 +613,10 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish();
     draws = rng.draws;
+    crossed = rng.crossed;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
+  wave_refill(__ballot(crossed), S.mt + (live ? i : 0) * MT_WORDS, e.mti, (lds_u32*)wring);
   if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
   if (live) {
     S.st4[i] = pack(e);
@@ -674,7 +852,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->S.st4, sizeof(uint4) * n);
   ALLOC(h->S.ang, sizeof(double2) * n);
   ALLOC(h->S.ep, sizeof(int2) * n);
-  ALLOC(h->S.mt, sizeof(uint32_t) * MT_N * (size_t)n);
+  ALLOC(h->S.mt, sizeof(uint32_t) * MT_WORDS * (size_t)n);
   ALLOC(h->eps, sizeof(tg_episode) * (size_t)h->eps_cap);
   ALLOC(h->eps_count, sizeof(int32_t));
   ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n));
@@ -690,8 +868,13 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
       hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)) != hipSuccess ||
       hipMemset(h->err, 0, sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail(TG_E_HIP, "tg_create: upload failed"));
-  hipLaunchKernelGGL(k_create, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, h->L,
+  // seed -> generation 1 (first half) -> generation 2 (second half) -> the constructor's draws
+  hipLaunchKernelGGL(k_create, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n,
                      seed_base + (uint64_t)global_offset, h->genrand);
+  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, (uint32_t)MT_N);
+  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, 0u);
+  hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, h->L,
+                     (const uint8_t*)nullptr, (double*)nullptr);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) return cleanup(fail(TG_E_HIP, "k_create: %s", hipGetErrorString(e)));
@@ -869,7 +1052,7 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
   BIND(h);
   HIP_TRY(hipDeviceSynchronize());
   const int64_t n = h->n;
-  if (pos || flags || objs || mt_pos) {
+  if (pos || flags || objs) {
     std::vector<uint4> st((size_t)n);
     HIP_TRY(hipMemcpy(st.data(), h->S.st4, sizeof(uint4) * n, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; ++i) {
@@ -885,11 +1068,21 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
         objs[4 * i + 2] = (int8_t)((s.z >> 16) & 0xFF);
         objs[4 * i + 3] = (int8_t)(s.z >> 24);
       }
-      if (mt_pos) mt_pos[i] = s.w;
     }
   }
   if (ang) HIP_TRY(hipMemcpy(ang, h->S.ang, sizeof(double2) * n, hipMemcpyDeviceToHost));
-  if (mt) HIP_TRY(hipMemcpy(mt, h->S.mt, sizeof(uint32_t) * MT_N * (size_t)n, hipMemcpyDeviceToHost));
+  if (mt || mt_pos) {
+    // CPython's (mt[624], index) equivalent: the generation holding the position
+    std::vector<uint4> st((size_t)n);
+    HIP_TRY(hipMemcpy(st.data(), h->S.st4, sizeof(uint4) * n, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; ++i) {
+      const uint32_t p = st[(size_t)i].w;
+      if (mt_pos) mt_pos[i] = p % MT_N;
+      if (mt)
+        HIP_TRY(hipMemcpy(mt + i * MT_N, h->S.mt + i * MT_WORDS + mt_half(p), sizeof(uint32_t) * MT_N,
+                          hipMemcpyDeviceToHost));
+    }
+  }
   return TG_OK;
 }
 

@@ -13,7 +13,7 @@
 //     WALL (IM/:218-225) — here a 2-cell WALL border around the grid plus clamping;
 //   * near_enough (OB/:46-53) is the exact integer test d^2 < r^2 (inputs are integers);
 //   * the trigger cascade (OB/:76-94) is an explicit 8-bit-frame stack in one u64 register;
-//   * MT19937 twists lazily, one word pair at the point of consumption (see Rng below);
+//   * MT19937 keeps two pre-twisted generations per env; consumption only reads (Rng);
 //   * each option's policy/tick loop is specialised at compile time to the primitive actions
 //     that option can issue (a wave runs one option in the compacted kernel).
 // Prefixes: TG/ treasure_game.py, IM/ _treasure_game_impl.py, OB/ _objects.py,
@@ -84,111 +84,78 @@ TG_HD int floordiv(int a, int b) {  // Python // for b > 0
 TG_HD int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // ==========================================================================================
-// CPython random, lazily twisted.
-//   CPython (_randommodule.c genrand_uint32) twists all 624 words when index hits 624.  Word
-//   p of the new generation reads mt[p], mt[p+1] (old) and mt[p+397] (old, p < 227) or
-//   mt[p-227] (already new), and mt[0] (new) for p = 623.  Generating word p in place right
-//   before it is consumed therefore produces the identical stream: positions < p are new,
-//   positions >= p old.  A freshly seeded state (CPython index = 624) is position 0.
-//   No 624-iteration loop, hence no wavefront divergence on the twist.  Words are consumed in
-//   pairs (random() is the only consumer), so the position is always even; see the register
-//   window below for how the words reach registers.
+// CPython random over two pre-twisted generations.
+//   CPython (_randommodule.c genrand_uint32) regenerates all 624 words at once ("twist")
+//   whenever its index reaches 624, then tempers one word per call; random() takes two.
+//   Here each env keeps TWO consecutive generations, words [0, 624) and [624, 1248), and a
+//   position pos in [0, 1248) (always even: random() is the only consumer).  Consumption only
+//   reads: the half holding pos is CPython's mt[] with index pos % 624, and the other half is
+//   always the NEXT generation, so crossing 624 / 1248 continues the stream without a twist.
+//   The half a lane has left is regenerated (twist_gen of the one it is in) after the launch,
+//   by its whole wavefront, coalesced (tg_amd.hip wave_refill).  A launch that would enter a
+//   stale half (a second crossing: > 312 draws in one step) regenerates it first, per lane.
+//   Seeding (init_by_array) fills one half; two twists then give generations 1 and 2, pos 0.
 // ==========================================================================================
+constexpr int MT_WORDS = 2 * MT_N;  // per env
+constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu;
+
+TG_HD uint32_t mt_twist(uint32_t a, uint32_t b, uint32_t c) {
+  const uint32_t y = (a & MT_UPPER) | (b & MT_LOWER);
+  return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+TG_HD uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+// random_random (53-bit) from two consecutive words, exact in double (FMA-safe)
+TG_HD double mt_double(uint32_t w0, uint32_t w1) {
+  const uint32_t a = mt_temper(w0) >> 5, b = mt_temper(w1) >> 6;
+  return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
+}
+// dst = the generation after src (genrand_uint32's twist, out of place)
+TG_HD void twist_gen(const uint32_t* src, uint32_t* dst) {
+  for (int p = 0; p < MT_N - MT_M; ++p) dst[p] = mt_twist(src[p], src[p + 1], src[p + MT_M]);
+  for (int p = MT_N - MT_M; p < MT_N - 1; ++p)
+    dst[p] = mt_twist(src[p], src[p + 1], dst[p - (MT_N - MT_M)]);
+  dst[MT_N - 1] = mt_twist(src[MT_N - 1], dst[0], dst[MT_M - 1]);
+}
+TG_HD uint32_t mt_half(uint32_t pos) { return pos >= (uint32_t)MT_N ? (uint32_t)MT_N : 0u; }
+
+// Direct-load consumer (few draws per launch: create/reset/classify, and the host checks).
 struct Rng {
-  uint32_t* mt;    // this env's 624 words (HBM on device), 16-B aligned
-  uint32_t pos;    // always even: random() is the only consumer and takes words in pairs
+  uint32_t* mt;    // this env's MT_WORDS words
+  uint32_t pos;    // [0, MT_WORDS), even
   uint32_t draws;  // random() calls (instrumentation for the roofline)
-  // Register window over three 16-B chunks of each stream, refilled two chunks (4 draws)
-  // ahead so the gathered loads' L2-miss latency hides behind the ticks in between:
-  //   c0, c1, c2 = mt[pos & ~3 .. +12)                   (the words being twisted)
-  //   d0, d1, d2 = mt[q & ~3 .. +12), q = (pos + 397) % 624  (partners: pos+397 | pos-227)
-  // 624 = 4 * 156 and 397 = 1 (mod 4), so both streams walk the same 156 chunks cyclically:
-  // a pair at pos = 0 (mod 4) uses c0.xy(+c0.z) and d0.yz, a pair at pos = 2 (mod 4) uses
-  // c0.zw(+c1.x) and d0.w, d1.x and then shifts both windows by a chunk.  Each draw costs
-  // half a 16-B load per stream and half a 16-B store.  finish() flushes a half-rewritten c0.
-  // Prefetched chunks hold old words: the twist only rewrites position pos, and the partner
-  // stream runs 397 words ahead (old) or 227 behind (new long ago).
-  uint4 c0, c1, c2, d0, d1, d2;
-  bool primed;
+  bool crossed;    // entered the other half in this launch: the half left needs a refill
 
-  TG_HD Rng(uint32_t* m, uint32_t p)
-      : mt(m), pos(p), draws(0u), c0{}, c1{}, c2{}, d0{}, d1{}, d2{}, primed(false) {}
+  TG_HD Rng(uint32_t* m, uint32_t p) : mt(m), pos(p), draws(0u), crossed(false) {}
 
-  static TG_HD uint32_t wrap(uint32_t q) { return q >= (uint32_t)MT_N ? q - MT_N : q; }
-  TG_HD uint4 chunk(uint32_t q) const { return *reinterpret_cast<const uint4*>(mt + q); }
-  static TG_HD uint32_t twist(uint32_t a, uint32_t b, uint32_t c) {
-    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-  }
-  static TG_HD uint32_t temper(uint32_t y) {
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
-  }
-  TG_HD void prime() {
-    const uint32_t cb = pos & ~3u, db = wrap(pos + MT_M) & ~3u;
-    c0 = chunk(cb);
-    c1 = chunk(wrap(cb + 4));
-    c2 = chunk(wrap(cb + 8));
-    d0 = chunk(db);
-    d1 = chunk(wrap(db + 4));
-    d2 = chunk(wrap(db + 8));
-    primed = true;
-  }
-  // genrand_uint32 twice + random_random (53-bit), exact in double (FMA-safe).  Words pos and
-  // pos+1 of the next generation are twisted in place (lazy twist): word 623's successor is
-  // the already-new mt[0], which is what c1.x holds when pos = 622.
   TG_HD double random() {
-#ifdef TG_DIAG_NORNG
-    // DIAGNOSTIC BUILD ONLY (scripts/diag_ablation.py): words from a register hash instead
-    // of the MT state, to price the MT memory traffic.  Never part of the product library.
-    uint32_t z = (pos * 0x9E3779B9u) ^ (uint32_t)(uintptr_t)mt;
-    pos = (pos + 2 == MT_N) ? 0u : pos + 2;
-    z ^= z >> 16; z *= 0x85EBCA6Bu; z ^= z >> 13; z *= 0xC2B2AE35u; z ^= z >> 16;
-    ++draws;
-    return (double)(z >> 5) * (1.0 / 134217728.0);
-#endif
-    if (!primed) prime();
-    uint32_t w0, w1;
-    if ((pos & 2u) == 0u) {
-      w0 = twist(c0.x, c0.y, d0.y);
-      w1 = twist(c0.y, c0.z, d0.z);
-      c0.x = w0;
-      c0.y = w1;
-      pos += 2;
-    } else {
-      w0 = twist(c0.z, c0.w, d0.w);
-      w1 = twist(c0.w, c1.x, d1.x);
-      c0.z = w0;
-      c0.w = w1;
-      *reinterpret_cast<uint4*>(mt + (pos & ~3u)) = c0;  // chunk fully rewritten
-      pos = wrap(pos + 2);
-      c0 = c1;
-      c1 = c2;
-      c2 = chunk(wrap(pos + 8));
-      d0 = d1;
-      d1 = d2;
-      d2 = chunk(wrap((wrap(pos + MT_M) & ~3u) + 8));
+    const uint32_t w0 = mt[pos], w1 = mt[pos + 1];
+    pos += 2;
+    if (pos == (uint32_t)MT_WORDS) pos = 0u;
+    if (pos == 0u || pos == (uint32_t)MT_N) {
+      // entering the other half; a second crossing in one launch finds it stale (two
+      // generations behind): regenerate it from the half just left before reading it
+      if (crossed) twist_gen(mt + (MT_N - pos), mt + pos);
+      crossed = true;
     }
     ++draws;
-    const uint32_t a = temper(w0) >> 5, b = temper(w1) >> 6;
-    return (a * 67108864.0 + b) * (1.0 / 9007199254740992.0);
+    return mt_double(w0, w1);
   }
   // Random.uniform = a + (b-a)*random(); built with -ffp-contract=off (no FMA)
   TG_HD double uniform(double a, double b) { return a + (b - a) * random(); }
-  // write back a half-rewritten chunk; returns the position to store with the env
-  TG_HD uint32_t finish() {
-#ifndef TG_DIAG_NORNG
-    if (primed && (pos & 2u)) *reinterpret_cast<uint4*>(mt + (pos & ~3u)) = c0;
-#endif
-    primed = false;
-    return pos;
-  }
+  TG_HD uint32_t finish() { return pos; }
 };
+// after a launch: regenerate the half a crossing lane left (per-lane form of wave_refill)
+TG_HD void refill_after(uint32_t* mt, uint32_t pos) {
+  twist_gen(mt + mt_half(pos), mt + (MT_N - mt_half(pos)));
+}
 
-// init_by_array([seed lo, seed hi?]) into this env's words; position 0 (see above)
+// init_by_array([seed lo, seed hi?]) into 624 words (CPython's state before its first twist)
 TG_HD void seed_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed) {
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   const uint32_t klen = key1 ? 2u : 1u;
@@ -366,13 +333,15 @@ TG_HD bool is_closed_door_at(const Level& L, const Env& e, int xc, int yc) {
 }
 
 // handle.set_angle_wiggle (OB/:127-131)
-TG_HD void wiggle(Env& e, int h, Rng& rng) {
+template <class R>
+TG_HD void wiggle(Env& e, int h, R& rng) {
   const bool up = (e.f >> (F_OBJ + 3 + h)) & 1u;
   const double a = up ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
   if (h == 0) e.ang0 = a; else e.ang1 = a;
 }
 // set_val of door (OB/:231-235) / handle (OB/:145-149) / bolt (OB/:175-178): apply only
-TG_HD bool set_val(Env& e, int o, int v, Rng& rng) {
+template <class R>
+TG_HD bool set_val(Env& e, int o, int v, R& rng) {
   const uint32_t bit = 1u << (F_OBJ + o);
   if ((((e.f & bit) != 0) ? 1 : 0) == v) return false;
   e.f ^= bit;
@@ -382,7 +351,8 @@ TG_HD bool set_val(Env& e, int o, int v, Rng& rng) {
 // set_val(o0, v0) followed by the process_trigger cascade (OB/:76-94), depth-first in file
 // order with the previously_triggered guard; frames are 8 bits of one u64.  `trig` is the
 // level's [6][2] trigger table (LDS on device).
-TG_HD void cascade(const uint32_t* trig, Env& e, int o0, int v0, Rng& rng) {
+template <class R>
+TG_HD void cascade(const uint32_t* trig, Env& e, int o0, int v0, R& rng) {
   if (!set_val(e, o0, v0, rng)) return;
   uint64_t stack = (uint64_t)(o0 | (v0 << 3));
   uint32_t prev = 1u << o0;
@@ -408,7 +378,8 @@ TG_HD void cascade(const uint32_t* trig, Env& e, int o0, int v0, Rng& rng) {
   }
 }
 // handle.flip (OB/:117-122): uniform(0, 1) <= 0.8 (== random() exactly)
-TG_HD void flip(const uint32_t* trig, Env& e, int h, Rng& rng) {
+template <class R>
+TG_HD void flip(const uint32_t* trig, Env& e, int h, R& rng) {
   if (rng.random() <= 0.8) {
     const int up = (e.f >> (F_OBJ + 3 + h)) & 1u;
     cascade(trig, e, 3 + h, !up, rng);
@@ -425,8 +396,8 @@ constexpr uint32_t PM_ALL = 0x7Fu;
 template <uint32_t PM>
 TG_HD bool may(int prim, int p) { return ((PM >> p) & 1u) && prim == p; }
 
-template <uint32_t PM>
-TG_HD int tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, int prim, Rng& rng) {
+template <uint32_t PM, class R>
+TG_HD int tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, int prim, R& rng) {
   int xd = 0, yd = 0;
   // the action's precondition (IM/:297-319); moves and the jump share one draw site
   bool ok = false;
@@ -674,7 +645,8 @@ TG_HD bool is_done(const Env& e) {
 // reset_game (IM/:55-73): objects re-read (handle angles, 2 draws), start position (gauss
 // pair, 2 draws), empty bag.  Keeps the error bits.
 // ==========================================================================================
-TG_HD void reset_env(const Level& L, Env& e, Rng& rng) {
+template <class R>
+TG_HD void reset_env(const Level& L, Env& e, R& rng) {
   e.f = (e.f & E_MASK) | L.init_flags | F_FACING;
   e.ang0 = ((L.init_flags >> (F_OBJ + 3)) & 1u) ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
   e.ang1 = ((L.init_flags >> (F_OBJ + 4)) & 1u) ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
@@ -704,22 +676,23 @@ struct StepResult {
   int ticks;
 };
 // the while-not-done loop of _Option.run (OP/:28-31) for option K, whose can_run held
-template <int K>
-TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env& e, Rng& rng,
+template <int K, class R>
+TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env& e, R& rng,
                         StepResult& r) {
   r.ran = 1;
   Opt o{0, false, false};
   do {
     const int prim = policy<K>(L, m, e, o);
-    r.reward += tick<prims_of(K)>(L, trig, m, e, prim, rng);
+    r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
     if (++r.ticks >= TICK_CAP) {
       e.f |= E_TICKCAP;
       break;
     }
   } while (!o.done);
 }
+template <class R>
 TG_HD void run_option(const Level& L, const uint32_t* trig, const Map& m, Env& e, int k,
-                      Rng& rng, StepResult& r) {
+                      R& rng, StepResult& r) {
   switch (k) {
     case O_GO_LEFT: run_option_k<O_GO_LEFT>(L, trig, m, e, rng, r); break;
     case O_GO_RIGHT: run_option_k<O_GO_RIGHT>(L, trig, m, e, rng, r); break;
@@ -737,8 +710,9 @@ TG_HD int option_index(int a) {
   if (a < -O_COUNT || a >= O_COUNT) return -1;
   return a < 0 ? a + O_COUNT : a;  // Python negative indexing
 }
+template <class R>
 TG_HD StepResult env_step(const Level& L, const uint32_t* trig, const Map& m, Env& e, int a,
-                          Rng& rng) {
+                          R& rng) {
   StepResult r{0, 0, 0, 0};
   const int k = option_index(a);
   if (k < 0) e.f |= E_ACTION;

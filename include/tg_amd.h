@@ -141,7 +141,9 @@ int tg_stats_reset(tg_batch *h);
 
 /* Raw SoA state copy-out for checkpoints and tests (host buffers, synchronises):
  * pos int32 [N][2], flags u32 [N], objs int32 [N][4] (key cx,cy, gold cx,cy),
- * ang f64 [N][2], mt u32 [N][624], mt_pos u32 [N].  Any pointer may be NULL. */
+ * ang f64 [N][2], mt u32 [N][624], mt_pos u32 [N].  Any pointer may be NULL.
+ * (mt, mt_pos) is the env's random.getstate() equivalent: the current MT19937 generation and
+ * the index into it (CPython's state right after a twist, index 0..623). */
 int tg_read_state(tg_batch *h, int32_t *pos, uint32_t *flags, int32_t *objs, double *ang,
                   uint32_t *mt, uint32_t *mt_pos);
 

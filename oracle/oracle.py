@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "libtg_oracle.so")
 LEVEL_DIR = os.path.join(os.path.dirname(HERE), "gym-treasure-game_amd", "levels", "default")
 
 _lib = None
-_level = None
+_levels = {}
 
 
 def build(force=False):
@@ -65,17 +65,19 @@ def lib():
     return _lib
 
 
-def level():
-    global _level
-    if _level is None:
+def level(level_dir=None):
+    """Parsed level (the reference's three level texts); default = the shipped level."""
+    d = os.path.abspath(level_dir or LEVEL_DIR)
+    if d not in _levels:
         texts = []
         for f in ("domain.txt", "domain-objects.txt", "domain-interactions.txt"):
-            with open(os.path.join(LEVEL_DIR, f), "rb") as fh:
+            with open(os.path.join(d, f), "rb") as fh:
                 texts.append(fh.read())
-        _level = lib().tgo_level_parse(*texts)
-        if not _level:
-            raise RuntimeError("oracle: level parse failed")
-    return _level
+        lv = lib().tgo_level_parse(*texts)
+        if not lv:
+            raise RuntimeError("oracle: level parse failed: %s" % d)
+        _levels[d] = lv
+    return _levels[d]
 
 
 def _p(a):
@@ -85,9 +87,9 @@ def _p(a):
 class OracleEnv:
     """One reference-equivalent env: random.seed(seed); TreasureGame(); reset()."""
 
-    def __init__(self, seed):
+    def __init__(self, seed, level_dir=None):
         self._obs = np.zeros(9, np.float64)
-        self._h = lib().tgo_env_new(level(), seed, _p(self._obs))
+        self._h = lib().tgo_env_new(level(level_dir), seed, _p(self._obs))
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -139,7 +141,7 @@ class OracleEnv:
 
 
 def run(seed_base, g0, n, steps, action_seed, policy=0, autoreset=False, full=True,
-        nthreads=0):
+        nthreads=0, level_dir=None):
     """Batched oracle run. Returns dict of numpy arrays (env-major, t=0 is the reset)."""
     T1 = steps + 1
     out = {}
@@ -152,7 +154,7 @@ def run(seed_base, g0, n, steps, action_seed, policy=0, autoreset=False, full=Tr
     out["hash"] = np.zeros(n, np.uint64)
     out["draws"] = np.zeros(n, np.int64)
     out["ticks"] = np.zeros(n, np.int64)
-    rc = lib().tgo_run(level(), seed_base, g0, n, steps, action_seed, policy, int(autoreset),
+    rc = lib().tgo_run(level(level_dir), seed_base, g0, n, steps, action_seed, policy, int(autoreset),
                        _p(out.get("obs")), _p(out.get("reward")), _p(out.get("valid")),
                        _p(out.get("done")), _p(out.get("final_obs")), _p(out["hash"]),
                        _p(out["draws"]), _p(out["ticks"]), nthreads)

@@ -61,19 +61,23 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
   const Map m{grid.data(), L->W, L->H};
   const uint32_t* trig = &L->trig[0][0];
   const int64_t T1 = (int64_t)steps + 1;
-  std::vector<uint32_t> mt(MT_N);
+  std::vector<uint32_t> mt(MT_WORDS);
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t g = (uint64_t)(g0 + i);
-    seed_mt(mt.data(), gen, seed_base + g);
+    seed_mt(mt.data() + MT_N, gen, seed_base + g);  // k_create, then k_gen_twist x2
+    twist_gen(mt.data() + MT_N, mt.data());
+    twist_gen(mt.data(), mt.data() + MT_N);
     Env e{};
     int64_t ndraws = 0;
-    {  // construct + reset, each a separate launch on the device (k_create, k_reset)
+    {  // construct + reset, each a separate launch on the device (k_reset)
       Rng rng(mt.data(), 0u);
       reset_env(*L, e, rng);
       e.mti = rng.finish();
+      if (rng.crossed) refill_after(mt.data(), e.mti);
       Rng rng2(mt.data(), e.mti);
       reset_env(*L, e, rng2);
       e.mti = rng2.finish();
+      if (rng2.crossed) refill_after(mt.data(), e.mti);
       ndraws += rng.draws + rng2.draws;
     }
     double o[9], fo[9];
@@ -97,7 +101,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
           a = __builtin_ctz(mm);
         }
       }
-      Rng rng(mt.data(), e.mti);  // per step, as each launch rebuilds the register window
+      Rng rng(mt.data(), e.mti);  // per step, as each launch
       const StepResult r = env_step(*L, trig, m, e, a, rng);
       nt += r.ticks;
       observe(*L, e, fo);
@@ -107,6 +111,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
         observe(*L, e, o);
       }
       e.mti = rng.finish();
+      if (rng.crossed) refill_after(mt.data(), e.mti);  // wave_refill after the launch
       ndraws += rng.draws;
       h = rec_hash(h, fo, r.reward, r.ran, r.done);
       const int64_t j = i * T1 + t + 1;
@@ -119,6 +124,28 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
     if (hash) hash[i] = h;
     if (draws) draws[i] = ndraws;  // includes the 8 construct + reset draws
     if (ticks) ticks[i] = nt;
+  }
+  return 0;
+}
+
+// random.seed(seed); then launches[j] calls of random() per "launch", the generation buffer
+// handled as the kernels do (refill after a launch that crossed, in-launch regeneration on a
+// second crossing).  out = every value, in order.
+int hc_rng_stream(uint64_t seed, const int32_t* launches, int nl, double* out) {
+  uint32_t gen[MT_N];
+  gen[0] = 19650218u;
+  for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
+  std::vector<uint32_t> mt(MT_WORDS);
+  seed_mt(mt.data() + MT_N, gen, seed);
+  twist_gen(mt.data() + MT_N, mt.data());
+  twist_gen(mt.data(), mt.data() + MT_N);
+  uint32_t pos = 0;
+  int64_t k = 0;
+  for (int j = 0; j < nl; ++j) {
+    Rng rng(mt.data(), pos);
+    for (int d = 0; d < launches[j]; ++d) out[k++] = rng.random();
+    pos = rng.finish();
+    if (rng.crossed) refill_after(mt.data(), pos);
   }
   return 0;
 }

@@ -1,8 +1,9 @@
-"""The product's per-env core (csrc/tg_core.h: lazy-twist MT, cell-level predicates,
+"""The product's per-env core (csrc/tg_core.h: double-buffered MT generations, cell-level predicates,
 register-stack trigger cascade) compiled for the host, against the golden vectors and the
 oracle.  This is the same code every kernel lane runs; the GPU tests then check the kernels
 themselves (LDS staging, SoA packing, ballots) on the device."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -12,14 +13,24 @@ from conftest import golden
 KEYS = ["obs", "reward", "valid", "done", "final_obs", "hash", "draws", "ticks"]
 
 
-def hc_run(lib, seed_base, g0, n, steps, a0, policy, autoreset):
+CORRIDOR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", "corridor")
+
+
+def level_texts(level_dir):
+    if level_dir is None:
+        return None, None, None
+    return tuple(open(os.path.join(level_dir, f), "rb").read()
+                 for f in ("domain.txt", "domain-objects.txt", "domain-interactions.txt"))
+
+
+def hc_run(lib, seed_base, g0, n, steps, a0, policy, autoreset, level_dir=None):
     t1 = steps + 1
     o = {"obs": np.zeros((n, t1, 9)), "final_obs": np.zeros((n, t1, 9)),
          "reward": np.zeros((n, t1), np.int32), "valid": np.zeros((n, t1), np.uint8),
          "done": np.zeros((n, t1), np.uint8), "hash": np.zeros(n, np.uint64),
          "draws": np.zeros(n, np.int64), "ticks": np.zeros(n, np.int64)}
     p = {k: o[k].ctypes.data_as(ctypes.c_void_p) for k in o}
-    rc = lib.hc_run(None, None, None, seed_base, g0, n, steps, a0, policy, int(autoreset),
+    rc = lib.hc_run(*level_texts(level_dir), seed_base, g0, n, steps, a0, policy, int(autoreset),
                     p["obs"], p["reward"], p["valid"], p["done"], p["final_obs"], p["hash"],
                     p["draws"], p["ticks"])
     assert rc == 0
@@ -83,3 +94,39 @@ def test_core_vs_oracle(hostcheck, oracle, seed_base, g0, n, steps, policy, auto
     np.testing.assert_array_equal(o["ticks"], r["ticks"])
     if autoreset and steps > 1000:
         assert r["done"].sum() > 0
+
+
+@pytest.mark.parametrize("seed", [0, 1, 12345, (1 << 32) + 5])
+@pytest.mark.parametrize("pattern", ["small", "boundaries", "long"])
+def test_rng_generations_vs_cpython(hostcheck, seed, pattern):
+    """tg::Rng's two pre-twisted generations + per-launch refill == CPython's random() stream
+    (Python's own random module IS the reference's generator).  "long" launches cross two and
+    three generation boundaries inside one launch (the in-launch regeneration path)."""
+    import random
+    rs = np.random.default_rng(seed & 0xFFFF)
+    if pattern == "small":
+        launches = rs.integers(0, 9, 600)
+    elif pattern == "boundaries":
+        launches = np.array([312, 312, 1, 311, 312, 2, 310, 312, 312, 624 - 2, 3])
+    else:
+        launches = np.array([5, 313, 700, 1, 950, 0, 312, 1000, 7])
+    launches = launches.astype(np.int32)
+    total = int(launches.sum())
+    out = np.zeros(total)
+    assert hostcheck.hc_rng_stream(seed, launches.ctypes.data_as(ctypes.c_void_p), len(launches),
+                                   out.ctypes.data_as(ctypes.c_void_p)) == 0
+    r = random.Random(seed)
+    want = np.array([r.random() for _ in range(total)])
+    assert np.array_equal(out, want)
+
+
+@pytest.mark.parametrize("policy,autoreset", [(0, False), (1, True)])
+def test_core_vs_oracle_corridor(hostcheck, oracle, policy, autoreset):
+    """Custom level whose go options take ~650 draws in one step (two MT generation crossings
+    inside one launch; tests/golden/levels/corridor/README.md)."""
+    n, steps, a0 = 64, 30, 0xC0FFEE
+    o = hc_run(hostcheck, 3, 0, n, steps, a0, policy, autoreset, level_dir=CORRIDOR)
+    r = oracle.run(3, 0, n, steps, a0, policy, autoreset, level_dir=CORRIDOR)
+    assert_same(o, r)
+    np.testing.assert_array_equal(o["ticks"], r["ticks"])
+    assert r["draws"].max() > 624 * 4  # many multi-generation steps really happened

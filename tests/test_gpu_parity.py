@@ -1,6 +1,8 @@
 """GPU parity: the gfx950 kernels, called through the C ABI (libtg_amd.so), against the
 reference's golden vectors and the CPU oracle.  Bit-exact everywhere: obs compared as f64 bit
 patterns, reward / None / done exactly, draw and tick counts exactly."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -33,11 +35,12 @@ MODES = ["compact", "direct"]
 
 
 def run_gpu(tg, seed_base, g0, n, steps, a0, policy, autoreset, rows=None, hash_only=False,
-            drain_every=0, mode="compact"):
+            drain_every=0, mode="compact", level_dir=None):
     """Drive a TreasureGameVec like tgo_run drives the oracle; returns env-major arrays.
     drain_every > 0 collects the auto-reset episode records every that many steps."""
     pol = "masked" if policy else "uniform"
-    vec = tg.TreasureGameVec(n, seed=seed_base, global_offset=g0, autoreset=autoreset, mode=mode)
+    vec = tg.TreasureGameVec(n, seed=seed_base, global_offset=g0, autoreset=autoreset, mode=mode,
+                             level_dir=level_dir)
     idx = None if rows is None else torch.as_tensor(rows, device=vec.device)
     pick = (lambda t: t) if idx is None else (lambda t: t.index_select(0, idx))
     obs0 = pick(vec.reset()).cpu().numpy()
@@ -270,3 +273,26 @@ def test_modes_identical_full_outputs(tg):
     assert torch.equal(outs[0][0], outs[1][0])
     for k in ("steps", "valid_steps", "ticks", "draws", "episodes"):
         assert outs[0][1][k] == outs[1][1][k], k
+
+
+CORRIDOR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", "corridor")
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("policy,autoreset", [(0, False), (1, True)])
+def test_corridor_multi_generation_steps(tg, oracle, mode, policy, autoreset):
+    """~650 draws per go step: the LDS ring crosses two MT generations inside one launch and
+    must regenerate the second one itself (RngRing::fetch -> regen_half), and the wave refills
+    the rest after the launch (wave_refill).  Bit-exact vs the oracle on the same level."""
+    n, steps, a0 = 192, 40, 0xC0FFEE
+    g = run_gpu(tg, 3, 0, n, steps, a0, policy, autoreset, mode=mode, level_dir=CORRIDOR)
+    r = oracle.run(3, 0, n, steps, a0, policy, autoreset, level_dir=CORRIDOR)
+    for k in ("obs", "final_obs", "reward", "valid", "done"):
+        x, y = g[k], r[k]
+        if x.dtype == np.float64:
+            x, y = x.view(np.uint64), y.view(np.uint64)
+        np.testing.assert_array_equal(x, y, err_msg=k)
+    np.testing.assert_array_equal(g["hash"], r["hash"])
+    assert g["stats"]["draws"] == int(r["draws"].sum()) - 8 * n  # minus construct + reset
+    assert r["draws"].max() > 624 * 4
+    assert g["errors"] == 0
