@@ -29,6 +29,9 @@ using namespace tg;
 namespace {
 
 constexpr int BLOCK = 256;
+#ifndef TG_RING_SLOTS
+#define TG_RING_SLOTS 4
+#endif
 
 thread_local std::string g_err;
 int fail(int code, const char* fmt, ...) {
@@ -110,25 +113,31 @@ __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o
 // ------------------------------------------------------------------------------------------
 // CPython random for the option loops (k_run, k_step): tg::Rng's read-only consumption of the
 // two pre-twisted generations, with a 16-B chunk window in LDS.
-//   Each wave owns a ring [slot 4][lane 64] x 16 B (4 KiB).  Chunk c (words 4c..4c+3, 312
-//   chunks over both halves) sits in slot c % 4 (312 = 4 * 78, so the ring survives the
-//   wrap).  A lane holds chunks c..c+3; when its draw finishes chunk c it fetches chunk c+4
-//   into the freed slot with global_load_lds_dwordx4 (LDS-DMA: no VGPR destination).
+//   Each wave owns a ring [slot R][lane 64] x 16 B.  Chunk c (words 4c..4c+3, 312 chunks over
+//   both halves) sits in slot c % R (312 % R == 0, so the ring survives the wrap).  A lane
+//   reading chunk c holds chunks c .. c+R-2; at its first draw in chunk c (o = 0) it fetches
+//   chunk c+R-1 into the slot of chunk c-1 with global_load_lds_dwordx4 (LDS-DMA: no VGPR
+//   destination).
 //   Why not a register window: one that rotates (c0 = c1; c1 = c2; c2 = load) makes the
 //   compiler copy the freshly loaded chunk at once, i.e. wait for the load it has just issued
 //   (ISA: s_waitcnt vmcnt(1)/(0) after each prefetch), so every shift paid a full HBM
 //   latency.  The DMAs are issued from inline asm, invisible to the compiler's waitcnt pass,
-//   and ordered by hand: "s_waitcnt vmcnt(RING_SLOTS - 2)" before each draw's LDS read.  Why
-//   it suffices: a draw reads chunk c and, at o = 2, nothing else — chunk c was fetched when
-//   the lane finished chunk c-4 (or in prime()), and finishing c-3 and c-2 issued two more
-//   DMAs since; vmcnt counts every VMEM op of the wave in issue order (loads, stores, DMA:
-//   MI355X_MICROARCH.md §vmcnt), so "all but the two youngest done" covers chunk c.
+//   and ordered by hand:
+//   * RAW: "s_waitcnt vmcnt(R-2)" before each draw's LDS read.  Chunk c was fetched at the
+//     first draw of chunk c-R+1 (or in prime(), before chunks c+1..); the lane's fetches at
+//     chunks c-R+2 .. c-1 (R-2 DMAs) were issued after it, and vmcnt counts every VMEM op of
+//     the wave in issue order (MI355X_MICROARCH.md §vmcnt), so "all but the R-2 youngest
+//     done" covers chunk c.
+//   * WAR: a DMA never targets a slot read in the same draw: chunk c-1's slot was last read a
+//     draw earlier, and "s_waitcnt lgkmcnt(0)" before the DMA retires that read (a DMA that
+//     hits in L1 lands in ~150 cycles, possibly before a queued ds_read executes).
 // ------------------------------------------------------------------------------------------
-constexpr int RING_SLOTS = 4;
+constexpr int RING_SLOTS = TG_RING_SLOTS;
 constexpr int RING_SLOT_BYTES = 64 * 16;
-constexpr int RING_WAVE_BYTES = RING_SLOTS * RING_SLOT_BYTES;  // 4 KiB per wave
-constexpr uint32_t MT_CHUNKS = MT_WORDS / 4;                    // 312
+constexpr int RING_WAVE_BYTES = RING_SLOTS * RING_SLOT_BYTES;
+constexpr uint32_t MT_CHUNKS = MT_WORDS / 4;  // 312
 static_assert(MT_CHUNKS % RING_SLOTS == 0, "ring slot of a chunk must survive the wrap");
+static_assert(RING_SLOTS >= 3, "prefetch distance");
 static_assert(RING_WAVE_BYTES >= MT_N * 4, "wave_refill reuses the ring as scratch");
 
 typedef __attribute__((address_space(1))) uint32_t glb_u32;
@@ -151,11 +160,12 @@ __device__ __forceinline__ void glds16(uint32_t m0, const uint32_t* gptr) {
       : "memory");
 }
 // chunk -> its slot of the wave's ring; M0 must be wave-uniform, so one DMA per slot value
+template <int J = 0>
 __device__ __forceinline__ void ring_fetch(uint32_t m0_slot0, uint32_t slot, const uint32_t* g) {
-  if (slot == 0u) glds16(m0_slot0, g);
-  else if (slot == 1u) glds16(m0_slot0 + RING_SLOT_BYTES, g);
-  else if (slot == 2u) glds16(m0_slot0 + 2 * RING_SLOT_BYTES, g);
-  else glds16(m0_slot0 + 3 * RING_SLOT_BYTES, g);
+  if constexpr (J < RING_SLOTS) {
+    if (slot == (uint32_t)J) glds16(m0_slot0 + J * RING_SLOT_BYTES, g);
+    else ring_fetch<J + 1>(m0_slot0, slot, g);
+  }
 }
 
 // the rare second crossing (RngRing::fetch), out of line so that the draw sites stay small
@@ -184,21 +194,35 @@ struct RngRing {
       // the half the lane is in before any of its chunks is fetched (per lane, rare)
       regen_half(mt, c * 4u);
     }
-    ring_fetch(m0, c & (RING_SLOTS - 1), mt + c * 4u);
+    ring_fetch(m0, c % RING_SLOTS, mt + c * 4u);
   }
   __device__ __forceinline__ void prime() {
+    // chunks c .. c+R-2, and c+R-1 too when the first draw is at o = 2 (no o = 0 draw in
+    // chunk c will fetch it); chunk c-1's slot is free
     const uint32_t c = pos >> 2;
 #pragma unroll
-    for (int j = 0; j < RING_SLOTS; ++j) fetch(c + j);
+    for (int j = 0; j < RING_SLOTS - 1; ++j) fetch(c + j);
+    if (pos & 2u) fetch(c + RING_SLOTS - 1);
     primed = true;
   }
   __device__ __forceinline__ double random() {
+#ifdef TG_DIAG_NORNG
+    // DIAGNOSTIC BUILD ONLY (scripts/diag_ablation.py): words from a register hash instead
+    // of the MT buffer, to price the RNG's memory path.  Never part of the product library.
+    uint32_t z = (pos * 0x9E3779B9u) ^ (uint32_t)(uintptr_t)mt;
+    pos = (pos + 2 == (uint32_t)MT_WORDS) ? 0u : pos + 2;
+    z ^= z >> 16; z *= 0x85EBCA6Bu; z ^= z >> 13; z *= 0xC2B2AE35u; z ^= z >> 16;
+    ++draws;
+    return (double)(z >> 5) * (1.0 / 134217728.0);
+#endif
     if (!primed) prime();
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    static_assert(RING_SLOTS - 2 == 2, "the vmcnt above");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING_SLOTS - 2) : "memory");
     const uint32_t c = pos >> 2, o = pos & 2u;
-    const u32x2 w = *(const lds_u2*)((const lds_u32*)(cell + (c & (RING_SLOTS - 1)) * RING_SLOT_BYTES) + o);
-    if (o) fetch(c + RING_SLOTS);  // chunk c done: its slot takes chunk c + 4
+    const u32x2 w = *(const lds_u2*)((const lds_u32*)(cell + (c % RING_SLOTS) * RING_SLOT_BYTES) + o);
+    if (!o) {  // first draw in chunk c: chunk c-1's slot (read a draw ago) takes chunk c+R-1
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      fetch(c + RING_SLOTS - 1);
+    }
     pos += 2;
     if (pos == (uint32_t)MT_WORDS) pos = 0u;
     if (pos == 0u || pos == (uint32_t)MT_N) crossed = true;

@@ -26,7 +26,8 @@ DIAG = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_diag.so")
 def build_diag():
     src = os.path.join(ROOT, "gym-treasure-game_amd", "csrc", "tg_amd.hip")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                           "-ffp-contract=off", "-fPIC", "-shared", "-DTG_DIAG_NORNG", "-o", DIAG,
+                           "-ffp-contract=off", "-fPIC", "-shared", "-DTG_DIAG_NORNG",
+                           "-Wno-bitwise-instead-of-logical", "-o", DIAG,
                            src])
 
 
@@ -54,8 +55,7 @@ def time_variant(lib_path, mode, n, steps, warmup):
 def main():
     n = int(os.environ.get("N", 1 << 20))
     steps, warmup = 60, 10
-    if not os.path.exists(DIAG):
-        build_diag()
+    build_diag()  # always: the product sources may have changed
     prod = _lib.LIB_PATH
     variants = [("prod", prod, "compact"), ("prod", prod, "direct"), ("norng", DIAG, "compact"),
                 ("norng", DIAG, "direct")]

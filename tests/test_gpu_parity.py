@@ -296,3 +296,16 @@ def test_corridor_multi_generation_steps(tg, oracle, mode, policy, autoreset):
     assert g["stats"]["draws"] == int(r["draws"].sum()) - 8 * n  # minus construct + reset
     assert r["draws"].max() > 624 * 4
     assert g["errors"] == 0
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_every_env_hash_vs_oracle(tg, oracle, mode):
+    """Every env of a 262,144-env batch (40 steps, auto-reset) against the oracle, twice in the
+    default mode: the ring's hand-placed waits must hold for every lane under full load, not
+    only for a sample (a race shows up as a handful of envs per million, different per run)."""
+    n, steps, a0 = 1 << 18, 40, 0xC3
+    r = oracle.run(11, 0, n, steps, a0, 0, True, full=False)
+    for rep in range(2 if mode == "compact" else 1):
+        g = run_gpu(tg, 11, 0, n, steps, a0, 0, True, hash_only=True, mode=mode)
+        bad = np.flatnonzero(g["hash"] != r["hash"])
+        assert len(bad) == 0, "run %d: %d envs differ, first %s" % (rep, len(bad), bad[:8].tolist())
