@@ -148,6 +148,16 @@ typedef __attribute__((address_space(3))) u32x2 lds_u2;
 
 // LDS-DMA of one 16-B chunk per active lane into LDS [m0 + lane * 16]; M0 is saved/restored
 __device__ __forceinline__ void glds16(uint32_t m0, const uint32_t* gptr) {
+#ifdef TG_GLDS_NOSAVE
+  asm volatile(
+      "s_mov_b32 m0, %0\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off"
+      :
+      : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
+      : "memory");
+  return;
+#endif
   uint32_t save;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -180,19 +190,22 @@ struct RngRing {
   uint32_t m0;     // LDS address of slot 0 of the wave's ring (wave-uniform)
   uint32_t pos;    // [0, MT_WORDS), even
   uint32_t draws;
-  bool primed, crossed;
+  bool primed, crossed, entered;  // crossed / entered: as tg::Rng
 
-  __device__ __forceinline__ RngRing(uint32_t* m, uint32_t p, lds_u8* wave_ring)
+  __device__ __forceinline__ RngRing(uint32_t* m, uint32_t state, lds_u8* wave_ring)
       : mt(m), cell(wave_ring + (threadIdx.x & 63) * 16),
-        m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_ring)), pos(p), draws(0u),
-        primed(false), crossed(false) {}
+        m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_ring)),
+        pos(state & MT_POS_MASK), draws(0u), primed(false), crossed((state & MT_STALE) != 0u),
+        entered(false) {}
 
   __device__ __forceinline__ void fetch(uint32_t c) {
     if (c >= MT_CHUNKS) c -= MT_CHUNKS;
-    if (crossed && (c == 0u || c == MT_CHUNKS / 2)) {
-      // the lane will enter a second half in this launch: it is stale, regenerate it from
-      // the half the lane is in before any of its chunks is fetched (per lane, rare)
-      regen_half(mt, c * 4u);
+    const uint32_t other = (uint32_t)MT_N - mt_half(pos);
+    if (crossed && c * 4u == other) {
+      // the first chunk of the other half while it is stale (left in this launch, or not yet
+      // refilled since an earlier one): regenerate it from the half the lane is in before
+      // any of its chunks is fetched (per lane, rare)
+      regen_half(mt, other);
     }
     ring_fetch(m0, c % RING_SLOTS, mt + c * 4u);
   }
@@ -225,16 +238,20 @@ struct RngRing {
     }
     pos += 2;
     if (pos == (uint32_t)MT_WORDS) pos = 0u;
-    if (pos == 0u || pos == (uint32_t)MT_N) crossed = true;
+    if (pos == 0u || pos == (uint32_t)MT_N) crossed = entered = true;
     ++draws;
     return mt_double(w.x, w.y);
   }
   __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
-  // drain the DMAs (the ring is reused as scratch); returns the position to store
+  // drain the DMAs (the ring is reused as scratch); returns the state word to store
   __device__ __forceinline__ uint32_t finish() {
     if (primed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     primed = false;
-    return pos;
+    return pos | (crossed ? MT_STALE : 0u);
+  }
+  __device__ __forceinline__ uint32_t finish_queued() {
+    (void)finish();
+    return pos | (entered ? MT_STALE : 0u);
   }
 };
 
@@ -243,42 +260,46 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
   return ((uint64_t)hi << 32) | lo;
 }
-// After a launch, every lane in `need` has left one half of its MT buffer: the wave
-// regenerates it (twist_gen of the half the lane is in), one env at a time, all 64 lanes
-// coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which
-// an earlier 64-word round wrote into the wave's LDS scratch (rounds are >= 3 apart).
-// Must be reached by all 64 lanes of the wave.
-__device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* env_mt, uint32_t pos,
-                                            lds_u32* scratch) {
+// Regenerate one env's stale half with the whole wave: dst = twist_gen(src), 64 words per round,
+// coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
+// earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart).  src / dst are
+// wave-uniform; must be reached by all 64 lanes of the wave.
+__device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, lds_u32* scratch) {
   const int lane = threadIdx.x & 63;
+  constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
+  uint32_t a[ROUNDS], b[ROUNDS], c[4];
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    const int p = r * 64 + lane;
+    a[r] = p < MT_N ? src[p] : 0u;
+    b[r] = p + 1 < MT_N ? src[p + 1] : 0u;
+    if (r < 4) c[r] = p < MT_N - MT_M ? src[p + MT_M] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    const int p = r * 64 + lane;
+    if (p < MT_N) {
+      const uint32_t bb = p + 1 < MT_N ? b[r] : scratch[0];
+      const uint32_t cc = p < MT_N - MT_M ? c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
+      const uint32_t w = mt_twist(a[r], bb, cc);
+      scratch[p] = w;
+      dst[p] = w;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // round r visible to later rounds
+  }
+}
+// For every lane in `need`: regenerate the stale half of its env (the one not holding the
+// position in its state word), one env at a time.  Must be reached by all 64 lanes.
+__device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* env_mt, uint32_t state,
+                                            lds_u32* scratch) {
+  const uint32_t pos = state & MT_POS_MASK;
   const uint64_t src_l = (uint64_t)(uintptr_t)(env_mt + mt_half(pos));
   const uint64_t dst_l = (uint64_t)(uintptr_t)(env_mt + (MT_N - mt_half(pos)));
-  constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
   while (need) {
     const int L = __ffsll((long long)need) - 1;
     need &= need - 1;
-    const glb_u32* src = (const glb_u32*)(uintptr_t)readlane64(src_l, L);
-    glb_u32* dst = (glb_u32*)(uintptr_t)readlane64(dst_l, L);
-    uint32_t a[ROUNDS], b[ROUNDS], c[4];
-#pragma unroll
-    for (int r = 0; r < ROUNDS; ++r) {
-      const int p = r * 64 + lane;
-      a[r] = p < MT_N ? src[p] : 0u;
-      b[r] = p + 1 < MT_N ? src[p + 1] : 0u;
-      if (r < 4) c[r] = p < MT_N - MT_M ? src[p + MT_M] : 0u;
-    }
-#pragma unroll
-    for (int r = 0; r < ROUNDS; ++r) {
-      const int p = r * 64 + lane;
-      if (p < MT_N) {
-        const uint32_t bb = p + 1 < MT_N ? b[r] : scratch[0];
-        const uint32_t cc = p < MT_N - MT_M ? c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
-        const uint32_t w = mt_twist(a[r], bb, cc);
-        scratch[p] = w;
-        dst[p] = w;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // round r visible to later rounds
-    }
+    wave_twist((const glb_u32*)(uintptr_t)readlane64(src_l, L),
+               (glb_u32*)(uintptr_t)readlane64(dst_l, L), scratch);
   }
 }
 
@@ -323,18 +344,15 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
   __shared__ uint32_t scratch[BLOCK / 64][MT_N];
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
-  bool crossed = false;
+  const bool reset = live && (!mask || mask[i]);
   Env e;
+  e.mti = 0u;
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
-    if (!mask || mask[i]) {
+    if (reset) {
       Rng rng(S.mt + i * MT_WORDS, e.mti);
       reset_env(L, e, rng);
       e.mti = rng.finish();
-      crossed = rng.crossed;
-      S.st4[i] = pack(e);
-      S.ang[i] = make_double2(e.ang0, e.ang1);
-      S.ep[i] = make_int2(0, 0);
     }
     if (obs) {
       double o[9];
@@ -342,8 +360,15 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
       store_obs(obs, i, o);
     }
   }
-  wave_refill(__ballot(crossed), S.mt + (live ? i : 0) * MT_WORDS, live ? e.mti : 0u,
+  const bool stale = reset && (e.mti & MT_STALE);
+  wave_refill(__ballot(stale), S.mt + (live ? i : 0) * MT_WORDS, e.mti,
               (lds_u32*)scratch[threadIdx.x >> 6]);
+  if (reset) {
+    e.mti &= ~MT_STALE;
+    S.st4[i] = pack(e);
+    S.ang[i] = make_double2(e.ang0, e.ang1);
+    S.ep[i] = make_int2(0, 0);
+  }
 }
 
 struct StepIO {
@@ -443,7 +468,6 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
   const bool live = i < n;
   StepResult r{0, 0, 0, 0};
   uint32_t draws = 0;
-  bool crossed = false;
   Env e;
   e.mti = 0u;
   int2 ep = make_int2(0, 0);
@@ -455,10 +479,12 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish();
     draws = rng.draws;
-    crossed = rng.crossed;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
-  wave_refill(__ballot(crossed), S.mt + (live ? i : 0) * MT_WORDS, e.mti, (lds_u32*)wring);
+  // one pass, no classify pass after it: regenerate the halves left in this launch now
+  wave_refill(__ballot(live && (e.mti & MT_STALE)), S.mt + (live ? i : 0) * MT_WORDS, e.mti,
+              (lds_u32*)wring);
+  e.mti &= ~MT_STALE;
   if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
   if (live) {
     S.st4[i] = pack(e);
@@ -482,10 +508,13 @@ constexpr int SHARDS = 8;
 constexpr int NSEG = O_COUNT * SHARDS;
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
 struct Work {
-  int32_t* __restrict__ lists;  // [NSEG][shard_cap], segment = option * SHARDS + shard
-  int32_t* __restrict__ ctr;    // [NSEG * CTR_STRIDE]
+  int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = option * SHARDS + shard
+  int32_t* __restrict__ ctr;     // [NSEG * CTR_STRIDE]
+  uint32_t* __restrict__ refill;  // [n]: per classify wave w, slots 64w..: env | source half
+  uint8_t* __restrict__ nrefill;  // [n / 64]: entries of classify wave w (no atomics)
   int64_t shard_cap;
 };
+constexpr int REFILL_BLOCKS = 64;  // k_run workgroups beyond the padded worklists (>= 256 idle waves)
 // worklist order: longest options first (mean ticks, uniform policy: go 56, jumps 36, drops
 // 30, ladders 26, interact 1 — DESIGN.md §3)
 __constant__ int kOrder[O_COUNT] = {O_GO_LEFT,   O_GO_RIGHT,   O_JUMP_LEFT,   O_JUMP_RIGHT,
@@ -499,7 +528,6 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      unsigned long long* __restrict__ stats,
                                                      uint32_t* __restrict__ err_or) {
   __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
-  __shared__ uint32_t scratch[BLOCK / 64][MT_N];
   if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
   LEVEL_IN_LDS();  // includes the barrier
   (void)trig;
@@ -515,6 +543,17 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     unpack_st4(s4, e);  // the angles are only needed if the env finishes here
     k = option_index(io.actions[i]);
     runs = k >= 0 && can_run(L, m, e, k);
+  }
+  // halves left in the previous step (MT_STALE) go on the refill list; k_run's idle waves
+  // regenerate them beside the option loops (a lane that needs one first does it itself)
+  {
+    const bool stale = live && (e.mti & MT_STALE);
+    const unsigned long long b = __ballot(stale);
+    const int64_t wv = i >> 6;
+    if (stale)
+      w.refill[wv * 64 + __popcll(b & ((1ull << lane) - 1ull))] =
+          (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
+    if (lane == 0) w.nrefill[wv] = (uint8_t)__popcll(b);
   }
   // workgroup-local slots: one LDS atomic per wave and option
   int slot = 0;
@@ -540,7 +579,6 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   if (runs) w.lists[(int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot] = (int32_t)i;
 
   int2 ep = make_int2(0, 0);
-  bool crossed = false;
   if (live && !runs) {  // reward None: state unchanged, rows written here
     if (k < 0) e.f |= E_ACTION;
     const double2 a2 = S.ang[i];
@@ -551,13 +589,9 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     Rng rng(S.mt + i * MT_WORDS, e.mti);
     StepResult r{0, 0, (int)dn, 0};
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
-    e.mti = rng.finish();
-    crossed = rng.crossed;
+    e.mti = rng.finish_queued();  // an auto-reset that crosses leaves MT_STALE for the next step
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
-  if (AUTORESET)
-    wave_refill(__ballot(crossed), S.mt + (live ? i : 0) * MT_WORDS, live ? e.mti : 0u,
-                (lds_u32*)scratch[threadIdx.x >> 6]);
   if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, q, stats);
   if (live && !runs) {
     const uint4 s4n = pack(e);
@@ -619,7 +653,6 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   e.mti = 0u;
   int2 ep = make_int2(0, 0);
   uint32_t draws = 0;
-  bool crossed = false;
   lds_u8* const wring = (lds_u8*)ring + (threadIdx.x >> 6) * RING_WAVE_BYTES;
   unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   TG_STAMP(t0);
@@ -635,17 +668,32 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     TG_STAMP(t2);
     r.done = is_done(e);
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
-    e.mti = rng.finish();
+    e.mti = rng.finish_queued();  // MT_STALE if a half was left: the next step refills it
     draws = rng.draws;
-    crossed = rng.crossed;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
-  wave_refill(__ballot(crossed), S.mt + (live ? i : 0) * MT_WORDS, e.mti, (lds_u32*)wring);
   if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
   if (live) {
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
     S.ep[i] = ep;
+  }
+  if (base >= total) {
+    // an idle wave: regenerate stale MT halves listed by k_classify, beside the option loops
+    // (an env's half may also be regenerated by its own lane if it needs it first; both write
+    // the same generation)
+    const int nidle = (int)gridDim.x * (BLOCK / 64) - total / 64;
+    const int nregions = (int)((n + 63) >> 6);  // k_classify's waves
+    for (int r = (base - total) / 64; r < nregions; r += nidle) {
+      const int cnt = w.nrefill[r];
+      for (int j = 0; j < cnt; ++j) {
+        const uint32_t ent = w.refill[(int64_t)r * 64 + j];
+        uint32_t* const env_mt = S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS;
+        const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
+        wave_twist((const glb_u32*)(env_mt + src), (glb_u32*)(env_mt + (MT_N - src)),
+                   (lds_u32*)wring);
+      }
+    }
   }
   block_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0);
 #ifdef TG_DIAG_STAMPS
@@ -781,6 +829,8 @@ struct tg_batch {
   int mode = TG_MODE_COMPACT;
   int32_t* wl = nullptr;   // per-(option, shard) worklists (compact mode)
   int32_t* wctr = nullptr; // sharded counters
+  uint32_t* refill = nullptr;  // stale MT halves to regenerate in k_run (compact mode)
+  uint8_t* nrefill = nullptr;
   int64_t shard_cap = 0;
   bool timing = false;
   std::vector<hipEvent_t> ev;  // (start, stop) pairs
@@ -791,7 +841,7 @@ struct tg_batch {
 namespace {
 int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 // k_run needs one wave per 64-lane chunk of the padded worklists: at most n/64 + NSEG chunks
-int run_grid_for(int64_t n) { return grid_for(n) + (NSEG * 64 + BLOCK - 1) / BLOCK; }
+int run_grid_for(int64_t n) { return grid_for(n) + (NSEG * 64 + BLOCK - 1) / BLOCK + REFILL_BLOCKS; }
 // per-block launch-counter slots cover the largest step grid
 int stat_slots(int64_t n) { return run_grid_for(n); }
 
@@ -885,6 +935,8 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   h->shard_cap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK;
   ALLOC(h->wl, sizeof(int32_t) * NSEG * (size_t)h->shard_cap);
   ALLOC(h->wctr, sizeof(int32_t) * NSEG * CTR_STRIDE);
+  ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63));
+  ALLOC(h->nrefill, (size_t)((n + 63) >> 6));
 #undef ALLOC
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
@@ -912,7 +964,7 @@ void tg_destroy(tg_batch* h) {
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   for (auto ev : h->ev) (void)hipEventDestroy(ev);
   void* bufs[] = {h->grid, h->genrand, h->S.st4, h->S.ang,   h->S.ep, h->S.mt,
-                  h->eps,  h->eps_count, h->stats, h->err, h->wl,   h->wctr};
+                  h->eps,  h->eps_count, h->stats, h->err, h->wl,   h->wctr, h->refill, h->nrefill};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -951,7 +1003,7 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
     hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, h->g0,
                        h->stats, h->err);
   } else {
-    const Work w{h->wl, h->wctr, h->shard_cap};
+    const Work w{h->wl, h->wctr, h->refill, h->nrefill, h->shard_cap};
     HIP_TRY(hipMemsetAsync(h->wctr, 0, sizeof(int32_t) * NSEG * CTR_STRIDE, st));
     auto kc = ar ? (fo ? k_classify<true, true> : k_classify<true, false>)
                  : (fo ? k_classify<false, true> : k_classify<false, false>);

@@ -74,7 +74,7 @@ struct Env {
   uint32_t f;            // flags above
   int kx, ky, gx, gy;    // key / goldcoin cell (OB/:34-38)
   double ang0, ang1;     // handle angles (OB/:111-114)
-  uint32_t mti;          // lazy-twist MT position (0..622, even)
+  uint32_t mti;          // MT state word: position (0..1246, even) | MT_STALE (see Rng)
 };
 
 TG_HD int floordiv(int a, int b) {  // Python // for b > 0
@@ -91,12 +91,16 @@ TG_HD int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v)
 //   position pos in [0, 1248) (always even: random() is the only consumer).  Consumption only
 //   reads: the half holding pos is CPython's mt[] with index pos % 624, and the other half is
 //   always the NEXT generation, so crossing 624 / 1248 continues the stream without a twist.
-//   The half a lane has left is regenerated (twist_gen of the one it is in) after the launch,
-//   by its whole wavefront, coalesced (tg_amd.hip wave_refill).  A launch that would enter a
-//   stale half (a second crossing: > 312 draws in one step) regenerates it first, per lane.
+//   The half a lane has left is stale (two generations behind) until it is regenerated
+//   (twist_gen of the one the lane is in); the env's state word carries MT_STALE meanwhile.
+//   The kernels regenerate it later, a whole wavefront per env, coalesced (tg_amd.hip
+//   wave_refill: the next step's classify pass, or after the launch).  A launch that would
+//   enter a stale half (> 312 draws since the refill) regenerates it first, per lane.
 //   Seeding (init_by_array) fills one half; two twists then give generations 1 and 2, pos 0.
 // ==========================================================================================
 constexpr int MT_WORDS = 2 * MT_N;  // per env
+constexpr uint32_t MT_STALE = 1u << 31;   // state word: the half not holding pos is stale
+constexpr uint32_t MT_POS_MASK = 0xFFFFu;
 constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu;
 
 TG_HD uint32_t mt_twist(uint32_t a, uint32_t b, uint32_t c) {
@@ -129,9 +133,12 @@ struct Rng {
   uint32_t* mt;    // this env's MT_WORDS words
   uint32_t pos;    // [0, MT_WORDS), even
   uint32_t draws;  // random() calls (instrumentation for the roofline)
-  bool crossed;    // entered the other half in this launch: the half left needs a refill
+  bool crossed;    // the half not holding pos is stale (MT_STALE on entry, or entered one)
+  bool entered;    // entered a half in this launch (the one left is stale)
 
-  TG_HD Rng(uint32_t* m, uint32_t p) : mt(m), pos(p), draws(0u), crossed(false) {}
+  TG_HD Rng(uint32_t* m, uint32_t state)
+      : mt(m), pos(state & MT_POS_MASK), draws(0u), crossed((state & MT_STALE) != 0u),
+        entered(false) {}
 
   TG_HD double random() {
     const uint32_t w0 = mt[pos], w1 = mt[pos + 1];
@@ -141,18 +148,23 @@ struct Rng {
       // entering the other half; a second crossing in one launch finds it stale (two
       // generations behind): regenerate it from the half just left before reading it
       if (crossed) twist_gen(mt + (MT_N - pos), mt + pos);
-      crossed = true;
+      crossed = entered = true;
     }
     ++draws;
     return mt_double(w0, w1);
   }
   // Random.uniform = a + (b-a)*random(); built with -ffp-contract=off (no FMA)
   TG_HD double uniform(double a, double b) { return a + (b - a) * random(); }
-  TG_HD uint32_t finish() { return pos; }
+  // the state word to store: position, and whether the other half is stale
+  TG_HD uint32_t finish() const { return pos | (crossed ? MT_STALE : 0u); }
+  // the same when a refill of the half that was stale on entry is already queued
+  TG_HD uint32_t finish_queued() const { return pos | (entered ? MT_STALE : 0u); }
 };
-// after a launch: regenerate the half a crossing lane left (per-lane form of wave_refill)
-TG_HD void refill_after(uint32_t* mt, uint32_t pos) {
-  twist_gen(mt + mt_half(pos), mt + (MT_N - mt_half(pos)));
+// regenerate the stale half (per-lane form of wave_refill); returns the clean state word
+TG_HD uint32_t refill_after(uint32_t* mt, uint32_t state) {
+  const uint32_t pos = state & MT_POS_MASK;
+  if (state & MT_STALE) twist_gen(mt + mt_half(pos), mt + (MT_N - mt_half(pos)));
+  return pos;
 }
 
 // init_by_array([seed lo, seed hi?]) into 624 words (CPython's state before its first twist)

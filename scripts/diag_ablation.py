@@ -20,15 +20,22 @@ sys.path.insert(0, ROOT)
 import gym_treasure_game_amd as tg  # noqa: E402
 from gym_treasure_game_amd import _lib  # noqa: E402
 
-DIAG = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_diag.so")
+VARIANTS = os.environ.get(
+    "VARIANTS", "prod:compact:,prod:direct:,norng:compact:-DTG_DIAG_NORNG,norng:direct:-DTG_DIAG_NORNG")
 
 
-def build_diag():
+def build_variant(name, flags):
+    """Variant libraries: the product sources with extra -D flags (diagnostic builds only)."""
+    if not flags:
+        return _lib.LIB_PATH
+    out = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_%s.so" % name)
+    if os.environ.get("NOBUILD") and os.path.exists(out):
+        return out
     src = os.path.join(ROOT, "gym-treasure-game_amd", "csrc", "tg_amd.hip")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                           "-ffp-contract=off", "-fPIC", "-shared", "-DTG_DIAG_NORNG",
-                           "-Wno-bitwise-instead-of-logical", "-o", DIAG,
-                           src])
+                           "-ffp-contract=off", "-fPIC", "-shared",
+                           "-Wno-bitwise-instead-of-logical"] + flags.split() + ["-o", out, src])
+    return out
 
 
 def time_variant(lib_path, mode, n, steps, warmup):
@@ -55,12 +62,18 @@ def time_variant(lib_path, mode, n, steps, warmup):
 def main():
     n = int(os.environ.get("N", 1 << 20))
     steps, warmup = 60, 10
-    build_diag()  # always: the product sources may have changed
     prod = _lib.LIB_PATH
-    variants = [("prod", prod, "compact"), ("prod", prod, "direct"), ("norng", DIAG, "compact"),
-                ("norng", DIAG, "direct")]
+    variants = []
+    only = os.environ.get("ONLY")
+    for v in VARIANTS.split(","):
+        name, mode, flags = v.split(":", 2)
+        if only and name != only:
+            continue
+        variants.append((name, build_variant(name, flags), mode))
+    if os.environ.get("BUILD_ONLY"):
+        return
     best = {}
-    for _ in range(3):
+    for _ in range(int(os.environ.get("ROUNDS", 3))):
         for name, path, mode in variants:
             r = time_variant(path, mode, n, steps, warmup)
             k = "%s/%s" % (name, mode)

@@ -15,14 +15,16 @@ sys.path.insert(0, ROOT)
 import gym_treasure_game_amd as tg  # noqa: E402
 from gym_treasure_game_amd import _lib  # noqa: E402
 
-SO = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_stamps.so")
+FLAGS = os.environ.get("FLAGS", "").split()
+SO = os.path.join(ROOT, "gym-treasure-game_amd",
+                  "libtg_amd_stamps%s.so" % os.environ.get("TAG", ""))
 
 
 def main():
-    if not os.path.exists(SO):
-        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                               "-ffp-contract=off", "-fPIC", "-shared", "-DTG_DIAG_STAMPS", "-o", SO,
-                               os.path.join(ROOT, "gym-treasure-game_amd", "csrc", "tg_amd.hip")])
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                           "-ffp-contract=off", "-fPIC", "-shared", "-DTG_DIAG_STAMPS",
+                           "-Wno-bitwise-instead-of-logical"] + FLAGS + ["-o", SO,
+                           os.path.join(ROOT, "gym-treasure-game_amd", "csrc", "tg_amd.hip")])
     _lib._lib = None
     _lib.LIB_PATH = SO
     L = _lib.load()
@@ -49,6 +51,11 @@ def main():
                     ("lane eff", sm / 64 / np.maximum(mx, 1))):
         print("%-10s mean %10.1f p50 %10.1f p90 %10.1f max %10.1f" % (
             name, v.mean(), np.median(v), np.percentile(v, 90), v.max()))
+    long = mx >= 80
+    if long.any():
+        v = b[long, 1] / mx[long]
+        print("long waves (>=80 iters): %d, loop/iter mean %.1f p50 %.1f; load mean %.1f epi mean %.1f"
+              % (long.sum(), v.mean(), np.median(v), b[long, 0].mean(), b[long, 2].mean()))
     w = np.flatnonzero(act)
     for lo, hi in ((0, 100), (len(w) // 2, len(w) // 2 + 5), (len(w) - 5, len(w))):
         for k in range(lo, min(hi, len(w)), max(1, (hi - lo) // 5)):

@@ -44,7 +44,7 @@ def hostcheck():
     L.hc_predicates.argtypes = [ctypes.c_int] * 3
     L.hc_predicate_table.argtypes = [ctypes.c_int] * 4 + [ctypes.c_uint, P]
     L.hc_rng_stream.restype = ctypes.c_int
-    L.hc_rng_stream.argtypes = [ctypes.c_uint64, P, ctypes.c_int, P]
+    L.hc_rng_stream.argtypes = [ctypes.c_uint64, P, ctypes.c_int, ctypes.c_int, P]
     return L
 
 

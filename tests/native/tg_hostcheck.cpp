@@ -72,12 +72,10 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
     {  // construct + reset, each a separate launch on the device (k_reset)
       Rng rng(mt.data(), 0u);
       reset_env(*L, e, rng);
-      e.mti = rng.finish();
-      if (rng.crossed) refill_after(mt.data(), e.mti);
+      e.mti = refill_after(mt.data(), rng.finish());  // k_reset refills at once
       Rng rng2(mt.data(), e.mti);
       reset_env(*L, e, rng2);
-      e.mti = rng2.finish();
-      if (rng2.crossed) refill_after(mt.data(), e.mti);
+      e.mti = refill_after(mt.data(), rng2.finish());
       ndraws += rng.draws + rng2.draws;
     }
     double o[9], fo[9];
@@ -101,6 +99,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
           a = __builtin_ctz(mm);
         }
       }
+      e.mti = refill_after(mt.data(), e.mti);  // the classify pass: last step's stale half
       Rng rng(mt.data(), e.mti);  // per step, as each launch
       const StepResult r = env_step(*L, trig, m, e, a, rng);
       nt += r.ticks;
@@ -110,8 +109,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
         reset_env(*L, e, rng);
         observe(*L, e, o);
       }
-      e.mti = rng.finish();
-      if (rng.crossed) refill_after(mt.data(), e.mti);  // wave_refill after the launch
+      e.mti = rng.finish();  // may carry MT_STALE into the next step
       ndraws += rng.draws;
       h = rec_hash(h, fo, r.reward, r.ran, r.done);
       const int64_t j = i * T1 + t + 1;
@@ -129,9 +127,10 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
 }
 
 // random.seed(seed); then launches[j] calls of random() per "launch", the generation buffer
-// handled as the kernels do (refill after a launch that crossed, in-launch regeneration on a
-// second crossing).  out = every value, in order.
-int hc_rng_stream(uint64_t seed, const int32_t* launches, int nl, double* out) {
+// handled as the kernels do: a stale half is refilled before launch j when j % defer == 0
+// (the classify pass), otherwise the launch starts with it stale and must regenerate it
+// itself if it gets there.  out = every value, in order.
+int hc_rng_stream(uint64_t seed, const int32_t* launches, int nl, int defer, double* out) {
   uint32_t gen[MT_N];
   gen[0] = 19650218u;
   for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
@@ -139,13 +138,13 @@ int hc_rng_stream(uint64_t seed, const int32_t* launches, int nl, double* out) {
   seed_mt(mt.data() + MT_N, gen, seed);
   twist_gen(mt.data() + MT_N, mt.data());
   twist_gen(mt.data(), mt.data() + MT_N);
-  uint32_t pos = 0;
+  uint32_t state = 0;
   int64_t k = 0;
   for (int j = 0; j < nl; ++j) {
-    Rng rng(mt.data(), pos);
+    if (defer > 0 && j % defer == 0) state = refill_after(mt.data(), state);
+    Rng rng(mt.data(), state);
     for (int d = 0; d < launches[j]; ++d) out[k++] = rng.random();
-    pos = rng.finish();
-    if (rng.crossed) refill_after(mt.data(), pos);
+    state = rng.finish();
   }
   return 0;
 }

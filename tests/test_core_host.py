@@ -98,10 +98,12 @@ def test_core_vs_oracle(hostcheck, oracle, seed_base, g0, n, steps, policy, auto
 
 @pytest.mark.parametrize("seed", [0, 1, 12345, (1 << 32) + 5])
 @pytest.mark.parametrize("pattern", ["small", "boundaries", "long"])
-def test_rng_generations_vs_cpython(hostcheck, seed, pattern):
-    """tg::Rng's two pre-twisted generations + per-launch refill == CPython's random() stream
-    (Python's own random module IS the reference's generator).  "long" launches cross two and
-    three generation boundaries inside one launch (the in-launch regeneration path)."""
+@pytest.mark.parametrize("defer", [1, 3, 0])
+def test_rng_generations_vs_cpython(hostcheck, seed, pattern, defer):
+    """tg::Rng's two pre-twisted generations == CPython's random() stream (Python's own random
+    module IS the reference's generator).  The stale half is refilled before every launch,
+    every third launch, or never (defer 0: every crossing regenerates in-launch); "long"
+    launches cross two and three generation boundaries inside one launch."""
     import random
     rs = np.random.default_rng(seed & 0xFFFF)
     if pattern == "small":
@@ -114,7 +116,7 @@ def test_rng_generations_vs_cpython(hostcheck, seed, pattern):
     total = int(launches.sum())
     out = np.zeros(total)
     assert hostcheck.hc_rng_stream(seed, launches.ctypes.data_as(ctypes.c_void_p), len(launches),
-                                   out.ctypes.data_as(ctypes.c_void_p)) == 0
+                                   defer, out.ctypes.data_as(ctypes.c_void_p)) == 0
     r = random.Random(seed)
     want = np.array([r.random() for _ in range(total)])
     assert np.array_equal(out, want)
