@@ -81,7 +81,8 @@ struct Soa {
   uint4* st4;
   double2* ang;
   int2* ep;
-  uint32_t* mt;
+  uint32_t* mt;   // [N][MT_WORDS]
+  double* mtd;    // [N][MT_DOUBLES]: the random() values of both generations
 };
 
 // The level in LDS: the bordered cell grid (per-lane indexed probes) and the trigger table
@@ -172,6 +173,10 @@ __device__ __forceinline__ void glds16(uint32_t m0, const uint32_t* gptr) {
 // chunk -> its slot of the wave's ring; M0 must be wave-uniform, so one DMA per slot value
 template <int J = 0>
 __device__ __forceinline__ void ring_fetch(uint32_t m0_slot0, uint32_t slot, const uint32_t* g) {
+#ifdef TG_DIAG_ONEVAR  // DIAGNOSTIC ONLY: one DMA for every lane, wrong slots (prices the variants)
+  glds16(m0_slot0, g);
+  return;
+#endif
   if constexpr (J < RING_SLOTS) {
     if (slot == (uint32_t)J) glds16(m0_slot0 + J * RING_SLOT_BYTES, g);
     else ring_fetch<J + 1>(m0_slot0, slot, g);
@@ -179,24 +184,27 @@ __device__ __forceinline__ void ring_fetch(uint32_t m0_slot0, uint32_t slot, con
 }
 
 // the rare second crossing (RngRing::fetch), out of line so that the draw sites stay small
-__device__ __noinline__ void regen_half(uint32_t* mt, uint32_t h) {
+__device__ __noinline__ void regen_half(uint32_t* mt, double* md, uint32_t h) {
   twist_gen(mt + (MT_N - h), mt + h);
+  gen_doubles(mt + h, md + h / 2);
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
 }
 
 struct RngRing {
-  uint32_t* mt;    // this env's MT_WORDS words (HBM)
+  uint32_t* mt;    // this env's MT_WORDS words (HBM; only to regenerate a stale half)
+  double* md;      // this env's MT_DOUBLES (HBM): what the ring streams
   lds_u8* cell;    // this lane's 16-B cell in slot 0 of the wave's ring
   uint32_t m0;     // LDS address of slot 0 of the wave's ring (wave-uniform)
-  uint32_t pos;    // [0, MT_WORDS), even
+  uint32_t pos;    // [0, MT_WORDS), even: the next draw is double pos / 2
   uint32_t draws;
-  bool primed, crossed, entered;  // crossed / entered: as tg::Rng
+  double nx;       // the next draw, read from the ring one draw ahead
+  bool primed, loaded, crossed, entered;  // crossed / entered: as tg::Rng
 
-  __device__ __forceinline__ RngRing(uint32_t* m, uint32_t state, lds_u8* wave_ring)
-      : mt(m), cell(wave_ring + (threadIdx.x & 63) * 16),
+  __device__ __forceinline__ RngRing(uint32_t* m, double* d, uint32_t state, lds_u8* wave_ring)
+      : mt(m), md(d), cell(wave_ring + (threadIdx.x & 63) * 16),
         m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_ring)),
-        pos(state & MT_POS_MASK), draws(0u), primed(false), crossed((state & MT_STALE) != 0u),
-        entered(false) {}
+        pos(state & MT_POS_MASK), draws(0u), nx(0.0), primed(false), loaded(false),
+        crossed((state & MT_STALE) != 0u), entered(false) {}
 
   __device__ __forceinline__ void fetch(uint32_t c) {
     if (c >= MT_CHUNKS) c -= MT_CHUNKS;
@@ -205,9 +213,18 @@ struct RngRing {
       // the first chunk of the other half while it is stale (left in this launch, or not yet
       // refilled since an earlier one): regenerate it from the half the lane is in before
       // any of its chunks is fetched (per lane, rare)
-      regen_half(mt, other);
+      regen_half(mt, md, other);
     }
-    ring_fetch(m0, c % RING_SLOTS, mt + c * 4u);
+    // chunk c = doubles 2c, 2c+1: the same 16 bytes as words 4c..4c+3 of the word array
+    ring_fetch(m0, c % RING_SLOTS, reinterpret_cast<const uint32_t*>(md) + c * 4u);
+  }
+  // the double at pos from the ring (its chunk has landed: see the vmcnt argument above)
+  __device__ __forceinline__ double ring_read() const {
+#ifndef TG_DIAG_NOWAIT  // DIAGNOSTIC ONLY when defined: no RAW wait (prices it; results wrong)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING_SLOTS - 2) : "memory");
+#endif
+    typedef __attribute__((address_space(3))) double lds_f64;
+    return *(const lds_f64*)(cell + ((pos >> 2) % RING_SLOTS) * RING_SLOT_BYTES + (pos & 2u) * 4u);
   }
   __device__ __forceinline__ void prime() {
     // chunks c .. c+R-2, and c+R-1 too when the first draw is at o = 2 (no o = 0 draw in
@@ -218,10 +235,12 @@ struct RngRing {
     if (pos & 2u) fetch(c + RING_SLOTS - 1);
     primed = true;
   }
+  // random(): returns the value read one draw ago and reads the next one, so the LDS round
+  // trip overlaps the tick in between instead of sitting in the draw's dependency chain
   __device__ __forceinline__ double random() {
 #ifdef TG_DIAG_NORNG
-    // DIAGNOSTIC BUILD ONLY (scripts/diag_ablation.py): words from a register hash instead
-    // of the MT buffer, to price the RNG's memory path.  Never part of the product library.
+    // DIAGNOSTIC BUILD ONLY (scripts/diag_ablation.py): values from a register hash instead
+    // of the MT buffers, to price the RNG's memory path.  Never part of the product library.
     uint32_t z = (pos * 0x9E3779B9u) ^ (uint32_t)(uintptr_t)mt;
     pos = (pos + 2 == (uint32_t)MT_WORDS) ? 0u : pos + 2;
     z ^= z >> 16; z *= 0x85EBCA6Bu; z ^= z >> 13; z *= 0xC2B2AE35u; z ^= z >> 16;
@@ -229,24 +248,33 @@ struct RngRing {
     return (double)(z >> 5) * (1.0 / 134217728.0);
 #endif
     if (!primed) prime();
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING_SLOTS - 2) : "memory");
-    const uint32_t c = pos >> 2, o = pos & 2u;
-    const u32x2 w = *(const lds_u2*)((const lds_u32*)(cell + (c % RING_SLOTS) * RING_SLOT_BYTES) + o);
-    if (!o) {  // first draw in chunk c: chunk c-1's slot (read a draw ago) takes chunk c+R-1
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      fetch(c + RING_SLOTS - 1);
+    if (!loaded) {  // first draw of the launch: the first chunk's DMA must land first
+      nx = ring_read();
+      loaded = true;
     }
+    const double v = nx;
+    const uint32_t c = pos >> 2, o = pos & 2u;
     pos += 2;
     if (pos == (uint32_t)MT_WORDS) pos = 0u;
     if (pos == 0u || pos == (uint32_t)MT_N) crossed = entered = true;
     ++draws;
-    return mt_double(w.x, w.y);
+    // read the next draw BEFORE this draw's fetch: vmcnt counts the wave's VMEM instructions
+    // in issue order, so a wait placed after a fetch would wait for that very fetch
+    nx = ring_read();
+    if (!o) {  // first draw in chunk c: chunk c-1's slot (read draws ago) takes chunk c+R-1
+      asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");  // all but the read just issued
+      const uint32_t p = pos;
+      pos = c * 4u;  // fetch() tests the half of the chunk being read
+      fetch(c + RING_SLOTS - 1);
+      pos = p;
+    }
+    return v;
   }
   __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
   // drain the DMAs (the ring is reused as scratch); returns the state word to store
   __device__ __forceinline__ uint32_t finish() {
-    if (primed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    primed = false;
+    if (primed) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    primed = loaded = false;
     return pos | (crossed ? MT_STALE : 0u);
   }
   __device__ __forceinline__ uint32_t finish_queued() {
@@ -264,7 +292,9 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
 // coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
 // earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart).  src / dst are
 // wave-uniform; must be reached by all 64 lanes of the wave.
-__device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, lds_u32* scratch) {
+typedef __attribute__((address_space(1))) double glb_f64;
+__device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, glb_f64* dst_d,
+                                           lds_u32* scratch) {
   const int lane = threadIdx.x & 63;
   constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
   uint32_t a[ROUNDS], b[ROUNDS], c[4];
@@ -287,19 +317,31 @@ __device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, lds
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // round r visible to later rounds
   }
+  // the generation's 312 random() values
+#pragma unroll
+  for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
+    const int k = r * 64 + lane;
+    if (k < MT_N / 2) {
+      const u32x2 ww = *(const lds_u2*)(scratch + 2 * k);
+      dst_d[k] = mt_double(ww.x, ww.y);
+    }
+  }
 }
 // For every lane in `need`: regenerate the stale half of its env (the one not holding the
 // position in its state word), one env at a time.  Must be reached by all 64 lanes.
-__device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* env_mt, uint32_t state,
-                                            lds_u32* scratch) {
+__device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* env_mt, double* env_md,
+                                            uint32_t state, lds_u32* scratch) {
   const uint32_t pos = state & MT_POS_MASK;
+  const uint32_t dst = MT_N - mt_half(pos);
   const uint64_t src_l = (uint64_t)(uintptr_t)(env_mt + mt_half(pos));
-  const uint64_t dst_l = (uint64_t)(uintptr_t)(env_mt + (MT_N - mt_half(pos)));
+  const uint64_t dst_l = (uint64_t)(uintptr_t)(env_mt + dst);
+  const uint64_t dd_l = (uint64_t)(uintptr_t)(env_md + dst / 2);
   while (need) {
     const int L = __ffsll((long long)need) - 1;
     need &= need - 1;
     wave_twist((const glb_u32*)(uintptr_t)readlane64(src_l, L),
-               (glb_u32*)(uintptr_t)readlane64(dst_l, L), scratch);
+               (glb_u32*)(uintptr_t)readlane64(dst_l, L),
+               (glb_f64*)(uintptr_t)readlane64(dd_l, L), scratch);
   }
 }
 
@@ -334,7 +376,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t 
   __shared__ uint32_t scratch[BLOCK / 64][MT_N];
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
-  wave_refill(__ballot(live), S.mt + (live ? i : 0) * MT_WORDS, from_pos,
+  wave_refill(__ballot(live), S.mt + (live ? i : 0) * MT_WORDS, S.mtd + (live ? i : 0) * MT_DOUBLES, from_pos,
               (lds_u32*)scratch[threadIdx.x >> 6]);
 }
 
@@ -350,7 +392,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
     if (reset) {
-      Rng rng(S.mt + i * MT_WORDS, e.mti);
+      Rng rng(S.mt + i * MT_WORDS, e.mti, S.mtd + i * MT_DOUBLES);
       reset_env(L, e, rng);
       e.mti = rng.finish();
     }
@@ -361,7 +403,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
     }
   }
   const bool stale = reset && (e.mti & MT_STALE);
-  wave_refill(__ballot(stale), S.mt + (live ? i : 0) * MT_WORDS, e.mti,
+  wave_refill(__ballot(stale), S.mt + (live ? i : 0) * MT_WORDS, S.mtd + (live ? i : 0) * MT_DOUBLES, e.mti,
               (lds_u32*)scratch[threadIdx.x >> 6]);
   if (reset) {
     e.mti &= ~MT_STALE;
@@ -474,7 +516,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
-    RngRing rng(S.mt + i * MT_WORDS, e.mti, wring);
+    RngRing rng(S.mt + i * MT_WORDS, S.mtd + i * MT_DOUBLES, e.mti, wring);
     r = env_step(L, trig, m, e, io.actions[i], rng);
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish();
@@ -482,7 +524,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   // one pass, no classify pass after it: regenerate the halves left in this launch now
-  wave_refill(__ballot(live && (e.mti & MT_STALE)), S.mt + (live ? i : 0) * MT_WORDS, e.mti,
+  wave_refill(__ballot(live && (e.mti & MT_STALE)), S.mt + (live ? i : 0) * MT_WORDS,
+              S.mtd + (live ? i : 0) * MT_DOUBLES, e.mti,
               (lds_u32*)wring);
   e.mti &= ~MT_STALE;
   if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
@@ -535,7 +578,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   const bool live = i < n;
   const int lane = threadIdx.x & 63;
   int k = -1;
-  bool runs = false, dn = false;
+  bool runs = false;
   Env e;
   uint4 s4 = make_uint4(0, 0, 0, 0);
   if (live) {
@@ -578,30 +621,35 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   __syncthreads();
   if (runs) w.lists[(int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot] = (int32_t)i;
 
+  // envs whose option cannot run: reward None, state unchanged (TG/:91-96, OP/:22-23)
+  bool dn = false;
   int2 ep = make_int2(0, 0);
-  if (live && !runs) {  // reward None: state unchanged, rows written here
+  uint32_t draws = 0;
+  if (live && !runs) {
     if (k < 0) e.f |= E_ACTION;
     const double2 a2 = S.ang[i];
     e.ang0 = a2.x;
     e.ang1 = a2.y;
     ep = S.ep[i];
     dn = is_done(e);
-    Rng rng(S.mt + i * MT_WORDS, e.mti);
+    Rng rng(S.mt + i * MT_WORDS, e.mti, S.mtd + i * MT_DOUBLES);
     StepResult r{0, 0, (int)dn, 0};
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
-    e.mti = rng.finish_queued();  // an auto-reset that crosses leaves MT_STALE for the next step
+    e.mti = rng.finish_queued();  // the stale half, if any, is on the refill list
+    draws = rng.draws;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, q, stats);
   if (live && !runs) {
     const uint4 s4n = pack(e);
-    if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w) {  // reset / error
+    if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w) {  // reset / flag
       S.st4[i] = s4n;
       S.ang[i] = make_double2(e.ang0, e.ang1);
     }
     S.ep[i] = ep;
   }
-  block_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, AUTORESET ? (live && !runs && dn) : 0);
+  block_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
+              AUTORESET ? (live && !runs && dn) : 0);
 }
 
 #ifdef TG_DIAG_STAMPS
@@ -661,7 +709,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     i = w.lists[(int64_t)(k * SHARDS + sh) * w.shard_cap + idx];
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
-    RngRing rng(S.mt + i * MT_WORDS, e.mti, wring);
+    RngRing rng(S.mt + i * MT_WORDS, S.mtd + i * MT_DOUBLES, e.mti, wring);
     rng.prime();  // issue the ring DMAs now; the first draw comes after the policy setup
     TG_STAMP(t1);
     run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform: one specialised loop
@@ -684,14 +732,16 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     // the same generation)
     const int nidle = (int)gridDim.x * (BLOCK / 64) - total / 64;
     const int nregions = (int)((n + 63) >> 6);  // k_classify's waves
-    for (int r = (base - total) / 64; r < nregions; r += nidle) {
-      const int cnt = w.nrefill[r];
+    for (int rg = (base - total) / 64; rg < nregions; rg += nidle) {
+      // the stale MT halves k_classify listed for these 64 envs
+      const int cnt = w.nrefill[rg];
       for (int j = 0; j < cnt; ++j) {
-        const uint32_t ent = w.refill[(int64_t)r * 64 + j];
-        uint32_t* const env_mt = S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS;
+        const uint32_t ent = w.refill[(int64_t)rg * 64 + j];
+        const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
+        uint32_t* const env_mt = S.mt + env * MT_WORDS;
         const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
         wave_twist((const glb_u32*)(env_mt + src), (glb_u32*)(env_mt + (MT_N - src)),
-                   (lds_u32*)wring);
+                   (glb_f64*)(S.mtd + env * MT_DOUBLES + (MT_N - src) / 2), (lds_u32*)wring);
       }
     }
   }
@@ -927,6 +977,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->S.ang, sizeof(double2) * n);
   ALLOC(h->S.ep, sizeof(int2) * n);
   ALLOC(h->S.mt, sizeof(uint32_t) * MT_WORDS * (size_t)n);
+  ALLOC(h->S.mtd, sizeof(double) * MT_DOUBLES * (size_t)n);
   ALLOC(h->eps, sizeof(tg_episode) * (size_t)h->eps_cap);
   ALLOC(h->eps_count, sizeof(int32_t));
   ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n));
@@ -963,7 +1014,7 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   for (auto ev : h->ev) (void)hipEventDestroy(ev);
-  void* bufs[] = {h->grid, h->genrand, h->S.st4, h->S.ang,   h->S.ep, h->S.mt,
+  void* bufs[] = {h->grid, h->genrand, h->S.st4, h->S.ang,   h->S.ep, h->S.mt, h->S.mtd,
                   h->eps,  h->eps_count, h->stats, h->err, h->wl,   h->wctr, h->refill, h->nrefill};
   for (void* b : bufs)
     if (b) (void)hipFree(b);

@@ -127,6 +127,13 @@ TG_HD void twist_gen(const uint32_t* src, uint32_t* dst) {
   dst[MT_N - 1] = mt_twist(src[MT_N - 1], dst[0], dst[MT_M - 1]);
 }
 TG_HD uint32_t mt_half(uint32_t pos) { return pos >= (uint32_t)MT_N ? (uint32_t)MT_N : 0u; }
+// The kernels' option loops read random() values, not words: every generation is stored twice,
+// as 624 words (for the next twist) and as its 312 random() doubles (MT_DOUBLES per env, half h
+// at h / 2), both written by whoever regenerates the half.
+constexpr int MT_DOUBLES = MT_N;  // 2 x 312
+TG_HD void gen_doubles(const uint32_t* words, double* d) {
+  for (int k = 0; k < MT_N / 2; ++k) d[k] = mt_double(words[2 * k], words[2 * k + 1]);
+}
 
 // Direct-load consumer (few draws per launch: create/reset/classify, and the host checks).
 struct Rng {
@@ -135,10 +142,11 @@ struct Rng {
   uint32_t draws;  // random() calls (instrumentation for the roofline)
   bool crossed;    // the half not holding pos is stale (MT_STALE on entry, or entered one)
   bool entered;    // entered a half in this launch (the one left is stale)
+  double* md;      // the env's MT_DOUBLES (device), kept in step when a half is regenerated
 
-  TG_HD Rng(uint32_t* m, uint32_t state)
+  TG_HD Rng(uint32_t* m, uint32_t state, double* d = nullptr)
       : mt(m), pos(state & MT_POS_MASK), draws(0u), crossed((state & MT_STALE) != 0u),
-        entered(false) {}
+        entered(false), md(d) {}
 
   TG_HD double random() {
     const uint32_t w0 = mt[pos], w1 = mt[pos + 1];
@@ -147,7 +155,10 @@ struct Rng {
     if (pos == 0u || pos == (uint32_t)MT_N) {
       // entering the other half; a second crossing in one launch finds it stale (two
       // generations behind): regenerate it from the half just left before reading it
-      if (crossed) twist_gen(mt + (MT_N - pos), mt + pos);
+      if (crossed) {
+        twist_gen(mt + (MT_N - pos), mt + pos);
+        if (md) gen_doubles(mt + pos, md + pos / 2);
+      }
       crossed = entered = true;
     }
     ++draws;
@@ -161,9 +172,13 @@ struct Rng {
   TG_HD uint32_t finish_queued() const { return pos | (entered ? MT_STALE : 0u); }
 };
 // regenerate the stale half (per-lane form of wave_refill); returns the clean state word
-TG_HD uint32_t refill_after(uint32_t* mt, uint32_t state) {
+TG_HD uint32_t refill_after(uint32_t* mt, uint32_t state, double* md = nullptr) {
   const uint32_t pos = state & MT_POS_MASK;
-  if (state & MT_STALE) twist_gen(mt + mt_half(pos), mt + (MT_N - mt_half(pos)));
+  if (state & MT_STALE) {
+    const uint32_t dst = MT_N - mt_half(pos);
+    twist_gen(mt + mt_half(pos), mt + dst);
+    if (md) gen_doubles(mt + dst, md + dst / 2);
+  }
   return pos;
 }
 
