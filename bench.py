@@ -7,13 +7,13 @@
 
 One "step" = one TreasureGame.step() (TG/:91-96) of EVERY env of the batch: the on-device
 synthetic policy writes the actions (uniform over the 9 options, counter hash keyed by the
-global env index), k_step runs each env's option to completion with auto-reset, completed
-episodes are drained on the device and, for N > 1, all-gathered over RCCL.  Per-GPU work is
-fixed (1,048,576 envs per GPU = config C3, C4 at 8 GPUs), so scaling is weak.  Inputs are
-resident in HBM when the timed region starts.
+global env index), tg_step runs each env's option to completion with auto-reset (k_classify
+then k_run), completed episodes are drained on the device and, for N > 1, all-gathered over
+RCCL.  Per-GPU work is fixed (1,048,576 envs per GPU = config C3, C4 at 8 GPUs), so scaling
+is weak.  Inputs are resident in HBM when the timed region starts.
 
-Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (the step kernel's
-algorithmic bytes per launch over its HIP-event-timed duration vs the 8 TB/s HBM peak) and
+Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (tg_step's kernels:
+algorithmic bytes per launch over their HIP-event-timed duration vs the 8 TB/s HBM peak) and
 ``cpu_baseline`` (the C oracle timed on this box's host cores, a bounded sample).
 """
 import argparse
@@ -32,11 +32,19 @@ METRIC = "env-steps/sec (whole node) at 1M batched envs, 1/2/4/8 MI355X; bit-exa
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ACTION_SEED = 0x5EED0001
 EP_CAP = 4096          # episode records gathered per rank per step (padded)
-# algorithmic bytes of one env-step in k_step:
-#   action 4 + obs 72 + reward 4 + valid 1 + done 1 + state read/write 2 x 40 = 162 per env,
-#   + 24 per random() draw (2 MT words, each: read mt[p], mt[p+397|p-227], write mt[p])
-BYTES_PER_ENV = 162
-BYTES_PER_DRAW = 24
+# algorithmic bytes of one tg_step, per launch:
+#   every env: action 4 + state word 16 read (classify)
+#   reward-None env: angles 16 + episode 8 read; episode 8 + obs 72 + reward/valid/done 6 written
+#   valid env: worklist index 4 + 4, state 16 + 16, angles 16 + 16, episode 8 + 8, obs 72, rows 6
+#   random() draw: one 8-B value (the pre-twisted generation's doubles)
+#   MT regeneration: 624 words read, 624 words + 312 values written
+BYTES_ENV, BYTES_INVALID, BYTES_VALID, BYTES_DRAW, BYTES_REGEN = 20, 110, 166, 8, 7488
+
+
+def alg_bytes(st):
+    inval = st["steps"] - st["valid_steps"]
+    return (BYTES_ENV * st["steps"] + BYTES_INVALID * inval + BYTES_VALID * st["valid_steps"] +
+            BYTES_DRAW * st["draws"] + BYTES_REGEN * st["regens"])
 
 
 def parse():
@@ -53,7 +61,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU-baseline sample (0 disables it)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_step.json"),
-                    help="PMC-derived HBM bytes per k_step launch (profiles/), if measured")
+                    help="PMC-derived HBM bytes per tg_step (profiles/), if measured")
     return ap.parse_args()
 
 
@@ -163,8 +171,8 @@ def main():
         assert node["steps"] == env_steps, (node, env_steps)
         launches = max(st["launches"], 1)
         kern_s = st["kernel_ms"] / 1e3 / launches
-        alg_bytes = (BYTES_PER_ENV * st["steps"] + BYTES_PER_DRAW * st["draws"]) / launches
-        achieved = alg_bytes / kern_s / 1e9
+        alg = alg_bytes(st) / launches
+        achieved = alg / kern_s / 1e9
         traffic = None
         if os.path.exists(args.traffic_json):
             tj = json.load(open(args.traffic_json))
@@ -187,12 +195,14 @@ def main():
             "valid_step_frac": node["valid_steps"] / max(node["steps"], 1),
             "draws_per_step": node["draws"] / max(node["steps"], 1),
             "episodes": node["episodes"], "error_flags": errs,
+            "regens_per_step": st["regens"] / launches,
             "roofline": {"bound": "hbm",
-                         "kernel": "k_classify+k_run" if args.mode == "compact" else "k_step",
+                         "kernel": ("tg_step = k_classify + k_run" if args.mode == "compact"
+                                    else "tg_step = k_step"),
                          "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel_ms": kern_s * 1e3,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg},
         }
         if args.cpu_seconds > 0 and world == 1:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.policy)

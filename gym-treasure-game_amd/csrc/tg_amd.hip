@@ -352,7 +352,7 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
-enum { ST_STEPS, ST_VALID, ST_TICKS, ST_DRAWS, ST_EPISODES, ST_EP_OVERFLOW, ST_COUNT };
+enum { ST_STEPS, ST_VALID, ST_TICKS, ST_DRAWS, ST_EPISODES, ST_EP_OVERFLOW, ST_REGENS, ST_COUNT };
 
 // ------------------------------------------------------------------------------------------
 // kernels
@@ -459,7 +459,8 @@ __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, 
 // (One counter word per launch took ~32k same-line atomics: ~370 us at ~88 atomics/us.)
 // Must be reached by every thread of the block.
 __device__ __forceinline__ void block_stats(unsigned long long* __restrict__ part, int steps,
-                                            int valid, int ticks, int draws, int episodes) {
+                                            int valid, int ticks, int draws, int episodes,
+                                            int regens = 0) {
   __shared__ int acc[5];
   if (threadIdx.x < 5) acc[threadIdx.x] = 0;
   __syncthreads();
@@ -471,6 +472,9 @@ __device__ __forceinline__ void block_stats(unsigned long long* __restrict__ par
     if (s2) atomicAdd(&acc[2], s2);
     if (s3) atomicAdd(&acc[3], s3);
     if (s4) atomicAdd(&acc[4], s4);
+    // wave-uniform counts (one per wave, lane 0): regenerations
+    if (regens) atomicAdd((unsigned long long*)&part[(size_t)blockIdx.x * ST_COUNT + ST_REGENS],
+                          (unsigned long long)regens);
   }
   __syncthreads();
   if (threadIdx.x < 5 && acc[threadIdx.x])
@@ -524,7 +528,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   // one pass, no classify pass after it: regenerate the halves left in this launch now
-  wave_refill(__ballot(live && (e.mti & MT_STALE)), S.mt + (live ? i : 0) * MT_WORDS,
+  const unsigned long long need = __ballot(live && (e.mti & MT_STALE));
+  wave_refill(need, S.mt + (live ? i : 0) * MT_WORDS,
               S.mtd + (live ? i : 0) * MT_DOUBLES, e.mti,
               (lds_u32*)wring);
   e.mti &= ~MT_STALE;
@@ -534,7 +539,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     S.ang[i] = make_double2(e.ang0, e.ang1);
     S.ep[i] = ep;
   }
-  block_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0);
+  block_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
+              __popcll(need));
 }
 
 // ---- two-pass compacted step (TG_MODE_COMPACT) -------------------------------------------
@@ -701,6 +707,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   e.mti = 0u;
   int2 ep = make_int2(0, 0);
   uint32_t draws = 0;
+  int regens = 0;  // wave-uniform
   lds_u8* const wring = (lds_u8*)ring + (threadIdx.x >> 6) * RING_WAVE_BYTES;
   unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   TG_STAMP(t0);
@@ -735,6 +742,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     for (int rg = (base - total) / 64; rg < nregions; rg += nidle) {
       // the stale MT halves k_classify listed for these 64 envs
       const int cnt = w.nrefill[rg];
+      regens += cnt;
       for (int j = 0; j < cnt; ++j) {
         const uint32_t ent = w.refill[(int64_t)rg * 64 + j];
         const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
@@ -745,7 +753,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
       }
     }
   }
-  block_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0);
+  block_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0, regens);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
   {
@@ -1162,6 +1170,7 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   out->episodes_dropped = (int64_t)s[ST_EP_OVERFLOW];
   out->launches = out->steps / (h->n ? h->n : 1);
   out->kernel_ms = h->kernel_ms_done;
+  out->regens = (int64_t)s[ST_REGENS];
   return TG_OK;
 }
 

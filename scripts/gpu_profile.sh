@@ -3,7 +3,7 @@
 # A test failure (rc 1) does not stop the session; any other failure ends it.
 set -u
 OUT=${OUT:-gpurun_out}
-TAG=${TAG:-r01}
+TAG=${TAG:-r01c}
 BENCH_ARGS=${BENCH_ARGS:---steps 100 --warmup 10}
 PMC_ARGS=${PMC_ARGS:---steps 30 --warmup 5 --cpu-seconds 0}
 mkdir -p "$OUT"

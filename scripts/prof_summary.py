@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--envs", type=int, default=1 << 20)
     ap.add_argument("--policy", default="uniform")
+    ap.add_argument("--mode", default="compact")
     a = ap.parse_args()
     res = {"tag": a.tag, "envs": a.envs, "policy": a.policy}
     ks = kernel_stats(os.path.join(a.out, "trace_" + a.tag, "run_kernel_stats.csv"))
@@ -69,35 +70,35 @@ def main():
                 pm.setdefault(k, {}).update(d)
     res["pmc_avg_per_dispatch"] = pm
     res["dispatch_meta"] = meta
-    step = next((k for k in pm if k.startswith("k_step")), None)
-    if step and "k_errors" in pm and "FETCH_SIZE" in pm[step]:
-        known = 16.0 * a.envs  # k_errors: one 16-B uint4 per env
+    # the step's kernels: k_classify + k_run (compact) or k_step (direct)
+    names = (("k_classify", "k_run") if a.mode == "compact" else ("k_step",))
+    step_k = [k for k in pm if k.split("<")[0] in names]
+    if step_k and "k_errors" in pm and all("FETCH_SIZE" in pm[k] for k in step_k):
+        known = 16.0 * a.envs  # k_errors: one 16-B uint4 per env, 16 B per lane
         raw_err = pm["k_errors"]["FETCH_SIZE"] * 1024.0
         cal = known / raw_err if raw_err > 0 else None
-        fetch_raw = pm[step]["FETCH_SIZE"] * 1024.0
-        write = pm[step].get("WRITE_SIZE", 0.0) * 1024.0
-        fetch = fetch_raw * (cal or 1.0)
-        res["hbm"] = {"kernel": step, "fetch_bytes_raw": fetch_raw, "fetch_calibration": cal,
-                      "fetch_bytes": fetch, "write_bytes": write,
-                      "hbm_bytes_per_launch": fetch + write,
-                      "calibration_note": "k_errors reads %d B; FETCH_SIZE reported %.0f B" %
+        per = {}
+        for k in step_k:
+            fr = pm[k]["FETCH_SIZE"] * 1024.0
+            wr = pm[k].get("WRITE_SIZE", 0.0) * 1024.0
+            per[k] = {"fetch_bytes_raw": fr, "fetch_bytes": fr * (cal or 1.0), "write_bytes": wr}
+        tot = sum(v["fetch_bytes"] + v["write_bytes"] for v in per.values())
+        res["hbm"] = {"kernels": per, "fetch_calibration": cal, "hbm_bytes_per_launch": tot,
+                      "calibration_note": "FETCH_SIZE x (16 B/env read by k_errors / its FETCH_SIZE); "
+                                          "k_errors reads %d B, FETCH_SIZE reported %.0f B "
+                                          "(MI355X_MICROARCH.md: wide reads tallied at half)" %
                                           (known, raw_err)}
-        sq = pm[step]
-        if "SQ_INSTS_VALU" in sq and "SQ_WAVES" in sq:
-            res["per_wave"] = {c: sq[c] / sq["SQ_WAVES"] for c in sq if c.startswith("SQ_INSTS")}
-        if "GRBM_GUI_ACTIVE" in sq and step in ks:
-            # GRBM_GUI_ACTIVE sums over the 8 XCDs (MI355X_MICROARCH.md DVFS note)
-            res["effective_clock_ghz"] = sq["GRBM_GUI_ACTIVE"] / 8 / (ks[step]["avg_ns"])
-        tj = {"envs": a.envs, "policy": a.policy, "kernel": step,
-              "hbm_bytes_per_launch": fetch + write, "source": "profiles/%s_summary.json" % a.tag}
+        ns = sum(ks[k]["avg_ns"] for k in ks if k.split("<")[0] in names)
+        res["step_kernels_avg_ns"] = ns
+        tj = {"envs": a.envs, "policy": a.policy, "mode": a.mode, "kernels": sorted(step_k),
+              "hbm_bytes_per_launch": tot, "step_kernels_avg_ns": ns,
+              "source": "profiles/%s_summary.json" % a.tag}
         with open(os.path.join(ROOT, "profiles", "traffic_step.json"), "w") as f:
             json.dump(tj, f, indent=1)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "%s_summary.json" % a.tag), "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps({k: res[k] for k in res if k in ("hbm", "per_wave", "effective_clock_ghz")},
-                     indent=1))
-    print(json.dumps(ks.get(step or "", {}), indent=1))
+    print(json.dumps({k: res[k] for k in res if k in ("hbm", "step_kernels_avg_ns")}, indent=1))
 
 
 if __name__ == "__main__":
