@@ -558,7 +558,8 @@ constexpr int NSEG = O_COUNT * SHARDS;
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
 struct Work {
   int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = option * SHARDS + shard
-  int32_t* __restrict__ ctr;     // [NSEG * CTR_STRIDE]
+  int32_t* __restrict__ ctr;     // [NSEG * CTR_STRIDE], this step's counters
+  int32_t* __restrict__ ctr_next;  // the other parity's, zeroed here for the next step
   uint32_t* __restrict__ refill;  // [n]: per classify wave w, slots 64w..: env | source half
   uint8_t* __restrict__ nrefill;  // [n / 64]: entries of classify wave w (no atomics)
   int64_t shard_cap;
@@ -577,20 +578,32 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      unsigned long long* __restrict__ stats,
                                                      uint32_t* __restrict__ err_or) {
   __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
-  if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
-  LEVEL_IN_LDS();  // includes the barrier
-  (void)trig;
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
   const int lane = threadIdx.x & 63;
+  // every load this lane may need, issued before the level staging and the barriers so their
+  // latencies overlap (the angles / episode words only matter if the option cannot run)
+  uint4 s4 = make_uint4(0, 0, 0, 0);
+  int32_t act = 0;
+  double2 a2 = make_double2(0.0, 0.0);
+  int2 ep = make_int2(0, 0);
+  if (live) {
+    s4 = S.st4[i];
+    act = io.actions[i];
+    a2 = S.ang[i];
+    ep = S.ep[i];
+  }
+  if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < NSEG) w.ctr_next[threadIdx.x * CTR_STRIDE] = 0;
+  LEVEL_IN_LDS();  // includes the barrier
+  (void)trig;
   int k = -1;
   bool runs = false;
   Env e;
-  uint4 s4 = make_uint4(0, 0, 0, 0);
+  e.mti = 0u;
   if (live) {
-    s4 = S.st4[i];
-    unpack_st4(s4, e);  // the angles are only needed if the env finishes here
-    k = option_index(io.actions[i]);
+    unpack_st4(s4, e);
+    k = option_index(act);
     runs = k >= 0 && can_run(L, m, e, k);
   }
   // halves left in the previous step (MT_STALE) go on the refill list; k_run's idle waves
@@ -619,24 +632,22 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     }
   }
   __syncthreads();
+  // the workgroup's worklist ranges: issue the global atomics now, use them after the
+  // reward-None envs are finished (their latency overlaps that work)
   const int shard = blockIdx.x % SHARDS;
+  int my_base = 0;
   if (threadIdx.x < O_COUNT) {
     const int c = bcnt[threadIdx.x];
-    bbase[threadIdx.x] = c ? atomicAdd(&w.ctr[(threadIdx.x * SHARDS + shard) * CTR_STRIDE], c) : 0;
+    my_base = c ? atomicAdd(&w.ctr[(threadIdx.x * SHARDS + shard) * CTR_STRIDE], c) : 0;
   }
-  __syncthreads();
-  if (runs) w.lists[(int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot] = (int32_t)i;
 
   // envs whose option cannot run: reward None, state unchanged (TG/:91-96, OP/:22-23)
   bool dn = false;
-  int2 ep = make_int2(0, 0);
   uint32_t draws = 0;
   if (live && !runs) {
     if (k < 0) e.f |= E_ACTION;
-    const double2 a2 = S.ang[i];
     e.ang0 = a2.x;
     e.ang1 = a2.y;
-    ep = S.ep[i];
     dn = is_done(e);
     Rng rng(S.mt + i * MT_WORDS, e.mti, S.mtd + i * MT_DOUBLES);
     StepResult r{0, 0, (int)dn, 0};
@@ -654,6 +665,9 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     }
     S.ep[i] = ep;
   }
+  if (threadIdx.x < O_COUNT) bbase[threadIdx.x] = my_base;
+  __syncthreads();
+  if (runs) w.lists[(int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot] = (int32_t)i;
   block_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
               AUTORESET ? (live && !runs && dn) : 0);
 }
@@ -889,6 +903,7 @@ struct tg_batch {
   int32_t* wctr = nullptr; // sharded counters
   uint32_t* refill = nullptr;  // stale MT halves to regenerate in k_run (compact mode)
   uint8_t* nrefill = nullptr;
+  int parity = 0;  // which half of wctr this compact step counts in
   int64_t shard_cap = 0;
   bool timing = false;
   std::vector<hipEvent_t> ev;  // (start, stop) pairs
@@ -993,13 +1008,14 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   // a shard holds the envs of every SHARDS-th workgroup
   h->shard_cap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK;
   ALLOC(h->wl, sizeof(int32_t) * NSEG * (size_t)h->shard_cap);
-  ALLOC(h->wctr, sizeof(int32_t) * NSEG * CTR_STRIDE);
+  ALLOC(h->wctr, sizeof(int32_t) * 2 * NSEG * CTR_STRIDE);
   ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63));
   ALLOC(h->nrefill, (size_t)((n + 63) >> 6));
 #undef ALLOC
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
+      hipMemset(h->wctr, 0, sizeof(int32_t) * 2 * NSEG * CTR_STRIDE) != hipSuccess ||
       hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)) != hipSuccess ||
       hipMemset(h->err, 0, sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail(TG_E_HIP, "tg_create: upload failed"));
@@ -1062,8 +1078,12 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
     hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, h->g0,
                        h->stats, h->err);
   } else {
-    const Work w{h->wl, h->wctr, h->refill, h->nrefill, h->shard_cap};
-    HIP_TRY(hipMemsetAsync(h->wctr, 0, sizeof(int32_t) * NSEG * CTR_STRIDE, st));
+    // counters double-buffered by step parity: k_classify zeroes the next step's set (the
+    // previous k_run, which read it, has finished), so no memset launch per step
+    int32_t* const cur = h->wctr + (h->parity ? NSEG * CTR_STRIDE : 0);
+    int32_t* const nxt = h->wctr + (h->parity ? 0 : NSEG * CTR_STRIDE);
+    h->parity ^= 1;
+    const Work w{h->wl, cur, nxt, h->refill, h->nrefill, h->shard_cap};
     auto kc = ar ? (fo ? k_classify<true, true> : k_classify<true, false>)
                  : (fo ? k_classify<false, true> : k_classify<false, false>);
     auto kr = ar ? (fo ? k_run<true, true> : k_run<true, false>)

@@ -83,6 +83,22 @@ TG_HD int floordiv(int a, int b) {  // Python // for b > 0
 }
 TG_HD int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Pixel -> cell in the tick loops.  A 32-bit division by the constant 48 compiles to 32-bit
+// magic-number multiplies (v_mul_hi_u32 / v_mul_lo_u32, slower VALU); 24-bit operands take
+// the full-rate v_mul_u32_u24 instead.  v * 21846 >> 20 equals v / 48 for 0 <= v < 32,700
+// (21846 / 2^20 - 1/48 = 6.4e-7; 6.4e-7 * 32,700 < 1/48) — levels are at most 124 cells
+// (5,952 px) per side with the border.
+static_assert(S == 48, "div48 constants");
+TG_HD uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TG_NO_MUL24)
+  return __umul24(a, b);
+#else
+  return a * b;
+#endif
+}
+TG_HD int div48(int v) { return (int)(mul24((uint32_t)v, 21846u) >> 20); }  // 0 <= v < 32,700
+TG_HD int floordiv48(int a) { return div48(a + 16 * S) - 16; }              // -768 <= a < 31,900
+
 // ==========================================================================================
 // CPython random over two pre-twisted generations.
 //   CPython (_randommodule.c genrand_uint32) regenerates all 624 words at once ("twist")
@@ -228,13 +244,13 @@ struct Map {
   TG_HD uint32_t cellb(int cx, int cy) const {
     cx = clampi(cx, -PAD, W + PAD - 1);
     cy = clampi(cy, -PAD, H + PAD - 1);
-    return g[(cy + PAD) * pw() + cx + PAD];
+    return g[mul24((uint32_t)(cy + PAD), (uint32_t)pw()) + cx + PAD];
   }
   // object_type_at (IM/:218-225) as cell bits
   TG_HD uint32_t atb(int x, int y) const {
     x = clampi(x, -PAD * S, (W + PAD) * S - 1) + PAD * S;
     y = clampi(y, -PAD * S, (H + PAD) * S - 1) + PAD * S;
-    return g[(int)((unsigned)y / S) * pw() + (int)((unsigned)x / S)];
+    return g[mul24((uint32_t)div48(y), (uint32_t)pw()) + div48(x)];
   }
   // door state -> type: `dc` = closed-door bits (f >> F_OBJ) & 7
   static TG_HD bool is_open(uint32_t c, uint32_t dc) {
@@ -497,8 +513,8 @@ TG_HD int tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, int p
 // Options (MO/)
 // ==========================================================================================
 TG_HD void player_cell(const Env& e, int& xc, int& yc) {  // IM/:441-445
-  xc = floordiv(e.px, S);
-  yc = floordiv(e.py + S / 2, S);
+  xc = floordiv48(e.px);  // floordiv(px, S); players stay inside the level
+  yc = floordiv48(e.py + S / 2);
 }
 // close_enough_to / close_enough_x: |tx*48 + 24 - px| < 4 (MO/:69-72 and its copies)
 TG_HD bool close_x(const Env& e, int txc) {

@@ -28,6 +28,8 @@ def build_variant(name, flags):
     """Variant libraries: the product sources with extra -D flags (diagnostic builds only)."""
     if not flags:
         return _lib.LIB_PATH
+    if flags.startswith("@"):  # a prebuilt library, e.g. an earlier commit's (A/B)
+        return os.path.join(ROOT, flags[1:])
     out = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_%s.so" % name)
     if os.environ.get("NOBUILD") and os.path.exists(out):
         return out
