@@ -674,7 +674,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
 
 #ifdef TG_DIAG_STAMPS
 // DIAGNOSTIC BUILD ONLY (scripts/diag_stamps.py): per-wave s_memtime stamps of k_run
-__device__ unsigned long long g_stamps[(1 << 16) * 4];
+__device__ unsigned long long g_stamps[(1 << 16) * 6];  // per wave: 4 durations/counts + 100 MHz start, end
 #define TG_STAMP(v) v = __builtin_amdgcn_s_memtime()
 #else
 #define TG_STAMP(v) (void)0
@@ -725,6 +725,9 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   lds_u8* const wring = (lds_u8*)ring + (threadIdx.x >> 6) * RING_WAVE_BYTES;
   unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   TG_STAMP(t0);
+#ifdef TG_DIAG_STAMPS
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   (void)t0; (void)t1; (void)t2; (void)t3;
   if (live) {
     i = w.lists[(int64_t)(k * SHARDS + sh) * w.shard_cap + idx];
@@ -779,11 +782,14 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     const unsigned long long a1 = __shfl(t1, src, 64);
     const unsigned long long a2 = __shfl(t2, src, 64);
     const int wv = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    const unsigned long long rt3 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0 && bl && wv < (1 << 16)) {
-      g_stamps[wv * 4 + 0] = a1 - t0;
-      g_stamps[wv * 4 + 1] = a2 - a1;
-      g_stamps[wv * 4 + 2] = t3 - a2;
-      g_stamps[wv * 4 + 3] = (unsigned long long)mx | ((unsigned long long)sum << 32);
+      g_stamps[wv * 6 + 0] = a1 - t0;
+      g_stamps[wv * 6 + 1] = a2 - a1;
+      g_stamps[wv * 6 + 2] = t3 - a2;
+      g_stamps[wv * 6 + 3] = (unsigned long long)mx | ((unsigned long long)sum << 32);
+      g_stamps[wv * 6 + 4] = rt0;
+      g_stamps[wv * 6 + 5] = rt3;
     }
   }
 #endif
@@ -1246,7 +1252,7 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
 int tg_diag_stamps(unsigned long long* out, int n_waves) {
   if (n_waves > (1 << 16)) n_waves = 1 << 16;
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * n_waves));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 6 * n_waves));
   return TG_OK;
 }
 #endif

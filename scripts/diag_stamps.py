@@ -36,7 +36,7 @@ def main():
         vec.step(vec.policy_actions(t))
     torch.cuda.synchronize()
     nw = n // 64
-    buf = np.zeros((nw, 4), np.uint64)
+    buf = np.zeros((nw, 6), np.uint64)
     vec.stats_reset()
     vec.step(vec.policy_actions(999))
     torch.cuda.synchronize()
@@ -56,6 +56,22 @@ def main():
         v = b[long, 1] / mx[long]
         print("long waves (>=80 iters): %d, loop/iter mean %.1f p50 %.1f; load mean %.1f epi mean %.1f"
               % (long.sum(), v.mean(), np.median(v), b[long, 0].mean(), b[long, 2].mean()))
+    # timeline (s_memrealtime, 100 MHz, chip-wide)
+    st = buf[act, 4].astype(np.int64)
+    en = buf[act, 5].astype(np.int64)
+    t0 = st.min()
+    st_us, en_us = (st - t0) / 100.0, (en - t0) / 100.0
+    span = en_us.max()
+    print("span %.1f us; waves started by: 10%% %.1f 50%% %.1f 90%% %.1f 100%% %.1f us"
+          % (span, *np.percentile(st_us, [10, 50, 90, 100])))
+    print("waves ended by: 10%% %.1f 50%% %.1f 90%% %.1f 99%% %.1f 100%% %.1f us"
+          % tuple(np.percentile(en_us, [10, 50, 90, 99, 100])))
+    for t in np.linspace(0, span, 11):
+        print("  t=%6.1f us active waves %5d" % (t, ((st_us <= t) & (en_us > t)).sum()))
+    top = np.argsort(-en_us)[:10]
+    for j in top:
+        print("  last: start %.1f end %.1f us iters %d loop cyc/iter %.0f" % (
+            st_us[j], en_us[j], mx[j], b[j, 1] / max(mx[j], 1)))
     w = np.flatnonzero(act)
     for lo, hi in ((0, 100), (len(w) // 2, len(w) // 2 + 5), (len(w) - 5, len(w))):
         for k in range(lo, min(hi, len(w)), max(1, (hi - lo) // 5)):
