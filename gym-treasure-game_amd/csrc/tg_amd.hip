@@ -787,7 +787,8 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
       g_stamps[wv * 6 + 0] = a1 - t0;
       g_stamps[wv * 6 + 1] = a2 - a1;
       g_stamps[wv * 6 + 2] = t3 - a2;
-      g_stamps[wv * 6 + 3] = (unsigned long long)mx | ((unsigned long long)sum << 32);
+      g_stamps[wv * 6 + 3] = (unsigned long long)mx | ((unsigned long long)sum << 32) |
+                             ((unsigned long long)k << 56);
       g_stamps[wv * 6 + 4] = rt0;
       g_stamps[wv * 6 + 5] = rt3;
     }

@@ -31,7 +31,10 @@ constexpr int INCR = S / 10;   // x_incr / y_incr (IM/:46-47)
 constexpr int HALFW = S / 4;   // player_width // 2 (IM/:49)
 constexpr int MT_N = 624, MT_M = 397;
 constexpr int TICK_CAP = 1 << 14;  // the reference has no cap (OP/:28-31); observed max 105
-constexpr int PAD = 2;             // WALL cells around the grid in LDS (probes reach <= 60 px out)
+constexpr int PAD = 2;
+#ifndef TG_FULL_BATCH
+#define TG_FULL_BATCH 64  // lanes that must be waiting before a go wave runs the full tick
+#endif             // WALL cells around the grid in LDS (probes reach <= 60 px out)
 
 // Cell bits in the LDS grid.  A door object's cell carries only its one-hot door bit: its type
 // is 'D' or ' ' by the door's state (update_map overwrites whatever the file had there).
@@ -246,6 +249,9 @@ struct Map {
     cy = clampi(cy, -PAD, H + PAD - 1);
     return g[mul24((uint32_t)(cy + PAD), (uint32_t)pw()) + cx + PAD];
   }
+  // the cell column / row atb() probes for pixel x / y (clamped into the WALL border)
+  TG_HD int colx(int x) const { return div48(clampi(x, -PAD * S, (W + PAD) * S - 1) + PAD * S) - PAD; }
+  TG_HD int rowy(int y) const { return div48(clampi(y, -PAD * S, (H + PAD) * S - 1) + PAD * S) - PAD; }
   // object_type_at (IM/:218-225) as cell bits
   TG_HD uint32_t atb(int x, int y) const {
     x = clampi(x, -PAD * S, (W + PAD) * S - 1) + PAD * S;
@@ -431,6 +437,20 @@ TG_HD void flip(const uint32_t* trig, Env& e, int h, R& rng) {
   }
 }
 
+// pickups in object order: key then goldcoin (IM/:350-354)
+TG_HD void pickups(const Level& L, Env& e) {
+  if (near_cell(e, e.kx, e.ky, R2_OBJ)) {
+    e.kx = L.W - 1 - bag_len(e.f);
+    e.ky = L.H - 1;
+    bag_push(e.f, false);
+  }
+  if (near_cell(e, e.gx, e.gy, R2_OBJ)) {
+    e.gx = L.W - 1 - bag_len(e.f);
+    e.gy = L.H - 1;
+    bag_push(e.f, true);
+  }
+}
+
 // ==========================================================================================
 // Primitive tick: _TreasureGameImpl.step (IM/:290-359).  PM is the set of primitive actions
 // the caller can issue (a compile-time mask); the others compile away.
@@ -495,17 +515,7 @@ TG_HD int tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, int p
     }
   }
   e.py += yd;
-  // pickups in object order: key then goldcoin (IM/:350-354)
-  if (near_cell(e, e.kx, e.ky, R2_OBJ)) {
-    e.kx = L.W - 1 - bag_len(e.f);
-    e.ky = L.H - 1;
-    bag_push(e.f, false);
-  }
-  if (near_cell(e, e.gx, e.gy, R2_OBJ)) {
-    e.gx = L.W - 1 - bag_len(e.f);
-    e.gy = L.H - 1;
-    bag_push(e.f, true);
-  }
+  pickups(L, e);
   return may<PM>(prim, P_JUMP) ? -5 : -1;  // JUMP_REWARD / STEP_REWARD (IM/:15-16)
 }
 
@@ -718,12 +728,126 @@ struct StepResult {
   int done;    // got gold and back in row 0
   int ticks;
 };
+// ==========================================================================================
+// Plain go ticks.  While a go option walks on flat ground, its tick (policy MO/:74-85 +
+// IM/:290-359) probes the same cells and finds: not close to the target, side clear, no
+// jump ticker, no fall, no object in reach.  Such a tick is exactly: one draw, px += the
+// noisy step, facing set, reward -1.  go_plain_limit() returns how far px may go in the
+// direction of motion with all of those facts unchanged (INT_MIN / INT_MAX: not at all):
+//   * the probed columns px + 16*dir (can_go_side) and px -/+ 10 (can_fall) stay in their
+//     48-px cells (rows fixed: py does not change);
+//   * close_x: |T - px| >= 4 until 4 px short of the target centre T;
+//   * near_cell(key | gold): dx^2 + dy^2 < 24^2 needs |dx| < 24, so an object whose row is
+//     within reach bounds the span 24 px short of its centre.
+// Motion is monotonic (steps of 2-4 px in dir), so one bound per fact suffices.  A plain
+// tick whose step leaves the span checks the pickups at its new px as the full tick does;
+// the next tick is a full one, which computes the next span.
+// ==========================================================================================
+template <int DIR>
+TG_HD int go_plain_limit(const Map& m, const Env& e, int tx) {
+  constexpr int NONE = DIR > 0 ? -0x40000000 : 0x40000000;
+  if ((e.f & F_JT) || !m.can_go_side(e, DIR) || m.can_fall(e) || close_x(e, tx)) return NONE;
+  const int P = e.px;
+  // target and objects (px never reaches them inside the span)
+  const int T = tx * S + S / 2;
+  int lim = DIR > 0 ? T - INCR : T + INCR;
+  const int ocx[2] = {e.kx, e.gx}, ocy[2] = {e.ky, e.gy};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int dy = e.py - ocy[j] * S;
+    if (dy * dy >= R2_OBJ) continue;
+    const int X = ocx[j] * S + S / 2;
+    if ((P - X < 0 ? X - P : P - X) < S / 2) return NONE;
+    if (DIR > 0 && X > P) lim = min(lim, X - S / 2);
+    if (DIR < 0 && X < P) lim = max(lim, X + S / 2);
+  }
+  if (DIR > 0 ? lim < P : lim > P) return NONE;
+  // the probed rows are fixed (py does not change in the span)
+  const uint32_t dc = Map::dc_of(e.f);
+  const int rs1 = m.rowy(e.py + INCR), rs2 = m.rowy(e.py + S - INCR);  // can_go_side
+  const int rf1 = m.rowy(e.py), rf2 = m.rowy(e.py + S + 2);            // can_fall
+  // can_go_side(p) reads column colx(p + 16*dir): the span ends before the first column ahead
+  // whose two cells hold a WALL or a closed door
+  {
+    const int off = DIR * (HALFW + INCR);
+    const int c0 = m.colx(P + off), c1 = m.colx(lim + off);
+    for (int c = c0 + DIR; DIR > 0 ? c <= c1 : c >= c1; c += DIR) {
+      const uint32_t ta = m.cellb(c, rs1), tb = m.cellb(c, rs2);
+      if (Map::is_wall(ta | tb) | Map::is_door(ta, dc) | Map::is_door(tb, dc)) {
+        // first p with colx(p + off) == c
+        lim = DIR > 0 ? min(lim, c * S - off - 1) : max(lim, c * S + S - 1 - off + 1);
+        break;
+      }
+    }
+  }
+  // can_fall(p) = F(colx(p - 10)) & F(colx(p + 10)), F(c) = both probed cells OPEN: the span
+  // ends before the first p ahead where the leading column and the trailing one are both F
+  {
+    const int d = HALFW - 2;  // 10
+    const int lead0 = m.colx(P + DIR * d), lead1 = m.colx(lim + DIR * d);
+    bool fprev = Map::is_open(m.cellb(lead0, rf1), dc) & Map::is_open(m.cellb(lead0, rf2), dc);
+    if (fprev) {  // the trailing probe (not F now: can_fall is false) reaches lead0
+      const int p_both = DIR > 0 ? lead0 * S + d : lead0 * S + S - 1 - d;
+      lim = DIR > 0 ? min(lim, p_both - 1) : max(lim, p_both + 1);
+    }
+    for (int c = lead0 + DIR; DIR > 0 ? c <= lead1 : c >= lead1; c += DIR) {
+      const bool fc = Map::is_open(m.cellb(c, rf1), dc) & Map::is_open(m.cellb(c, rf2), dc);
+      if (fc) {
+        // the leading probe enters c at p_in; the trailing one reaches c at p_both
+        const int p_in = DIR > 0 ? c * S - d : c * S + S - 1 + d;
+        const int p_both = DIR > 0 ? c * S + d : c * S + S - 1 - d;
+        const int p = fprev ? p_in : p_both;
+        lim = DIR > 0 ? min(lim, p - 1) : max(lim, p + 1);
+        break;
+      }
+      fprev = fc;
+    }
+  }
+  return lim;
+}
+
 // the while-not-done loop of _Option.run (OP/:28-31) for option K, whose can_run held
 template <int K, class R>
 TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env& e, R& rng,
                         StepResult& r) {
   r.ran = 1;
   Opt o{0, false, false};
+#ifndef TG_NO_PLAIN
+  if constexpr (K == O_GO_LEFT || K == O_GO_RIGHT) {
+    constexpr int DIR = K == O_GO_LEFT ? -1 : 1;
+    int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
+    do {
+      const bool plain = DIR > 0 ? e.px <= lim : e.px >= lim;
+      // A lane whose next tick must be a full one waits until enough lanes of the wave do
+      // (or none can take a plain tick): each lane's own tick sequence is unchanged, only the
+      // interleaving across lanes, so the wave runs the full tick's code rarely.
+#ifdef __HIP_DEVICE_COMPILE__
+      const unsigned long long want = __ballot(!plain), can = __ballot(plain);
+      const bool run_full = !plain && (__popcll(want) >= TG_FULL_BATCH || can == 0ull);
+#else
+      const bool run_full = !plain;
+#endif
+      if (plain) {  // a plain tick (see go_plain_limit)
+        const double rr = rng.random();
+        e.px += (int)rint((DIR < 0 ? -4.0 : 2.0) + 2.0 * rr);
+        e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
+        r.reward += -1;
+        if (DIR > 0 ? e.px > lim : e.px < lim) pickups(L, e);  // left the span: as the full tick
+      } else if (run_full) {
+        const int prim = policy<K>(L, m, e, o);
+        r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
+        if (!o.done) lim = go_plain_limit<DIR>(m, e, o.tx);
+      } else {
+        continue;  // waits for the batch (no tick)
+      }
+      if (++r.ticks >= TICK_CAP) {
+        e.f |= E_TICKCAP;
+        break;
+      }
+    } while (!o.done);
+    return;
+  }
+#endif
   do {
     const int prim = policy<K>(L, m, e, o);
     r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);

@@ -44,7 +44,8 @@ def main():
     act = buf[:, 3] > 0
     b = buf[act].astype(np.float64)
     mx = (buf[act, 3] & 0xFFFFFFFF).astype(np.float64)
-    sm = (buf[act, 3] >> 32).astype(np.float64)
+    sm = ((buf[act, 3] >> 32) & 0xFFFFFF).astype(np.float64)
+    kk = (buf[act, 3] >> 56).astype(np.int64)
     print("active waves", act.sum(), "of", nw)
     for name, v in (("load", b[:, 0]), ("loop", b[:, 1]), ("epilogue", b[:, 2]),
                     ("loop/iter", b[:, 1] / np.maximum(mx, 1)), ("max ticks", mx),
@@ -68,6 +69,14 @@ def main():
           % tuple(np.percentile(en_us, [10, 50, 90, 99, 100])))
     for t in np.linspace(0, span, 11):
         print("  t=%6.1f us active waves %5d" % (t, ((st_us <= t) & (en_us > t)).sum()))
+    names = ["go_left", "go_right", "up_ladder", "down_ladder", "interact", "down_left",
+             "down_right", "jump_left", "jump_right"]
+    for k in range(9):
+        sel = kk == k
+        if sel.any():
+            print("  %-11s waves %5d end max %6.1f us p90 %6.1f  iters max %4d mean %5.1f  cyc/iter %6.0f"
+                  % (names[k], sel.sum(), en_us[sel].max(), np.percentile(en_us[sel], 90),
+                     mx[sel].max(), mx[sel].mean(), (b[sel, 1] / np.maximum(mx[sel], 1)).mean()))
     top = np.argsort(-en_us)[:10]
     for j in top:
         print("  last: start %.1f end %.1f us iters %d loop cyc/iter %.0f" % (
