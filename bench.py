@@ -15,6 +15,10 @@ is weak.  Inputs are resident in HBM when the timed region starts.
 Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (tg_step's kernels:
 algorithmic bytes per launch over their HIP-event-timed duration vs the 8 TB/s HBM peak) and
 ``cpu_baseline`` (the C oracle timed on this box's host cores, a bounded sample).
+
+``--workload c5`` is config C5 instead: 65,536 envs per GPU whose step also renders every
+env's screen (ObservationWrapper, TG/:38-51: tg_render -> k_render, 1,257,984 B per frame,
+synthetic sprite sheet); its roofline is k_render's frame bytes over its HIP-event time.
 """
 import argparse
 import json
@@ -39,6 +43,9 @@ EP_CAP = 4096          # episode records gathered per rank per step (padded)
 #   random() draw: one 8-B value (the pre-twisted generation's doubles)
 #   MT regeneration: 624 words read, 624 words + 312 values written
 BYTES_ENV, BYTES_INVALID, BYTES_VALID, BYTES_DRAW, BYTES_REGEN = 20, 110, 166, 8, 7488
+# algorithmic bytes of one k_render launch per env: the frame written (H*48 x W*48 x 3 =
+# 1,257,984 for the default level) + the env's state words read (st4 16 + angles 16)
+BYTES_RENDER_STATE = 32
 
 
 def alg_bytes(st):
@@ -52,7 +59,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--envs", type=int, default=1 << 20, help="envs per GPU")
+    ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
+                    help="c3: vector-obs step (default, the headline); c5: step + RGB render")
+    ap.add_argument("--envs", type=int, default=None,
+                    help="envs per GPU (default 1,048,576 for c3, 65,536 for c5)")
     ap.add_argument("--policy", default="uniform", choices=["uniform", "masked"])
     ap.add_argument("--no-autoreset", action="store_true")
     ap.add_argument("--mode", default="compact", choices=["compact", "direct"],
@@ -90,8 +100,38 @@ def cpu_baseline(seconds, policy):
             "reference_python_1core_measured_in_build_container": 14400.0}
 
 
+def cpu_baseline_render(seconds, policy):
+    """C5's CPU leg: the oracle's renderer restatement (plus construct/reset and one step per
+    env) on this box's host cores, synthetic sprites."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O  # noqa: E402 — bench's cpu_baseline leg only
+    from gym_treasure_game_amd.render import synthetic_sprites
+    O.build()
+    cores = len(os.sched_getaffinity(0))
+    threads = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    pol = 1 if policy == "masked" else 0
+    sprites = synthetic_sprites(seed=1)
+    n = threads * 4
+    t0 = time.perf_counter()
+    O.run_render(0, np.arange(n), 1, ACTION_SEED, pol, True, sprites, nthreads=threads)
+    dt = time.perf_counter() - t0
+    n = int(min(max(n, n * seconds / max(dt, 1e-3)), 20000))
+    t0 = time.perf_counter()
+    O.run_render(0, np.arange(n), 1, ACTION_SEED, pol, True, sprites, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "env-steps/s (rendered frames/s)", "cores": threads,
+            "kind": "port",
+            "sample": "C oracle renderer (oracle/tg_oracle.c tgo_run_render: construct, reset, 1 "
+                      "%s step, render('rgb_array')) for envs 0..%d, %d OpenMP threads, %.1f s"
+                      % (policy, n - 1, threads, dt)}
+
+
 def main():
     args = parse()
+    c5 = args.workload == "c5"
+    if args.envs is None:
+        args.envs = 65536 if c5 else 1 << 20
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -130,10 +170,24 @@ def main():
     pol = tg._lib.TG_POLICY_MASKED if args.policy == "masked" else tg._lib.TG_POLICY_UNIFORM
     args_step = (h, p(act), p(obs), p(rew), p(val), p(don), None, flags, stream)
 
+    frames, rev = None, []
+    if c5:  # ObservationWrapper.step: render every env's screen after its step
+        vec.render_init(tg.synthetic_sprites(seed=1))
+        frames = torch.empty((count,) + vec.frame_shape, dtype=torch.uint8, device=dev)
+    timing = [False]
+
     def one_step(t):
         tg._lib.check(L.tg_policy_actions(h, ACTION_SEED, t, pol, p(act), stream), "actions")
         tg._lib.check(L.tg_step(*args_step), "tg_step")
         tg._lib.check(L.tg_episodes(h, p(ep_rows), p(ep_cnt), EP_CAP, stream), "episodes")
+        if c5:
+            if timing[0]:  # k_render alone, on the stream it is launched on
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            tg._lib.check(L.tg_render(h, 0, count, p(frames), stream), "tg_render")
+            if timing[0]:
+                ev[1].record()
+                rev.append(ev)
         if world > 1:  # the one collective: completed episodes over RCCL/xGMI
             dist.all_gather_into_tensor(all_cnt, ep_cnt)
             dist.all_gather_into_tensor(all_rows, ep_rows)
@@ -143,6 +197,7 @@ def main():
     torch.cuda.synchronize(dev)
     vec.stats_reset()
     vec.set_timing(True)
+    timing[0] = True
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -179,15 +234,43 @@ def main():
             if (tj.get("envs") == args.envs and tj.get("policy") == args.policy
                     and tj.get("mode", "direct") == args.mode):
                 traffic = tj.get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm",
+                "kernel": ("tg_step = k_classify + k_run" if args.mode == "compact"
+                           else "tg_step = k_step"),
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic, "kernel_ms": kern_s * 1e3,
+                "alg_bytes_per_launch": alg}
+        workload = ("C3/C4: %d batched treasure_game-v0 envs per GPU, vector obs, %s random "
+                    "options, auto-reset%s" % (args.envs, args.policy,
+                                               " + RCCL episode gather" if world > 1 else ""))
+        extra = {}
+        if c5:
+            fh, fw, _ = vec.frame_shape
+            r_ms = sum(a.elapsed_time(b) for a, b in rev) / max(len(rev), 1)
+            r_alg = count * (fh * fw * 3 + BYTES_RENDER_STATE)
+            r_ach = r_alg / (r_ms / 1e3) / 1e9
+            r_traffic = None
+            tj_path = os.path.join(ROOT, "profiles", "traffic_render.json")
+            if os.path.exists(tj_path):
+                tj = json.load(open(tj_path))
+                if tj.get("envs") == count:
+                    r_traffic = tj.get("hbm_bytes_per_launch")
+            extra["step_roofline"] = roof
+            roof = {"bound": "hbm", "kernel": "k_render (tg_render)", "achieved": r_ach,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r_ach / HBM_PEAK_GBS,
+                    "traffic": r_traffic, "kernel_ms": r_ms, "alg_bytes_per_launch": r_alg}
+            workload = ("C5: %d batched treasure_game-v0 envs per GPU, ObservationWrapper RGB "
+                        "render (%dx%dx3 u8 frames, synthetic sprites) after every step, %s "
+                        "random options, auto-reset" % (args.envs, fh, fw, args.policy))
+            extra["frames_per_s"] = env_steps / dt
+            extra["frame_bytes"] = fh * fw * 3
         line = {
             "metric": METRIC, "value": env_steps / dt, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "int32+f64", "data": "synthetic",
-            "config": {"workload": "C3/C4: %d batched treasure_game-v0 envs per GPU, vector obs, "
-                                   "%s random options, auto-reset%s"
-                                   % (args.envs, args.policy,
-                                      " + RCCL episode gather" if world > 1 else ""),
+            "config": {"workload": workload,
                        "envs_per_gpu": args.envs, "total_envs": total, "policy": args.policy,
                        "autoreset": autoreset, "step_mode": args.mode,
                        "parallelism": "env-shard x%d" % world},
@@ -196,16 +279,12 @@ def main():
             "draws_per_step": node["draws"] / max(node["steps"], 1),
             "episodes": node["episodes"], "error_flags": errs,
             "regens_per_step": st["regens"] / launches,
-            "roofline": {"bound": "hbm",
-                         "kernel": ("tg_step = k_classify + k_run" if args.mode == "compact"
-                                    else "tg_step = k_step"),
-                         "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel_ms": kern_s * 1e3,
-                         "alg_bytes_per_launch": alg},
+            "roofline": roof,
         }
+        line.update(extra)
         if args.cpu_seconds > 0 and world == 1:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.policy)
+            line["cpu_baseline"] = (cpu_baseline_render if c5 else cpu_baseline)(
+                args.cpu_seconds, args.policy)
         print(json.dumps(line), flush=True)
     vec.close()
     if world > 1:

@@ -9,7 +9,9 @@ there is no CPU fallback.  Registration with gym / gymnasium happens on import w
 installed, mirroring gym_treasure_game/__init__.py:3-6.
 """
 from ._lib import TgError  # noqa: F401
-from .envs import OPTION_NAMES, STATE_NAMES, TreasureGame, TreasureGameVec, read_level  # noqa: F401
+from .envs import (OPTION_NAMES, STATE_NAMES, ObservationWrapper, TreasureGame,  # noqa: F401
+                   TreasureGameVec, read_level)
+from .render import load_sprites, synthetic_sprites  # noqa: F401
 
 __version__ = "0.1.0"
 ENV_ID = "treasure_game-v0"

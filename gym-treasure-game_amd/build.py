@@ -10,9 +10,10 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "tg_amd.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "tg_core.h"), os.path.join(HERE, "csrc", "tg_level.h"),
-        os.path.join(os.path.dirname(HERE), "include", "tg_amd.h")]
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("tg_amd.hip", "tg_render.hip")]
+DEPS = SRCS + [os.path.join(HERE, "csrc", f) for f in ("tg_core.h", "tg_level.h", "tg_batch.h",
+                                                        "tg_render.h")] + [
+    os.path.join(os.path.dirname(HERE), "include", "tg_amd.h")]
 OUT = os.path.join(HERE, "libtg_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
@@ -29,7 +30,7 @@ def needs_build():
 def build(force=False, verbose=False):
     if not force and not needs_build():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC]
+    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp"] + SRCS
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

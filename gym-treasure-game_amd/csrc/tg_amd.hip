@@ -23,7 +23,11 @@
 #include "../../include/tg_amd.h"
 #include "tg_core.h"
 #include "tg_level.h"
+#include "tg_batch.h"
 
+namespace tg {
+thread_local std::string g_err;
+}
 using namespace tg;
 
 namespace {
@@ -32,22 +36,6 @@ constexpr int BLOCK = 256;
 #ifndef TG_RING_SLOTS
 #define TG_RING_SLOTS 4
 #endif
-
-thread_local std::string g_err;
-int fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
-#define HIP_TRY(expr)                                                                    \
-  do {                                                                                   \
-    hipError_t e_ = (expr);                                                              \
-    if (e_ != hipSuccess) return fail(TG_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
-  } while (0)
 
 // ------------------------------------------------------------------------------------------
 // SoA pack / unpack
@@ -76,14 +64,6 @@ __device__ __forceinline__ uint4 pack(const Env& e) {
   s.w = e.mti;
   return s;
 }
-
-struct Soa {
-  uint4* st4;
-  double2* ang;
-  int2* ep;
-  uint32_t* mt;   // [N][MT_WORDS]
-  double* mtd;    // [N][MT_DOUBLES]: the random() values of both generations
-};
 
 // The level in LDS: the bordered cell grid (per-lane indexed probes) and the trigger table
 // (indexed per lane by the cascade; kernel arguments indexed per lane would be vector loads
@@ -888,55 +868,12 @@ __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4,
 
 }  // namespace
 
-// ------------------------------------------------------------------------------------------
-// handle
-// ------------------------------------------------------------------------------------------
-struct tg_batch {
-  int device = 0;
-  int64_t n = 0;
-  int64_t g0 = 0;
-  uint64_t seed0 = 0;
-  Level L{};
-  uint32_t* grid = nullptr;  // bordered cell grid, padded to whole words
-  uint32_t* genrand = nullptr;
-  Soa S{};
-  tg_episode* eps = nullptr;
-  int32_t* eps_count = nullptr;
-  int32_t eps_cap = 0;
-  unsigned long long* stats = nullptr;  // ST_COUNT
-  uint32_t* err = nullptr;
-  int mode = TG_MODE_COMPACT;
-  int32_t* wl = nullptr;   // per-(option, shard) worklists (compact mode)
-  int32_t* wctr = nullptr; // sharded counters
-  uint32_t* refill = nullptr;  // stale MT halves to regenerate in k_run (compact mode)
-  uint8_t* nrefill = nullptr;
-  int parity = 0;  // which half of wctr this compact step counts in
-  int64_t shard_cap = 0;
-  bool timing = false;
-  std::vector<hipEvent_t> ev;  // (start, stop) pairs
-  size_t ev_used = 0;
-  double kernel_ms_done = 0.0;
-};
-
 namespace {
 int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 // k_run needs one wave per 64-lane chunk of the padded worklists: at most n/64 + NSEG chunks
 int run_grid_for(int64_t n) { return grid_for(n) + (NSEG * 64 + BLOCK - 1) / BLOCK + REFILL_BLOCKS; }
 // per-block launch-counter slots cover the largest step grid
 int stat_slots(int64_t n) { return run_grid_for(n); }
-
-int bind(const tg_batch* h) {
-  int cur = -1;
-  HIP_TRY(hipGetDevice(&cur));
-  if (cur != h->device) HIP_TRY(hipSetDevice(h->device));
-  return TG_OK;
-}
-#define BIND(h)                       \
-  do {                                \
-    if (!(h)) return fail(TG_E_INVAL, "null handle"); \
-    int rc_ = bind(h);                \
-    if (rc_) return rc_;              \
-  } while (0)
 
 int flush_timing(tg_batch* h) {
   for (size_t k = 0; k + 1 < h->ev_used; k += 2) {
@@ -952,7 +889,7 @@ int flush_timing(tg_batch* h) {
 
 extern "C" {
 
-const char* tg_last_error(void) { return g_err.c_str(); }
+const char* tg_last_error(void) { return tg::g_err.c_str(); }
 const char* tg_version(void) { return "tg_amd 0.1 gfx950"; }
 int64_t tg_num_envs(const tg_batch* h) { return h ? h->n : 0; }
 
@@ -987,6 +924,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   h->g0 = global_offset;
   h->seed0 = seed_base;
   h->L = L;
+  h->domain = dom;
   // completed-episode queue: drained by tg_episodes; records beyond it are counted as dropped
   const int64_t cap = 4 * n > (1 << 16) ? 4 * n : (1 << 16);
   h->eps_cap = (int32_t)(cap < (1 << 28) ? cap : (1 << 28));
@@ -1045,6 +983,7 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   for (auto ev : h->ev) (void)hipEventDestroy(ev);
+  render_free(h->rs);
   void* bufs[] = {h->grid, h->genrand, h->S.st4, h->S.ang,   h->S.ep, h->S.mt, h->S.mtd,
                   h->eps,  h->eps_count, h->stats, h->err, h->wl,   h->wctr, h->refill, h->nrefill};
   for (void* b : bufs)

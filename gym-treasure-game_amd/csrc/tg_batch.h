@@ -1,0 +1,90 @@
+// tg_batch.h — the handle behind include/tg_amd.h, shared by the step (tg_amd.hip) and render
+// (tg_render.hip) translation units of libtg_amd.so.  Internal: not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/tg_amd.h"
+#include "tg_core.h"
+
+namespace tg {
+
+extern thread_local std::string g_err;  // tg_last_error() text (tg_amd.hip)
+inline int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+inline int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) return fail(TG_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+struct Soa {
+  uint4* st4;
+  double2* ang;
+  int2* ep;
+  uint32_t* mt;   // [N][MT_WORDS]
+  double* mtd;    // [N][MT_DOUBLES]: the random() values of both generations
+};
+
+struct RenderState;  // tg_render.hip
+void render_free(RenderState* rs);
+
+}  // namespace tg
+
+// the handle (tg_amd.h tg_batch)
+struct tg_batch {
+  int device = 0;
+  int64_t n = 0;
+  int64_t g0 = 0;
+  uint64_t seed0 = 0;
+  tg::Level L{};
+  uint32_t* grid = nullptr;  // bordered cell grid, padded to whole words
+  uint32_t* genrand = nullptr;
+  tg::Soa S{};
+  tg_episode* eps = nullptr;
+  int32_t* eps_count = nullptr;
+  int32_t eps_cap = 0;
+  unsigned long long* stats = nullptr;  // ST_COUNT
+  uint32_t* err = nullptr;
+  int mode = TG_MODE_COMPACT;
+  int32_t* wl = nullptr;   // per-(option, shard) worklists (compact mode)
+  int32_t* wctr = nullptr; // sharded counters
+  uint32_t* refill = nullptr;  // stale MT halves to regenerate in k_run (compact mode)
+  uint8_t* nrefill = nullptr;
+  int parity = 0;  // which half of wctr this compact step counts in
+  int64_t shard_cap = 0;
+  bool timing = false;
+  std::vector<hipEvent_t> ev;  // (start, stop) pairs
+  size_t ev_used = 0;
+  double kernel_ms_done = 0.0;
+  std::string domain;              // domain.txt text (the renderer's cell sprites)
+  tg::RenderState* rs = nullptr;   // tg_render_init
+};
+
+namespace tg {
+inline int bind(const tg_batch* h) {
+  int cur = -1;
+  HIP_TRY(hipGetDevice(&cur));
+  if (cur != h->device) HIP_TRY(hipSetDevice(h->device));
+  return TG_OK;
+}
+#define BIND(h)                       \
+  do {                                \
+    if (!(h)) return fail(TG_E_INVAL, "null handle"); \
+    int rc_ = bind(h);                \
+    if (rc_) return rc_;              \
+  } while (0)
+
+}  // namespace tg

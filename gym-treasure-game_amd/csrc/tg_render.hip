@@ -1,0 +1,191 @@
+// tg_render.hip — TreasureGame.render('rgb_array') for a whole batch (tg_render_init /
+// tg_render / tg_frame_shape of include/tg_amd.h).
+//
+// Reference: TG/:98-105 render() -> _TreasureGameDrawer.draw_domain (DR/:136-163) and
+// draw_object (DR/:238-269); ObservationWrapper (TG/:38-51) renders after every reset/step.
+// DR/ = _treasure_game_impl/_treasure_game_drawer.py.
+//
+// A frame is the env's screen as RGB bytes, [H*48][W*48][3] (surfarray.array3d().swapaxes(0,1)).
+// It splits into
+//   * a STATIC layer, identical for every env and every step: black, then one 48x48 sprite per
+//     description cell — wall or floor (a wall under a non-wall) or background, each a
+//     Random(12).choice over 5 variants in row-major cell order (draw_domain reseeds the
+//     generator every frame, DR/:137), ladders fixed.  Built once on the host at
+//     tg_render_init and kept in HBM (a few MB, L2-resident while the kernel streams);
+//   * a DYNAMIC layer of <= 9 items drawn over it in the reference's order: the 8 objects in
+//     file order (3 doors open/closed, 2 handles = 5-px shaft + r=4 knob + base sprite, key
+//     and gold unless moved off-screen, bolt open/locked), then the hero (mirrored when facing
+//     left).  They cover ~6 % of the pixels.
+// k_render: one workgroup per (env, band of 48 pixel rows), one wave per row, one lane per
+// 16-B chunk of the row's RGB bytes (coalesced, every byte of the frame written exactly once).
+// A chunk that no dynamic item touches is a 16-B copy of the static layer; the others
+// composite their 6 pixels in draw order and repack.  The kernel is HBM-write bound:
+// 1,257,984 B per frame of the default level.
+//
+// The per-chunk composition and the static-layer construction live in tg_render.h (shared
+// with the host-only check build); the pixel rules are listed there.  PARITY UNPINNED against
+// the reference (pygame is absent here); pinned against the oracle's restatement.
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "tg_batch.h"
+#include "tg_level.h"
+#include "tg_render.h"
+
+namespace tg {
+
+constexpr int RBLOCK = 256;  // 4 waves, one pixel row each
+
+struct RenderState {
+  int Wpx = 0, Hpx = 0, CH = 0;  // pixels, 16-B chunks per row
+  uint4* bg = nullptr;           // static layer, RGB bytes [Hpx][Wpx*3]
+  uint32_t* bg32 = nullptr;      // static layer, XRGB [Hpx][Wpx]
+  uint32_t* spr = nullptr;       // [D_COUNT][48*48] ARGB
+  uint64_t knob = 0;             // knob half widths + 1, 4 bits per row dy = -4..4
+};
+
+void render_free(RenderState* rs) {
+  if (!rs) return;
+  void* bufs[] = {rs->bg, rs->bg32, rs->spr};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  delete rs;
+}
+
+namespace {
+
+#ifndef TG_RENDER_NT
+#define TG_RENDER_NT 1  // non-temporal frame stores (streamed once, never re-read here)
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void store16(uint4* p, const uint4 x) {
+  u32x4 v = {x.x, x.y, x.z, x.w};
+#if TG_RENDER_NT
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+#else
+  *reinterpret_cast<u32x4*>(p) = v;
+#endif
+}
+
+// block = (env, band of 48 rows); wave w renders rows w, w+4, ... of the band, lane l the
+// 16-B chunks l, l+64, ... of the row
+__global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __restrict__ st4,
+                                                   const double2* __restrict__ angs,
+                                                   int64_t first, uint4* __restrict__ out) {
+  __shared__ Layer lay[NLAYER];
+  __shared__ uint32_t live_mask;
+  const int64_t e = blockIdx.x / A.H;
+  const int band = (int)(blockIdx.x - e * A.H);
+  const int ylo = band * RS;
+  if (threadIdx.x < 64) {
+    bool live = false;
+    if (threadIdx.x < NLAYER) {
+      Layer l;
+      const uint32_t err = make_layer(A, threadIdx.x, st4[first + e], angs[first + e], l, live);
+      if (err) atomicOr(A.err, err);
+      live = live && l.y1 > ylo && l.y0 < ylo + RS && l.x1 > 0 && l.x0 < A.Wpx;
+      lay[threadIdx.x] = l;
+    }
+    const uint64_t b = __ballot(live);
+    if (threadIdx.x == 0) live_mask = (uint32_t)b;
+  }
+  __syncthreads();
+  const uint32_t lm = live_mask;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint4* const frame = out + (e * (int64_t)A.Hpx) * A.CH;
+  for (int r = wave; r < RS; r += RBLOCK / 64) {
+    const int y = ylo + r;
+    const uint32_t rm = row_items(lay, lm, y);  // wave-uniform
+    const uint4* src = A.bg + (int64_t)y * A.CH;
+    uint4* dst = frame + (int64_t)y * A.CH;
+    for (int q = lane; q < A.CH; q += 64) {
+      const uint32_t hit = rm ? chunk_items(lay, rm, q) : 0u;
+      const uint4 v = hit ? compose_chunk(A, lay, hit, y, q) : src[q];
+      store16(dst + q, v);
+    }
+  }
+}
+
+}  // namespace
+}  // namespace tg
+
+using namespace tg;
+
+extern "C" {
+
+int tg_render_init(tg_batch* h, const uint8_t* sprites, int32_t sw, int32_t sh) {
+  BIND(h);
+  if (!sprites || sw <= 0 || sh <= 0 || sw > 4096 || sh > 4096)
+    return fail(TG_E_INVAL, "tg_render_init: bad sprite sheet");
+  // description cells (get_file_description, IM/:180-202)
+  std::vector<std::string> desc;
+  for (auto& l : lines_of(h->domain.c_str())) desc.push_back(strip(l));
+  while (!desc.empty() && desc.back().empty()) desc.pop_back();
+  const int W = h->L.W, H = h->L.H, Wpx = W * RS, Hpx = H * RS;
+  if ((int)desc.size() != H) return fail(TG_E_INVAL, "tg_render_init: level text mismatch");
+  // handle shafts + knobs must stay on the surface: x - 5 .. x + 53, y + 8 .. y + 50 (angles
+  // in [0, 1]: end point within 26 px across and 12..36 px above the pivot (x + 24, y + 48))
+  for (int k = 0; k < 2; ++k) {
+    const int x = h->L.handle_cx[k] * RS, y = h->L.handle_cy[k] * RS;
+    if (x - 6 < 0 || x + 55 > Wpx || y + 52 > Hpx)
+      return fail(TG_E_INVAL, "tg_render_init: handle %d's shaft would leave the screen", k);
+  }
+  const std::vector<uint32_t> sc = scale_sprites(sprites, sw, sh);
+  const std::vector<uint32_t> bg32 = static_layer(desc, W, H, sc);
+  const std::vector<uint8_t> rgb = rgb_bytes(bg32);
+  const std::vector<uint32_t> dyn = dynamic_sprites(sc);
+  RenderState* rs = new RenderState();
+  rs->Wpx = Wpx, rs->Hpx = Hpx, rs->CH = Wpx * 3 / 16;  // W * 144 bytes per row: whole chunks
+  rs->knob = knob_table(KNOB_R);
+  auto undo = [&](int code) {
+    render_free(rs);
+    return code;
+  };
+  if (hipMalloc((void**)&rs->bg, rgb.size()) != hipSuccess ||
+      hipMalloc((void**)&rs->bg32, bg32.size() * 4) != hipSuccess ||
+      hipMalloc((void**)&rs->spr, dyn.size() * 4) != hipSuccess)
+    return undo(fail(TG_E_NOMEM, "tg_render_init: device allocation failed"));
+  if (hipMemcpy(rs->bg, rgb.data(), rgb.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(rs->bg32, bg32.data(), bg32.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(rs->spr, dyn.data(), dyn.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return undo(fail(TG_E_HIP, "tg_render_init: upload failed"));
+  render_free(h->rs);
+  h->rs = rs;
+  return TG_OK;
+}
+
+int tg_frame_shape(const tg_batch* h, int32_t* height, int32_t* width) {
+  if (!h) return fail(TG_E_INVAL, "null handle");
+  if (height) *height = h->L.H * RS;
+  if (width) *width = h->L.W * RS;
+  return TG_OK;
+}
+
+int tg_render(tg_batch* h, int64_t first, int64_t count, uint8_t* rgb, void* stream) {
+  BIND(h);
+  if (!h->rs) return fail(TG_E_STATE, "tg_render: call tg_render_init first");
+  if (first < 0 || count < 0 || first + count > h->n || (count && !rgb))
+    return fail(TG_E_INVAL, "tg_render: envs [%lld, %lld) outside [0, %lld)", (long long)first,
+                (long long)(first + count), (long long)h->n);
+  if (((uintptr_t)rgb & 15u) != 0) return fail(TG_E_INVAL, "tg_render: rgb must be 16-B aligned");
+  if (!count) return TG_OK;
+  const RenderState* rs = h->rs;
+  RenderArgs A;
+  A.bg = rs->bg, A.bg32 = rs->bg32, A.spr = rs->spr, A.err = h->err;
+  A.Wpx = rs->Wpx, A.Hpx = rs->Hpx, A.CH = rs->CH, A.H = h->L.H;
+  A.knob = rs->knob;
+  for (int k = 0; k < 3; ++k) A.door_cx[k] = h->L.door_cx[k], A.door_cy[k] = h->L.door_cy[k];
+  for (int k = 0; k < 2; ++k) A.handle_cx[k] = h->L.handle_cx[k], A.handle_cy[k] = h->L.handle_cy[k];
+  A.bolt_cx = h->L.bolt_cx, A.bolt_cy = h->L.bolt_cy;
+  const int64_t blocks = count * h->L.H;
+  if (blocks > 0x7FFFFFFF) return fail(TG_E_INVAL, "tg_render: too many envs in one call");
+  hipLaunchKernelGGL(k_render, dim3((unsigned)blocks), dim3(RBLOCK), 0, (hipStream_t)stream, A,
+                     h->S.st4, h->S.ang, first, reinterpret_cast<uint4*>(rgb));
+  HIP_TRY(hipGetLastError());
+  return TG_OK;
+}
+
+}  // extern "C"

@@ -251,6 +251,39 @@ class TreasureGameVec:
     def stats_reset(self):
         check(self._L.tg_stats_reset(self.handle), "tg_stats_reset")
 
+    # -- render('rgb_array') (TG/:98-105; DR/ draw_domain) ---------------------------------------
+    def render_init(self, sprites=None):
+        """Load the sprite sheet (uint8 [24, h, w, 4] RGBA, ``render.load_sprites`` /
+        ``render.synthetic_sprites``; default: the installed reference's sprites)."""
+        from . import render as R
+        if sprites is None:
+            sprites = R.load_sprites()
+        sheet = np.ascontiguousarray(sprites, np.uint8)
+        if sheet.ndim != 4 or sheet.shape[0] != _lib.TG_SPR_COUNT or sheet.shape[3] != 4:
+            raise ValueError("sprite sheet must be uint8 [%d, h, w, 4]" % _lib.TG_SPR_COUNT)
+        check(self._L.tg_render_init(self.handle, sheet.ctypes.data_as(ctypes.c_void_p),
+                                     sheet.shape[2], sheet.shape[1]), "tg_render_init")
+        h, w = ctypes.c_int32(), ctypes.c_int32()
+        check(self._L.tg_frame_shape(self.handle, ctypes.byref(h), ctypes.byref(w)),
+              "tg_frame_shape")
+        self.frame_shape = (h.value, w.value, 3)
+
+    def render(self, first=0, count=None, out=None):
+        """render('rgb_array') of envs [first, first+count): uint8 [count, H*48, W*48, 3]
+        on the device (the reference's ``rgb`` array per env, TG/:103-105)."""
+        if getattr(self, "frame_shape", None) is None:
+            self.render_init()
+        count = self.num_envs - first if count is None else int(count)
+        if out is None:
+            out = torch.empty((count,) + self.frame_shape, dtype=torch.uint8, device=self.device)
+        elif (out.dtype != torch.uint8 or not out.is_contiguous() or out.device != self.device
+              or tuple(out.shape) != (count,) + self.frame_shape):
+            raise ValueError("out must be a contiguous uint8 [%d, %d, %d, 3] tensor on %s"
+                             % ((count,) + self.frame_shape[:2] + (self.device,)))
+        check(self._L.tg_render(self.handle, int(first), count, _ptr(out), self._stream()),
+              "tg_render")
+        return out
+
     def read_state(self, mt=False):
         """Host copy of the SoA state (checkpoints / tests)."""
         n = self.num_envs
@@ -277,13 +310,15 @@ class TreasureGame:
     equals ``random.seed(s); TreasureGame()`` in a fresh reference process; ``seed=None``
     draws a seed from Python's global ``random`` (so ``random.seed`` still makes runs
     reproducible, but not draw-for-draw identical to the reference's shared stream).
-    Pixel rendering (``render`` / ``ObservationWrapper``, TG/:38-51, 98-114) is not part of
-    this path yet and raises.
+    ``render(mode='rgb_array')`` returns the frame as a uint8 numpy array [624, 672, 3]
+    (TG/:98-105; the sprites are the installed reference's unless ``sprites=`` is given);
+    ``mode='human'`` needs gym's image viewer and raises.
     """
 
     metadata = {"render.modes": ["human", "rgb_array"]}
 
-    def __init__(self, seed=None, device=None, level_dir=None):
+    def __init__(self, seed=None, device=None, level_dir=None, sprites=None):
+        self._sprites = sprites
         if seed is None:
             seed = random.getrandbits(64)
         self._vec = TreasureGameVec(1, seed=seed, device=device, level_dir=level_dir)
@@ -315,9 +350,56 @@ class TreasureGame:
         return state, r, bool(packed[11]), {}
 
     def render(self, mode="human"):
-        raise NotImplementedError("pixel rendering (TG/:98-110) is outside this build's hot path")
+        if mode != "rgb_array":
+            raise NotImplementedError("render(mode=%r): only 'rgb_array' (no display / gym "
+                                      "image viewer here, TG/:106-110)" % (mode,))
+        if getattr(self._vec, "frame_shape", None) is None:
+            self._vec.render_init(self._sprites)
+        return self._vec.render().cpu().numpy()[0]
 
     def close(self):
         if self.viewer is not None:
             self.viewer = None
         self._vec.close()
+
+
+class ObservationWrapper:
+    """The reference's ``ObservationWrapper`` (treasure_game.py:38-51): reset / step return the
+    rendered screen instead of the state vector, and step's info carries the state as
+    ``info['world_state']``.
+
+    Over a ``TreasureGame`` the screen is a uint8 numpy array [624, 672, 3], as in the
+    reference.  Over a ``TreasureGameVec`` it is the batch's frames, a uint8 device tensor
+    [N, 624, 672, 3] rendered by one kernel launch into a buffer the wrapper owns
+    (overwritten each call), and step returns ``(frames, reward, valid, done, info)``.
+    """
+
+    def __init__(self, env, sprites=None):
+        self.env = env
+        self._vec = isinstance(env, TreasureGameVec)
+        if self._vec:
+            env.render_init(sprites)
+            self._frames = torch.empty((env.num_envs,) + env.frame_shape, dtype=torch.uint8,
+                                       device=env.device)
+        elif sprites is not None:
+            env._sprites = sprites
+        self.action_space = env.action_space
+        self.observation_space = env.observation_space
+
+    def __getattr__(self, name):
+        return getattr(self.env, name)
+
+    def _screen(self):
+        if self._vec:
+            return self.env.render(out=self._frames)
+        return self.env.render(mode="rgb_array")
+
+    def reset(self, **kwargs):
+        self.env.reset(**kwargs)
+        return self._screen()
+
+    def step(self, action):
+        out = self.env.step(action)
+        info = out[-1]
+        info["world_state"] = out[0]
+        return (self._screen(),) + tuple(out[1:])

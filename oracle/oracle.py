@@ -61,6 +61,11 @@ def lib():
         L.tgo_action_hash.argtypes = [u64, u64, u64]
         L.tgo_pick_action.restype = i32
         L.tgo_pick_action.argtypes = [u64, u64, u64, i32, ctypes.c_uint]
+        L.tgo_render.restype = i32
+        L.tgo_render.argtypes = [P, P, i32, i32, P]
+        L.tgo_run_render.restype = i32
+        L.tgo_run_render.argtypes = [P, u64, P, i64, i32, u64, i32, i32, P, i32, i32, P, i32]
+        L.tgo_choice_seq.argtypes = [u64, i32, i32, P]
         _lib = L
     return _lib
 
@@ -90,6 +95,7 @@ class OracleEnv:
     def __init__(self, seed, level_dir=None):
         self._obs = np.zeros(9, np.float64)
         self._h = lib().tgo_env_new(level(level_dir), seed, _p(self._obs))
+        self._shape = _level_frame_shape(level_dir)
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -129,6 +135,17 @@ class OracleEnv:
     def internal(self):
         out = np.zeros(12, np.int32)
         lib().tgo_internal(self._h, _p(out))
+        return out
+
+    def render(self, sprites):
+        """render('rgb_array') of the current state (PARITY UNPINNED, see tg_oracle.c):
+        uint8 [H*48, W*48, 3].  sprites: uint8 [24, sh, sw, 4] RGBA in TG_SPR_* order."""
+        sprites = np.ascontiguousarray(sprites, np.uint8)
+        h, w = self._shape
+        out = np.zeros((h, w, 3), np.uint8)
+        rc = lib().tgo_render(self._h, _p(sprites), sprites.shape[2], sprites.shape[1], _p(out))
+        if rc < 0:
+            raise RuntimeError("oracle render: unsupported geometry")
         return out
 
     def predicates(self, px, py, door_bits):
@@ -189,3 +206,34 @@ def rng_gauss(seed, pairs):
 
 def pick_action(a0, g, t, masked=False, mask=0):
     return int(lib().tgo_pick_action(a0, g, t, int(masked), mask))
+
+
+def _level_frame_shape(level_dir=None):
+    d = os.path.abspath(level_dir or LEVEL_DIR)
+    with open(os.path.join(d, "domain.txt")) as fh:
+        rows = [ln.strip() for ln in fh.read().split("\n")]
+    while rows and not rows[-1]:
+        rows.pop()
+    return len(rows) * 48, len(rows[0]) * 48
+
+
+def run_render(seed_base, envs, steps, action_seed, policy, autoreset, sprites, nthreads=0,
+               level_dir=None):
+    """Frames of the listed global envs after `steps` env-steps of the run() action stream:
+    uint8 [len(envs), H*48, W*48, 3] (PARITY UNPINNED renderer restatement)."""
+    envs = np.ascontiguousarray(envs, np.int64)
+    sprites = np.ascontiguousarray(sprites, np.uint8)
+    h, w = _level_frame_shape(level_dir)
+    out = np.zeros((len(envs), h, w, 3), np.uint8)
+    rc = lib().tgo_run_render(level(level_dir), seed_base, _p(envs), len(envs), steps, action_seed,
+                              int(policy), int(autoreset), _p(sprites), sprites.shape[2],
+                              sprites.shape[1], _p(out), nthreads)
+    if rc < 0:
+        raise RuntimeError("oracle run_render failed")
+    return out
+
+
+def choice_seq(seed, n, count):
+    out = np.zeros(count, np.int32)
+    lib().tgo_choice_seq(seed, n, count, _p(out))
+    return out

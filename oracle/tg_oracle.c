@@ -1099,3 +1099,352 @@ int tgo_run(const tgo_level *lv, uint64_t seed_base, int64_t g0, int64_t n, int 
     }
     return err ? -1 : 0;
 }
+
+/* ======================================================================================
+ * Renderer: TreasureGame.render('rgb_array') (TG/:98-105) -> _TreasureGameDrawer.draw_domain
+ * (DR/ = _treasure_game_impl/_treasure_game_drawer.py, DR/:136-163, DR/:238-269).
+ *
+ * PARITY UNPINNED: pygame is absent from this image, so the reference renderer cannot run
+ * here and no reference frame exists to check against.  This section restates pygame 1.9.6 /
+ * SDL 1.2 (the versions the reference's Python 3.7 era pulls in) as documented in DESIGN.md:
+ *   - transform.scale: transform.c stretch() (Bresenham step, source index floor(d*s/D));
+ *   - blit of a convert_alpha() sprite onto the convert()ed screen: SDL_blit_A.c
+ *     BlitRGBtoRGBPixelAlpha, i.e. per channel d + ((s - d) * a >> 8), a == 255 copies,
+ *     a == 0 skips;
+ *   - draw.line(width 5): draw.c clip_and_draw_line_width -> 5 one-pixel lines offset along
+ *     x or y, each drawline() (Bresenham, both end points, error term starting at 0);
+ *   - draw.circle(r, width 0): draw.c draw_fillellipse (SDL_gfx filled-ellipse scanlines);
+ *   - random_generator.choice: CPython Random.choice = seq[_randbelow(len)] with
+ *     getrandbits(bit_length(len)) rejection (pinned against Python's random in the tests).
+ * The screen is XRGB8888; the frame is its RGB bytes, rows top to bottom
+ * (surfarray.array3d(...).swapaxes(0, 1)).  Sprites come in as RGBA8 (PIL decode of the
+ * reference's PNGs, or synthetic sheets in the tests) in TGO_SPR_* order.
+ * ====================================================================================== */
+enum { /* sprite sheet order (shared with include/tg_amd.h TG_SPR_*) */
+    TGO_SPR_BACKGROUND = 0, /* 5 variants: sprites/background/background_{0..4}.png */
+    TGO_SPR_WALL = 5,       /* 5 variants: sprites/wall/wall_{0..4}.png */
+    TGO_SPR_FLOOR = 10,     /* 5 variants: sprites/floor/floor-{0..4}.png */
+    TGO_SPR_LADDER = 15, TGO_SPR_DOOR_CLOSED, TGO_SPR_DOOR_OPEN, TGO_SPR_KEY, TGO_SPR_GOLD,
+    TGO_SPR_BOLT_OPEN, TGO_SPR_BOLT_LOCKED, TGO_SPR_HERO, TGO_SPR_HANDLE_BASE, TGO_SPR_COUNT
+};
+
+typedef struct {
+    int w, h;
+    uint32_t *px; /* ARGB8888, row-major */
+} surf;
+
+/* pygame transform.c stretch(): nearest neighbour with a Bresenham error term */
+static void stretch(const surf *src, surf *dst) {
+    const int dw2 = dst->w << 1, dh2 = dst->h << 1, sw2 = src->w << 1, sh2 = src->h << 1;
+    int h_err = sh2 - dh2;
+    int srow = 0;
+    for (int looph = 0; looph < dst->h; ++looph) {
+        int w_err = sw2 - dw2, sx = 0;
+        for (int loopw = 0; loopw < dst->w; ++loopw) {
+            dst->px[looph * dst->w + loopw] = src->px[srow * src->w + sx];
+            while (w_err >= 0) {
+                ++sx;
+                w_err -= dw2;
+            }
+            w_err += sw2;
+        }
+        while (h_err >= 0) {
+            ++srow;
+            h_err -= dh2;
+        }
+        h_err += sh2;
+    }
+}
+
+/* SDL_blit_A.c BlitRGBtoRGBPixelAlpha for one pixel (dst alpha is not displayed) */
+static uint32_t blend_px(uint32_t d, uint32_t s) {
+    const uint32_t a = s >> 24;
+    if (a == 0) return d;
+    if (a == 255) return (s & 0x00ffffffu) | (d & 0xff000000u);
+    uint32_t out = d & 0xff000000u;
+    for (int sh = 0; sh < 24; sh += 8) {
+        const int sc = (int)((s >> sh) & 0xff), dc = (int)((d >> sh) & 0xff);
+        const int c = dc + (((sc - dc) * (int)a) >> 8); /* arithmetic shift == floor */
+        out |= (uint32_t)(c & 0xff) << sh;
+    }
+    return out;
+}
+
+/* Surface.blit(src, (x, y)) with SDL's clipping to the destination */
+static void blit(surf *dst, const surf *src, int x, int y, int flip_x) {
+    for (int j = 0; j < src->h; ++j) {
+        const int yy = y + j;
+        if (yy < 0 || yy >= dst->h) continue;
+        for (int i = 0; i < src->w; ++i) {
+            const int xx = x + i;
+            if (xx < 0 || xx >= dst->w) continue;
+            const int si = flip_x ? src->w - 1 - i : i; /* transform.flip(img, True, False) */
+            uint32_t *p = &dst->px[yy * dst->w + xx];
+            *p = blend_px(*p, src->px[j * src->w + si]);
+        }
+    }
+}
+
+static void set_at(surf *s, int x, int y, uint32_t c) {
+    if (x >= 0 && y >= 0 && x < s->w && y < s->h) s->px[y * s->w + x] = c;
+}
+
+/* draw.c drawline(): Bresenham over the longer axis, both end points drawn */
+static void drawline(surf *s, uint32_t color, int x1, int y1, int x2, int y2) {
+    int deltax = x2 - x1, deltay = y2 - y1;
+    const int signx = deltax < 0 ? -1 : 1, signy = deltay < 0 ? -1 : 1;
+    deltax = signx * deltax + 1;
+    deltay = signy * deltay + 1;
+    int px = signx, py = 0, qx = 0, qy = signy; /* major step (px,py), minor step (qx,qy) */
+    if (deltax < deltay) {                      /* swap axis if rise > run */
+        int t = deltax;
+        deltax = deltay;
+        deltay = t;
+        px = 0, py = signy, qx = signx, qy = 0;
+    }
+    int x = x1, y = y1, err = 0;
+    for (int k = 0; k < deltax; ++k) {
+        set_at(s, x, y, color);
+        err += deltay;
+        x += px, y += py;
+        if (err >= deltax) {
+            err -= deltax;
+            x += qx, y += qy;
+        }
+    }
+}
+
+/* draw.c clip_and_draw_line(): the renderer only draws lines that lie inside the surface
+ * (tgo_render checks), so clipline() is the accept case; horizontal / vertical lines cover
+ * the same pixels as drawline(). */
+static int clip_and_draw_line(surf *s, uint32_t color, const int *p) {
+    if (p[0] < 0 || p[2] < 0 || p[1] < 0 || p[3] < 0 || p[0] >= s->w || p[2] >= s->w ||
+        p[1] >= s->h || p[3] >= s->h)
+        return -1;
+    drawline(s, color, p[0], p[1], p[2], p[3]);
+    return 0;
+}
+
+/* draw.c clip_and_draw_line_width(): width-1 extra lines offset by +1, -1, +2, -2 along y
+ * for a mostly-horizontal line, else along x */
+static int clip_and_draw_line_width(surf *s, uint32_t color, int width, const int *pts) {
+    int xinc = 0, yinc = 0, rc = 0, np[4];
+    if (abs(pts[0] - pts[2]) > abs(pts[1] - pts[3])) yinc = 1;
+    else xinc = 1;
+    rc |= clip_and_draw_line(s, color, pts);
+    for (int loop = 1; loop < width; loop += 2) {
+        const int o = loop / 2 + 1;
+        np[0] = pts[0] + xinc * o, np[1] = pts[1] + yinc * o;
+        np[2] = pts[2] + xinc * o, np[3] = pts[3] + yinc * o;
+        rc |= clip_and_draw_line(s, color, np);
+        if (loop + 1 < width) {
+            np[0] = pts[0] - xinc * o, np[1] = pts[1] - yinc * o;
+            np[2] = pts[2] - xinc * o, np[3] = pts[3] - yinc * o;
+            rc |= clip_and_draw_line(s, color, np);
+        }
+    }
+    return rc;
+}
+
+static void hline(surf *s, uint32_t color, int x1, int y, int x2) {
+    for (int x = x1; x <= x2; ++x) set_at(s, x, y, color);
+}
+
+/* draw.c draw_fillellipse(x, y, rx, ry) with rx == ry (SDL_gfx filledEllipse scanlines) */
+static void fillellipse(surf *s, int x, int y, int rx, int ry, uint32_t color) {
+    int ix, iy, h, i, j, k, oh, oi, oj, ok;
+    if (rx == 0 && ry == 0) {
+        set_at(s, x, y, color);
+        return;
+    }
+    oh = oi = oj = ok = 0xFFFF;
+    if (rx > ry) {
+        ix = 0;
+        iy = rx * 64;
+        do {
+            h = (ix + 16) >> 6;
+            i = (iy + 16) >> 6;
+            j = (h * ry) / rx;
+            k = (i * ry) / rx;
+            if ((ok != k) && (oj != k)) {
+                if (k) {
+                    hline(s, color, x - h, y - k, x + h);
+                    hline(s, color, x - h, y + k, x + h);
+                } else {
+                    hline(s, color, x - h, y, x + h);
+                }
+                ok = k;
+            }
+            if ((oj != j) && (ok != j) && (k != j)) {
+                if (j) {
+                    hline(s, color, x - i, y - j, x + i);
+                    hline(s, color, x - i, y + j, x + i);
+                } else {
+                    hline(s, color, x - i, y, x + i);
+                }
+                oj = j;
+            }
+            ix = ix + iy / rx;
+            iy = iy - ix / rx;
+        } while (i > h);
+    } else {
+        ix = 0;
+        iy = ry * 64;
+        do {
+            h = (ix + 32) >> 6;
+            i = (iy + 32) >> 6;
+            j = (h * rx) / ry;
+            k = (i * rx) / ry;
+            if ((oi != i) && (oh != i)) {
+                if (i) {
+                    hline(s, color, x - j, y + i, x + j);
+                    hline(s, color, x - j, y - i, x + j);
+                } else {
+                    hline(s, color, x - j, y, x + j);
+                }
+                oi = i;
+            }
+            if ((oh != h) && (oi != h) && (i != h)) {
+                if (h) {
+                    hline(s, color, x - k, y + h, x + k);
+                    hline(s, color, x - k, y - h, x + k);
+                } else {
+                    hline(s, color, x - k, y, x + k);
+                }
+                oh = h;
+            }
+            ix = ix + iy / ry;
+            iy = iy - ix / ry;
+        } while (i > h);
+    }
+}
+
+/* CPython Random.choice(seq) with len(seq) == n: seq[_randbelow(n)] */
+static int pr_choice(pyrand *r, int n) {
+    int k = 0;
+    while ((1 << k) <= n) ++k; /* n.bit_length() */
+    int v = (int)(pr_u32(r) >> (32 - k));
+    while (v >= n) v = (int)(pr_u32(r) >> (32 - k));
+    return v;
+}
+
+void tgo_choice_seq(uint64_t seed, int n, int count, int32_t *out) {
+    pyrand r;
+    pr_seed(&r, seed);
+    for (int i = 0; i < count; ++i) out[i] = pr_choice(&r, n);
+}
+
+/* the handle drawing of draw_object (DR/:257-266): returns -1 if the shaft leaves the
+ * surface (not supported), sets *nearint if an end point lands within 1e-9 of an integer */
+static int draw_handle(surf *s, const gobj *o, const surf *base, int *nearint) {
+    const double pi = 3.141592653589793; /* math.pi */
+    const double angle = ((pi / 2.0) * o->angle) + pi / 4.0;
+    const double r = YSCALE * 0.75;
+    const double sx = o->x + XSCALE / 2.0, sy = (double)(o->y + YSCALE);
+    const double ex = sx + (r * cos(angle)), ey = sy - (r * sin(angle));
+    if (fabs(ex - rint(ex)) < 1e-9 || fabs(ey - rint(ey)) < 1e-9) *nearint = 1;
+    int pts[4] = {(int)sx, (int)sy, (int)ex, (int)ey}; /* pg_IntFromObj truncates floats */
+    if (clip_and_draw_line_width(s, 0x2F4F4Fu /* (47, 79, 79) */, 5, pts)) return -1;
+    fillellipse(s, pts[2], pts[3], XSCALE / 10, XSCALE / 10, 0xFF0000u); /* int(xscale / 10) */
+    blit(s, base, o->x, o->y, 0);
+    return 0;
+}
+
+/* Render env e's current state: rgb [H*48][W*48][3].  Returns 0, -1 (unsupported geometry),
+ * or 1 (an end point near an integer: libm watch). */
+int tgo_render(const tgo_env *e, const uint8_t *sprites_rgba, int sw, int sh, uint8_t *rgb) {
+    const int W = e->W * XSCALE, H = e->H * YSCALE;
+    surf spr[TGO_SPR_COUNT], src;
+    uint32_t *mem = (uint32_t *)malloc(sizeof(uint32_t) *
+                                       ((size_t)TGO_SPR_COUNT * XSCALE * YSCALE + (size_t)W * H + (size_t)sw * sh));
+    if (!mem) return -1;
+    surf screen = {W, H, mem};
+    src.w = sw, src.h = sh, src.px = mem + (size_t)W * H;
+    for (int k = 0; k < TGO_SPR_COUNT; ++k) { /* image.load().convert_alpha(); transform.scale */
+        const uint8_t *p = sprites_rgba + (size_t)k * sw * sh * 4;
+        for (int i = 0; i < sw * sh; ++i)
+            src.px[i] = ((uint32_t)p[4 * i + 3] << 24) | ((uint32_t)p[4 * i] << 16) |
+                        ((uint32_t)p[4 * i + 1] << 8) | p[4 * i + 2];
+        spr[k].w = XSCALE, spr[k].h = YSCALE;
+        spr[k].px = mem + (size_t)W * H + (size_t)sw * sh + (size_t)k * XSCALE * YSCALE;
+        stretch(&src, &spr[k]);
+    }
+    /* draw_domain (DR/:136-163) */
+    pyrand rg;
+    pr_seed(&rg, 12); /* self.random_generator.seed(self.seed) */
+    memset(screen.px, 0, sizeof(uint32_t) * (size_t)W * H); /* fill((0, 0, 0)) */
+    const tgo_level *lv = e->lv;
+    for (int i = 0; i < lv->H; ++i)
+        for (int j = 0; j < lv->W; ++j) {
+            const char c = lv->desc[i][j];
+            if (c == C_WALL) {
+                int key = TGO_SPR_WALL;
+                if (i > 0 && lv->desc[i - 1][j] != C_WALL) key = TGO_SPR_FLOOR;
+                blit(&screen, &spr[key + pr_choice(&rg, 5)], j * XSCALE, i * YSCALE, 0);
+            } else if (c == C_LADDER) {
+                blit(&screen, &spr[TGO_SPR_LADDER], j * XSCALE, i * YSCALE, 0);
+            } else if (c == C_OPEN) {
+                blit(&screen, &spr[TGO_SPR_BACKGROUND + pr_choice(&rg, 5)], j * XSCALE, i * YSCALE, 0);
+            }
+        }
+    int rc = 0, nearint = 0;
+    for (int i = 0; i < e->nobj && !rc; ++i) { /* draw_object (DR/:238-269) */
+        const gobj *o = &e->obj[i];
+        if (o->x < 0) continue;
+        switch (o->type) {
+        case O_DOOR:
+            blit(&screen, &spr[o->closed ? TGO_SPR_DOOR_CLOSED : TGO_SPR_DOOR_OPEN], o->x, o->y, 0);
+            break;
+        case O_KEY: blit(&screen, &spr[TGO_SPR_KEY], o->x, o->y, 0); break;
+        case O_GOLD: blit(&screen, &spr[TGO_SPR_GOLD], o->x, o->y, 0); break;
+        case O_BOLT:
+            blit(&screen, &spr[o->locked ? TGO_SPR_BOLT_LOCKED : TGO_SPR_BOLT_OPEN], o->x, o->y, 0);
+            break;
+        case O_HANDLE: rc = draw_handle(&screen, o, &spr[TGO_SPR_HANDLE_BASE], &nearint); break;
+        }
+    }
+    /* the hero at (playerx - xscale / 2, playery), flipped when facing left (DR/:157-161) */
+    blit(&screen, &spr[TGO_SPR_HERO], (int)(e->playerx - XSCALE / 2.0), e->playery, !e->facing_right);
+    for (size_t p = 0; p < (size_t)W * H; ++p) {
+        rgb[3 * p] = (uint8_t)(screen.px[p] >> 16);
+        rgb[3 * p + 1] = (uint8_t)(screen.px[p] >> 8);
+        rgb[3 * p + 2] = (uint8_t)screen.px[p];
+    }
+    free(mem);
+    return rc ? -1 : nearint;
+}
+
+/* Frames of listed envs after `steps` env-steps of the tgo_run action stream (same seeding,
+ * policy and auto-reset): frames [n][H*48][W*48][3].  Returns the OR of tgo_render codes
+ * (-1 on any failure). */
+int tgo_run_render(const tgo_level *lv, uint64_t seed_base, const int64_t *envs, int64_t n,
+                   int steps, uint64_t action_seed, int policy, int autoreset,
+                   const uint8_t *sprites_rgba, int sw, int sh, uint8_t *frames, int nthreads) {
+    int err = 0, warn = 0;
+    const size_t fb = (size_t)lv->W * XSCALE * lv->H * YSCALE * 3;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(| : err, warn)
+#endif
+    for (int64_t i = 0; i < n; i++) {
+        const uint64_t g = (uint64_t)envs[i];
+        tgo_env *e = (tgo_env *)malloc(sizeof(tgo_env));
+        if (!e) {
+            err |= 1;
+            continue;
+        }
+        env_init(e, lv, seed_base + g, NULL);
+        for (int t = 0; t < steps; t++) {
+            unsigned m = policy ? tgo_mask(e) : 0;
+            int a = tgo_pick_action(action_seed, g, (uint64_t)t, policy, m);
+            uint8_t d;
+            if (tgo_step(e, a, NULL, NULL, NULL, &d)) err |= 1;
+            if (autoreset && d) tgo_reset(e, NULL);
+        }
+        const int rc = tgo_render(e, sprites_rgba, sw, sh, frames + (size_t)i * fb);
+        if (rc < 0) err |= 1;
+        if (rc > 0) warn |= 1;
+        free(e);
+    }
+    return err ? -1 : warn;
+}

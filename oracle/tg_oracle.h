@@ -69,6 +69,17 @@ uint64_t tgo_action_hash(uint64_t a0, uint64_t g, uint64_t t);
 int tgo_pick_action(uint64_t a0, uint64_t g, uint64_t t, int masked, unsigned mask);
 uint64_t tgo_rec_hash(uint64_t h, const double obs[9], int32_t reward, int valid, int done);
 
+/* --- renderer (TG/:98-105 render('rgb_array') -> DR/ draw_domain); PARITY UNPINNED -------- */
+/* sprites_rgba: TGO_SPR_COUNT (24) RGBA8 images of sw x sh in include/tg_amd.h TG_SPR_* order.
+ * rgb: [H*48][W*48][3].  Returns 0, 1 (libm watch: a handle end point within 1e-9 of an
+ * integer) or -1 (a handle shaft leaving the surface: unsupported). */
+int tgo_render(const tgo_env *e, const uint8_t *sprites_rgba, int sw, int sh, uint8_t *rgb);
+int tgo_run_render(const tgo_level *lv, uint64_t seed_base, const int64_t *envs, int64_t n,
+                   int steps, uint64_t action_seed, int policy, int autoreset,
+                   const uint8_t *sprites_rgba, int sw, int sh, uint8_t *frames, int nthreads);
+/* Random(seed).choice over a sequence of length n, `count` times (DR/:83-86) */
+void tgo_choice_seq(uint64_t seed, int n, int count, int32_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,8 +16,8 @@ step() {  # name, timeout, command...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 step bench 600 python bench.py --steps ${STEPS:-100} --warmup ${WARMUP:-10}
 step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 30 --warmup 5 --cpu-seconds 0
 echo "== all done"

@@ -45,6 +45,10 @@ def hostcheck():
     L.hc_predicate_table.argtypes = [ctypes.c_int] * 4 + [ctypes.c_uint, P]
     L.hc_rng_stream.restype = ctypes.c_int
     L.hc_rng_stream.argtypes = [ctypes.c_uint64, P, ctypes.c_int, ctypes.c_int, P]
+    L.hc_render_run.restype = ctypes.c_int
+    L.hc_render_run.argtypes = [P, P, P, ctypes.c_uint64, P, ctypes.c_int64, ctypes.c_int,
+                                ctypes.c_uint64, ctypes.c_int, ctypes.c_int, P, ctypes.c_int,
+                                ctypes.c_int, P]
     return L
 
 

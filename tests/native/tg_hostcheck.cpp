@@ -12,6 +12,7 @@
 
 #include "../../gym-treasure-game_amd/csrc/tg_core.h"
 #include "../../gym-treasure-game_amd/csrc/tg_level.h"
+#include "../../gym-treasure-game_amd/csrc/tg_render.h"
 
 using namespace tg;
 
@@ -170,6 +171,103 @@ void hc_predicate_table(int x0, int x1, int y0, int y1, unsigned door_bits, uint
     for (int x = x0; x < x1; ++x)
       out[(size_t)(y - y0) * (size_t)(x1 - x0) + (size_t)(x - x0)] =
           (uint8_t)hc_predicates(x, y, door_bits);
+}
+
+// render('rgb_array') of env g = seed_base + envs[i] after `steps` steps of the hc_run
+// action stream, composed by tg_render.h exactly as k_render's lanes do (band by band, row by
+// row, 16-B chunk by chunk), with the static layer built by tg_render_init's host code.
+// frames [n][H*48][W*48][3].  Returns the OR of the TG_ERR_RENDER bits, or -1.
+int hc_render_run(const char* dom, const char* objs, const char* inter, uint64_t seed_base,
+                  const int64_t* envs, int64_t n, int steps, uint64_t a0, int policy,
+                  int autoreset, const uint8_t* sprites, int sw, int sh, uint8_t* frames) {
+  Level Lv;
+  std::vector<uint8_t> grid;
+  if (!load_level(dom, objs, inter, Lv, grid)) return -1;
+  const Level* L = &Lv;
+  std::vector<std::string> desc;
+  for (auto& l : lines_of(dom ? dom : kDefaultDomain)) desc.push_back(strip(l));
+  while (!desc.empty() && desc.back().empty()) desc.pop_back();
+  const std::vector<uint32_t> sc = scale_sprites(sprites, sw, sh);
+  const std::vector<uint32_t> bg32 = static_layer(desc, L->W, L->H, sc);
+  const std::vector<uint8_t> bg = rgb_bytes(bg32);
+  const std::vector<uint32_t> dyn = dynamic_sprites(sc);
+  uint32_t err = 0;
+  RenderArgs A;
+  A.bg = reinterpret_cast<const uint4*>(bg.data());
+  A.bg32 = bg32.data();
+  A.spr = dyn.data();
+  A.err = &err;
+  A.Wpx = L->W * RS, A.Hpx = L->H * RS, A.CH = A.Wpx * 3 / 16, A.H = L->H;
+  A.knob = knob_table(KNOB_R);
+  for (int k = 0; k < 3; ++k) A.door_cx[k] = L->door_cx[k], A.door_cy[k] = L->door_cy[k];
+  for (int k = 0; k < 2; ++k) A.handle_cx[k] = L->handle_cx[k], A.handle_cy[k] = L->handle_cy[k];
+  A.bolt_cx = L->bolt_cx, A.bolt_cy = L->bolt_cy;
+  uint32_t gen[MT_N];
+  gen[0] = 19650218u;
+  for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
+  const Map m{grid.data(), L->W, L->H};
+  const uint32_t* trig = &L->trig[0][0];
+  std::vector<uint32_t> mt(MT_WORDS);
+  const size_t fb = (size_t)A.Hpx * A.Wpx * 3;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t g = (uint64_t)envs[i];
+    seed_mt(mt.data() + MT_N, gen, seed_base + g);
+    twist_gen(mt.data() + MT_N, mt.data());
+    twist_gen(mt.data(), mt.data() + MT_N);
+    Env e{};
+    for (int r = 0; r < 2; ++r) {  // construct + reset
+      Rng rng(mt.data(), e.mti);
+      reset_env(*L, e, rng);
+      e.mti = refill_after(mt.data(), rng.finish());
+    }
+    for (int t = 0; t < steps; ++t) {
+      const uint64_t hh = sm64(sm64(a0 ^ sm64(g)) ^ (uint64_t)t);
+      int a = (int)(hh % 9ull);
+      if (policy == 1) {
+        const uint32_t mk = available_mask(*L, m, e);
+        const int c = __builtin_popcount(mk);
+        if (c) {
+          uint32_t k = (uint32_t)(hh % (uint64_t)c), mm = mk;
+          while (k--) mm &= mm - 1u;
+          a = __builtin_ctz(mm);
+        }
+      }
+      e.mti = refill_after(mt.data(), e.mti);
+      Rng rng(mt.data(), e.mti);
+      const StepResult r = env_step(*L, trig, m, e, a, rng);
+      if (autoreset && r.done) reset_env(*L, e, rng);
+      e.mti = rng.finish();
+    }
+    uint4 st;  // k_render reads the SoA state words
+    st.x = ((uint32_t)e.px & 0xFFFFu) | ((uint32_t)e.py << 16);
+    st.y = e.f;
+    st.z = ((uint32_t)e.kx & 0xFF) | (((uint32_t)e.ky & 0xFF) << 8) | (((uint32_t)e.gx & 0xFF) << 16) |
+           ((uint32_t)e.gy << 24);
+    st.w = e.mti;
+    double2 an;
+    an.x = e.ang0, an.y = e.ang1;
+    uint4* out = reinterpret_cast<uint4*>(frames + (size_t)i * fb);
+    for (int band = 0; band < A.H; ++band) {
+      const int ylo = band * RS;
+      Layer lay[NLAYER];
+      uint32_t live_mask = 0;
+      for (int k = 0; k < NLAYER; ++k) {
+        bool live = false;
+        err |= make_layer(A, k, st, an, lay[k], live);
+        live = live && lay[k].y1 > ylo && lay[k].y0 < ylo + RS && lay[k].x1 > 0 && lay[k].x0 < A.Wpx;
+        live_mask |= (uint32_t)live << k;
+      }
+      for (int r = 0; r < RS; ++r) {
+        const int y = ylo + r;
+        const uint32_t rm = row_items(lay, live_mask, y);
+        for (int q = 0; q < A.CH; ++q) {
+          const uint32_t hit = rm ? chunk_items(lay, rm, q) : 0u;
+          out[(size_t)y * A.CH + q] = hit ? compose_chunk(A, lay, hit, y, q) : A.bg[(size_t)y * A.CH + q];
+        }
+      }
+    }
+  }
+  return (int)err;
 }
 
 }  // extern "C"

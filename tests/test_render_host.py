@@ -1,0 +1,80 @@
+"""render('rgb_array') on the CPU: the oracle's pygame/SDL restatement (oracle/tg_oracle.c,
+"Renderer") against Python's own random for the background choices, and against the product's
+frame composition (csrc/tg_render.h, host-only build in tests/native, driven band by band and
+chunk by chunk as k_render's lanes are).  The renderer's parity with the reference itself is
+UNPINNED: pygame is absent from this image."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from gym_treasure_game_amd import render as R
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def hc_frames(lib, envs, steps, a0, policy, autoreset, sprites, seed_base=0):
+    envs = np.ascontiguousarray(envs, np.int64)
+    out = np.zeros((len(envs), 624, 672, 3), np.uint8)
+    rc = lib.hc_render_run(None, None, None, seed_base, _p(envs), len(envs), steps, a0, policy,
+                           int(autoreset), _p(sprites), sprites.shape[2], sprites.shape[1], _p(out))
+    assert rc == 0
+    return out
+
+
+def test_background_choices_vs_cpython(oracle):
+    """draw_domain's Random(12).choice sequence (DR/:83-86, 137) == CPython's."""
+    r = random.Random(12)
+    want = [r.choice(range(5)) for _ in range(2000)]
+    assert list(oracle.choice_seq(12, 5, 2000)) == want
+    for n in (1, 2, 3, 7, 8, 9):
+        r = random.Random(3)
+        assert list(oracle.choice_seq(3, n, 300)) == [r.choice(range(n)) for _ in range(300)]
+
+
+@pytest.mark.parametrize("policy,autoreset,steps", [(1, True, 0), (1, True, 7), (0, False, 25),
+                                                    (1, True, 60)])
+def test_composition_vs_oracle(hostcheck, oracle, policy, autoreset, steps):
+    sprites = R.synthetic_sprites(seed=steps + 1)
+    envs = np.arange(24) * 37
+    a0 = 0x51 + policy
+    got = hc_frames(hostcheck, envs, steps, a0, policy, autoreset, sprites)
+    want = oracle.run_render(0, envs, steps, a0, policy, autoreset, sprites)
+    for i in range(len(envs)):
+        np.testing.assert_array_equal(got[i], want[i], err_msg="env %d" % envs[i])
+
+
+def test_composition_vs_oracle_sprite_sizes(hostcheck, oracle):
+    """Sheets of other source sizes (scale up, down and 1:1)."""
+    envs = np.arange(6)
+    for size in (16, 48, 50, 64):
+        sprites = R.synthetic_sprites(seed=size, size=size)
+        got = hc_frames(hostcheck, envs, 12, 7, 1, True, sprites)
+        want = oracle.run_render(0, envs, 12, 7, 1, True, sprites)
+        np.testing.assert_array_equal(got, want, err_msg="size %d" % size)
+
+
+def test_composition_covers_every_item(hostcheck, oracle):
+    """Masked rollouts long enough that keys, gold, bolts, handles and doors all change and
+    the hero faces both ways; each frame matches and differs from the static layer."""
+    sprites = R.synthetic_sprites(seed=99)
+    envs = np.arange(64)
+    got = hc_frames(hostcheck, envs, 150, 0xBEEF, 1, False, sprites)
+    want = oracle.run_render(0, envs, 150, 0xBEEF, 1, False, sprites)
+    np.testing.assert_array_equal(got, want)
+    assert len({g.tobytes() for g in got}) > 32
+
+
+def test_real_sprites_if_present(hostcheck, oracle):
+    d = R.default_sprite_dir() or "/root/reference/gym_treasure_game/envs/_treasure_game_impl/sprites"
+    try:
+        sprites = R.load_sprites(d)
+    except (FileNotFoundError, OSError, ImportError):
+        pytest.skip("reference sprites not available")
+    envs = np.arange(8)
+    got = hc_frames(hostcheck, envs, 40, 3, 1, True, sprites)
+    want = oracle.run_render(0, envs, 40, 3, 1, True, sprites)
+    np.testing.assert_array_equal(got, want)
