@@ -16,11 +16,12 @@
 //     file order (3 doors open/closed, 2 handles = 5-px shaft + r=4 knob + base sprite, key
 //     and gold unless moved off-screen, bolt open/locked), then the hero (mirrored when facing
 //     left).  They cover ~6 % of the pixels.
-// k_render: one workgroup per (env, band of 48 pixel rows), one wave per row, one lane per
-// 16-B chunk of the row's RGB bytes (coalesced, every byte of the frame written exactly once).
-// A chunk that no dynamic item touches is a 16-B copy of the static layer; the others
-// composite their 6 pixels in draw order and repack.  The kernel is HBM-write bound:
-// 1,257,984 B per frame of the default level.
+// k_render: one workgroup per (group of 16 envs, band of 48 pixel rows), one wave per row,
+// one lane per 16-B chunk of the row's RGB bytes (coalesced, every byte of every frame written
+// exactly once).  The lane loads its static chunk once and stores it into the 16 frames,
+// except where a dynamic item touches the chunk: there it composites the chunk's 6 pixels in
+// draw order and repacks.  The kernel is HBM-write bound: 1,257,984 B per frame of the
+// default level; the static layer is read once per 16 frames (from L2 / Infinity Cache).
 //
 // The per-chunk composition and the static-layer construction live in tg_render.h (shared
 // with the host-only check build); the pixel rules are listed there.  PARITY UNPINNED against
@@ -70,41 +71,63 @@ __device__ __forceinline__ void store16(uint4* p, const uint4 x) {
 #endif
 }
 
-// block = (env, band of 48 rows); wave w renders rows w, w+4, ... of the band, lane l the
-// 16-B chunks l, l+64, ... of the row
+#ifndef TG_RENDER_G
+#define TG_RENDER_G 16  // envs per workgroup: each static-layer chunk is loaded once per G frames
+#endif
+constexpr int RG = TG_RENDER_G;
+
+// block = (group of RG envs, band of 48 rows); wave w renders rows w, w+4, ... of the band,
+// lane l the 16-B chunks l, l+64, ... of each row, for each env of the group in turn: the
+// static chunk is loaded once and stored RG times (composited where an item covers it).
 __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __restrict__ st4,
                                                    const double2* __restrict__ angs,
-                                                   int64_t first, uint4* __restrict__ out) {
-  __shared__ Layer lay[NLAYER];
-  __shared__ uint32_t live_mask;
-  const int64_t e = blockIdx.x / A.H;
-  const int band = (int)(blockIdx.x - e * A.H);
+                                                   int64_t first, int64_t count,
+                                                   uint4* __restrict__ out) {
+  __shared__ Layer lay[RG][NLAYER];
+  __shared__ uint32_t live[RG];
+  __shared__ uint16_t rows[RG][RS];  // items covering each row of the band, per env
+  const int64_t grp = blockIdx.x / A.H;
+  const int band = (int)(blockIdx.x - grp * A.H);
   const int ylo = band * RS;
-  if (threadIdx.x < 64) {
-    bool live = false;
-    if (threadIdx.x < NLAYER) {
+  const int64_t e0 = grp * RG;
+  const int ne = (int)(count - e0 < RG ? count - e0 : RG);
+  if (threadIdx.x < RG) live[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int t = threadIdx.x; t < RG * NLAYER; t += RBLOCK) {
+    const int k = t / NLAYER, i = t - k * NLAYER;
+    if (k < ne) {
       Layer l;
-      const uint32_t err = make_layer(A, threadIdx.x, st4[first + e], angs[first + e], l, live);
+      bool on = false;
+      const int64_t g = first + e0 + k;
+      const uint32_t err = make_layer(A, i, st4[g], angs[g], l, on);
       if (err) atomicOr(A.err, err);
-      live = live && l.y1 > ylo && l.y0 < ylo + RS && l.x1 > 0 && l.x0 < A.Wpx;
-      lay[threadIdx.x] = l;
+      if (on && l.y1 > ylo && l.y0 < ylo + RS && l.x1 > 0 && l.x0 < A.Wpx) {
+        lay[k][i] = l;
+        atomicOr(&live[k], 1u << i);
+      }
     }
-    const uint64_t b = __ballot(live);
-    if (threadIdx.x == 0) live_mask = (uint32_t)b;
   }
   __syncthreads();
-  const uint32_t lm = live_mask;
+  for (int t = threadIdx.x; t < RG * RS; t += RBLOCK) {
+    const int k = t / RS, r = t - k * RS;
+    rows[k][r] = (uint16_t)(k < ne ? row_items(lay[k], live[k], ylo + r) : 0u);
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint4* const frame = out + (e * (int64_t)A.Hpx) * A.CH;
+  const int64_t frame_chunks = (int64_t)A.Hpx * A.CH;
+  uint4* const base = out + e0 * frame_chunks;
   for (int r = wave; r < RS; r += RBLOCK / 64) {
     const int y = ylo + r;
-    const uint32_t rm = row_items(lay, lm, y);  // wave-uniform
-    const uint4* src = A.bg + (int64_t)y * A.CH;
-    uint4* dst = frame + (int64_t)y * A.CH;
-    for (int q = lane; q < A.CH; q += 64) {
-      const uint32_t hit = rm ? chunk_items(lay, rm, q) : 0u;
-      const uint4 v = hit ? compose_chunk(A, lay, hit, y, q) : src[q];
-      store16(dst + q, v);
+    for (int q0 = 0; q0 < A.CH; q0 += 64) {
+      const int q = q0 + lane;
+      if (q >= A.CH) break;
+      const uint4 v = A.bg[(int64_t)y * A.CH + q];
+      uint4* dst = base + (int64_t)y * A.CH + q;
+      for (int k = 0; k < ne; ++k, dst += frame_chunks) {
+        const uint32_t rm = rows[k][r];  // wave-uniform
+        const uint32_t hit = rm ? chunk_items(lay[k], rm, q) : 0u;
+        store16(dst, hit ? compose_chunk(A, lay[k], hit, y, q) : v);
+      }
     }
   }
 }
@@ -180,10 +203,10 @@ int tg_render(tg_batch* h, int64_t first, int64_t count, uint8_t* rgb, void* str
   for (int k = 0; k < 3; ++k) A.door_cx[k] = h->L.door_cx[k], A.door_cy[k] = h->L.door_cy[k];
   for (int k = 0; k < 2; ++k) A.handle_cx[k] = h->L.handle_cx[k], A.handle_cy[k] = h->L.handle_cy[k];
   A.bolt_cx = h->L.bolt_cx, A.bolt_cy = h->L.bolt_cy;
-  const int64_t blocks = count * h->L.H;
+  const int64_t blocks = (count + RG - 1) / RG * h->L.H;
   if (blocks > 0x7FFFFFFF) return fail(TG_E_INVAL, "tg_render: too many envs in one call");
   hipLaunchKernelGGL(k_render, dim3((unsigned)blocks), dim3(RBLOCK), 0, (hipStream_t)stream, A,
-                     h->S.st4, h->S.ang, first, reinterpret_cast<uint4*>(rgb));
+                     h->S.st4, h->S.ang, first, count, reinterpret_cast<uint4*>(rgb));
   HIP_TRY(hipGetLastError());
   return TG_OK;
 }

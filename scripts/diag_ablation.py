@@ -33,10 +33,8 @@ def build_variant(name, flags):
     out = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_%s.so" % name)
     if os.environ.get("NOBUILD") and os.path.exists(out):
         return out
-    src = os.path.join(ROOT, "gym-treasure-game_amd", "csrc", "tg_amd.hip")
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                           "-ffp-contract=off", "-fPIC", "-shared",
-                           "-Wno-bitwise-instead-of-logical"] + flags.split() + ["-o", out, src])
+    from gym_treasure_game_amd import build as B
+    subprocess.check_call([B.HIPCC] + B.FLAGS + flags.split() + ["-o", out] + B.SRCS)
     return out
 
 

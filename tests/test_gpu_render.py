@@ -37,7 +37,7 @@ def test_render_every_step_vs_oracle(tg, oracle):
 
 
 def test_render_subrange_and_out(tg):
-    n = 300
+    n = 300  # not a multiple of the 16-env workgroup
     vec = tg.TreasureGameVec(n, seed=9, autoreset=True)
     vec.render_init(tg.synthetic_sprites(seed=1, size=16))
     for t in range(15):
@@ -60,6 +60,7 @@ def test_render_c5_sample_vs_oracle(tg, oracle):
     sprites = tg.synthetic_sprites(seed=55)
     vec = tg.TreasureGameVec(n, seed=0, autoreset=True)
     vec.render_init(sprites)
+    vec.reset()
     for t in range(steps):
         vec.step(vec.policy_actions(t, a0, "uniform"))
     frames = vec.render()
