@@ -38,7 +38,6 @@ constexpr int NLAYER = 9;                  // 8 objects in file order + the hero
 // Everything the composition reads besides the env's state words.
 struct RenderArgs {
   const uint4* bg;       // static layer, RGB bytes [Hpx][Wpx*3] as 16-B chunks
-  const uint32_t* bg32;  // static layer, XRGB [Hpx][Wpx]
   const uint32_t* spr;   // dynamic sprites [D_COUNT][48*48] ARGB
   uint32_t* err;         // device error word (TG_ERR_RENDER)
   int Wpx, Hpx, CH, H;   // pixels, 16-B chunks per row, cell rows (= bands)
@@ -180,14 +179,31 @@ TG_HD uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t o) {  // ({hi,lo} 
 }
 
 // The 16 frame bytes [16q, 16q+16) of pixel row y, given the items `hit` (bit i = lay[i])
-// touching them.  The chunk starts in pixel p0 = 16q/3 at byte o = q % 3 and spans 6 pixels.
-TG_HD uint4 compose_chunk(const RenderArgs& A, const Layer* lay, uint32_t hit, int y, int q) {
+// touching them and the static layer's bytes `v` there.  The chunk starts in pixel
+// p0 = 16q/3 at byte o = q % 3 and spans 6 pixels; blending is per channel, so the pixels are
+// rebuilt from v's bytes alone (the 2 bytes of the end pixels outside the chunk are never
+// written back).
+TG_HD uint4 compose_chunk(const RenderArgs& A, const Layer* lay, uint32_t hit, int y, int q,
+                          const uint4 v) {
   const int p0 = (16 * q) / 3;
   const uint32_t o = (uint32_t)(q % 3);
+  // the 18-byte stream of pixels p0..p0+5 as 5 words (stream byte o + i = chunk byte i)
+  uint32_t s0, s1, s2, s3, s4;
+  if (o == 0u) {
+    s0 = v.x, s1 = v.y, s2 = v.z, s3 = v.w, s4 = 0u;
+  } else {
+    const uint32_t sh = 4u - o;
+    s0 = align_bytes(v.x, 0u, sh), s1 = align_bytes(v.y, v.x, sh), s2 = align_bytes(v.z, v.y, sh);
+    s3 = align_bytes(v.w, v.z, sh), s4 = align_bytes(0u, v.w, sh);
+  }
+  auto rgb = [](uint32_t r, uint32_t g, uint32_t b) { return ((r & 255u) << 16) | ((g & 255u) << 8) | (b & 255u); };
   uint32_t c[6];
-  const uint32_t* b32 = A.bg32 + (int64_t)y * A.Wpx + p0;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) c[j] = b32[j];
+  c[0] = rgb(s0, s0 >> 8, s0 >> 16);
+  c[1] = rgb(s0 >> 24, s1, s1 >> 8);
+  c[2] = rgb(s1 >> 16, s1 >> 24, s2);
+  c[3] = rgb(s2 >> 8, s2 >> 16, s2 >> 24);
+  c[4] = rgb(s3, s3 >> 8, s3 >> 16);
+  c[5] = rgb(s3 >> 24, s4, s4 >> 8);
   for (uint32_t m = hit; m; m &= m - 1) {
     const Layer& l = lay[__builtin_ctz(m)];
 #pragma unroll
@@ -197,12 +213,12 @@ TG_HD uint4 compose_chunk(const RenderArgs& A, const Layer* lay, uint32_t hit, i
                  a5 = px3(c[5]);
   const uint32_t w0 = a0 | (a1 << 24), w1 = (a1 >> 8) | (a2 << 16), w2 = (a2 >> 16) | (a3 << 8),
                  w3 = a4 | (a5 << 24), w4 = a5 >> 8;
-  uint4 v;
-  v.x = align_bytes(w1, w0, o);
-  v.y = align_bytes(w2, w1, o);
-  v.z = align_bytes(w3, w2, o);
-  v.w = align_bytes(w4, w3, o);
-  return v;
+  uint4 out;
+  out.x = align_bytes(w1, w0, o);
+  out.y = align_bytes(w2, w1, o);
+  out.z = align_bytes(w3, w2, o);
+  out.w = align_bytes(w4, w3, o);
+  return out;
 }
 
 // bit i set: lay[i] (live) covers row y and overlaps the chunk's pixels p0 .. p0+5

@@ -16,12 +16,12 @@
 //     file order (3 doors open/closed, 2 handles = 5-px shaft + r=4 knob + base sprite, key
 //     and gold unless moved off-screen, bolt open/locked), then the hero (mirrored when facing
 //     left).  They cover ~6 % of the pixels.
-// k_render: one workgroup per (group of 16 envs, band of 48 pixel rows), one wave per row,
+// k_render: one workgroup per (group of 8 envs, band of 48 pixel rows), one wave per row,
 // one lane per 16-B chunk of the row's RGB bytes (coalesced, every byte of every frame written
-// exactly once).  The lane loads its static chunk once and stores it into the 16 frames,
+// exactly once).  The lane loads its static chunk once and stores it into the 8 frames,
 // except where a dynamic item touches the chunk: there it composites the chunk's 6 pixels in
 // draw order and repacks.  The kernel is HBM-write bound: 1,257,984 B per frame of the
-// default level; the static layer is read once per 16 frames (from L2 / Infinity Cache).
+// default level; the static layer is read once per 8 frames (from L2 / Infinity Cache).
 //
 // The per-chunk composition and the static-layer construction live in tg_render.h (shared
 // with the host-only check build); the pixel rules are listed there.  PARITY UNPINNED against
@@ -37,19 +37,18 @@
 
 namespace tg {
 
-constexpr int RBLOCK = 256;  // 4 waves, one pixel row each
+constexpr int RBLOCK = 256;  // 4 waves
 
 struct RenderState {
   int Wpx = 0, Hpx = 0, CH = 0;  // pixels, 16-B chunks per row
   uint4* bg = nullptr;           // static layer, RGB bytes [Hpx][Wpx*3]
-  uint32_t* bg32 = nullptr;      // static layer, XRGB [Hpx][Wpx]
   uint32_t* spr = nullptr;       // [D_COUNT][48*48] ARGB
   uint64_t knob = 0;             // knob half widths + 1, 4 bits per row dy = -4..4
 };
 
 void render_free(RenderState* rs) {
   if (!rs) return;
-  void* bufs[] = {rs->bg, rs->bg32, rs->spr};
+  void* bufs[] = {rs->bg, rs->spr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete rs;
@@ -71,14 +70,20 @@ __device__ __forceinline__ void store16(uint4* p, const uint4 x) {
 #endif
 }
 
+#ifndef TG_RENDER_DIAG_NOCOMPOSE
+#define TG_RENDER_DIAG_NOCOMPOSE 0  // DIAGNOSTIC ONLY (wrong frames): store the static chunk
+#endif                               // where items are, to price the composition
+#ifndef TG_RENDER_ENV_OUTER
+#define TG_RENDER_ENV_OUTER 0
+#endif
 #ifndef TG_RENDER_G
-#define TG_RENDER_G 16  // envs per workgroup: each static-layer chunk is loaded once per G frames
+#define TG_RENDER_G 8  // envs per workgroup: each static-layer chunk is loaded once per G frames
 #endif
 constexpr int RG = TG_RENDER_G;
 
-// block = (group of RG envs, band of 48 rows); wave w renders rows w, w+4, ... of the band,
-// lane l the 16-B chunks l, l+64, ... of each row, for each env of the group in turn: the
-// static chunk is loaded once and stored RG times (composited where an item covers it).
+// block = (group of RG envs, band of 48 rows): lane l of wave w renders chunks 64w + l,
+// 64(w + 4) + l, ... of the band, for each env of the group in turn: the static chunk is
+// loaded once and stored RG times (composited where an item covers it).
 __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __restrict__ st4,
                                                    const double2* __restrict__ angs,
                                                    int64_t first, int64_t count,
@@ -113,23 +118,49 @@ __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __
     rows[k][r] = (uint16_t)(k < ne ? row_items(lay[k], live[k], ylo + r) : 0u);
   }
   __syncthreads();
+  // The band is one contiguous, 128-B aligned run of 48 * CH chunks in every frame (a frame
+  // row, 2,016 B, is not a whole number of 128-B lines): waves take 1-KB segments of it, so
+  // every store instruction writes 8 whole lines; a segment may straddle two pixel rows.
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t frame_chunks = (int64_t)A.Hpx * A.CH;
-  uint4* const base = out + e0 * frame_chunks;
-  for (int r = wave; r < RS; r += RBLOCK / 64) {
-    const int y = ylo + r;
-    for (int q0 = 0; q0 < A.CH; q0 += 64) {
-      const int q = q0 + lane;
-      if (q >= A.CH) break;
-      const uint4 v = A.bg[(int64_t)y * A.CH + q];
-      uint4* dst = base + (int64_t)y * A.CH + q;
-      for (int k = 0; k < ne; ++k, dst += frame_chunks) {
-        const uint32_t rm = rows[k][r];  // wave-uniform
-        const uint32_t hit = rm ? chunk_items(lay[k], rm, q) : 0u;
-        store16(dst, hit ? compose_chunk(A, lay[k], hit, y, q) : v);
-      }
+  const int band_chunks = RS * A.CH;
+  uint4* const base = out + e0 * frame_chunks + (int64_t)ylo * A.CH;
+  const uint4* const bgb = A.bg + (int64_t)ylo * A.CH;
+#if TG_RENDER_ENV_OUTER
+  // env by env: the block's stores stay inside one frame band at a time (DRAM page locality);
+  // the static chunk is re-read per env (an L2 hit)
+  for (int k = 0; k < ne; ++k) {
+    uint4* const fb = base + k * frame_chunks;
+    for (int c0 = wave * 64; c0 < band_chunks; c0 += RBLOCK) {
+      const int c = c0 + lane;
+      if (c >= band_chunks) break;
+      const int rs = c0 / A.CH;                            // wave-uniform first row
+      const int r = c - rs * A.CH >= A.CH ? rs + 1 : rs;  // this lane's row
+      const uint32_t rm = rows[k][r];
+      const uint32_t hit = rm ? chunk_items(lay[k], rm, c - r * A.CH) : 0u;
+      store16(fb + c, hit ? compose_chunk(A, lay[k], hit, ylo + r, c - r * A.CH, bgb[c]) : bgb[c]);
     }
   }
+#else
+  for (int c0 = wave * 64; c0 < band_chunks; c0 += RBLOCK) {
+    const int c = c0 + lane;
+    if (c >= band_chunks) break;
+    const int rs = c0 / A.CH;                            // wave-uniform first row of the segment
+    const int r = c - rs * A.CH >= A.CH ? rs + 1 : rs;  // this lane's row
+    const int q = c - r * A.CH, y = ylo + r;
+    const uint4 v = bgb[c];
+    uint4* dst = base + c;
+    for (int k = 0; k < ne; ++k, dst += frame_chunks) {
+      const uint32_t rm = rows[k][r];
+      const uint32_t hit = rm ? chunk_items(lay[k], rm, q) : 0u;
+#if TG_RENDER_DIAG_NOCOMPOSE
+      store16(dst, hit ? make_uint4(v.x ^ hit, v.y, v.z, v.w) : v);
+#else
+      store16(dst, hit ? compose_chunk(A, lay[k], hit, y, q, v) : v);
+#endif
+    }
+  }
+#endif
 }
 
 }  // namespace
@@ -168,11 +199,9 @@ int tg_render_init(tg_batch* h, const uint8_t* sprites, int32_t sw, int32_t sh) 
     return code;
   };
   if (hipMalloc((void**)&rs->bg, rgb.size()) != hipSuccess ||
-      hipMalloc((void**)&rs->bg32, bg32.size() * 4) != hipSuccess ||
       hipMalloc((void**)&rs->spr, dyn.size() * 4) != hipSuccess)
     return undo(fail(TG_E_NOMEM, "tg_render_init: device allocation failed"));
   if (hipMemcpy(rs->bg, rgb.data(), rgb.size(), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(rs->bg32, bg32.data(), bg32.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(rs->spr, dyn.data(), dyn.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return undo(fail(TG_E_HIP, "tg_render_init: upload failed"));
   render_free(h->rs);
@@ -197,7 +226,7 @@ int tg_render(tg_batch* h, int64_t first, int64_t count, uint8_t* rgb, void* str
   if (!count) return TG_OK;
   const RenderState* rs = h->rs;
   RenderArgs A;
-  A.bg = rs->bg, A.bg32 = rs->bg32, A.spr = rs->spr, A.err = h->err;
+  A.bg = rs->bg, A.spr = rs->spr, A.err = h->err;
   A.Wpx = rs->Wpx, A.Hpx = rs->Hpx, A.CH = rs->CH, A.H = h->L.H;
   A.knob = rs->knob;
   for (int k = 0; k < 3; ++k) A.door_cx[k] = h->L.door_cx[k], A.door_cy[k] = h->L.door_cy[k];

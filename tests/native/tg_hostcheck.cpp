@@ -194,7 +194,6 @@ int hc_render_run(const char* dom, const char* objs, const char* inter, uint64_t
   uint32_t err = 0;
   RenderArgs A;
   A.bg = reinterpret_cast<const uint4*>(bg.data());
-  A.bg32 = bg32.data();
   A.spr = dyn.data();
   A.err = &err;
   A.Wpx = L->W * RS, A.Hpx = L->H * RS, A.CH = A.Wpx * 3 / 16, A.H = L->H;
@@ -262,7 +261,8 @@ int hc_render_run(const char* dom, const char* objs, const char* inter, uint64_t
         const uint32_t rm = row_items(lay, live_mask, y);
         for (int q = 0; q < A.CH; ++q) {
           const uint32_t hit = rm ? chunk_items(lay, rm, q) : 0u;
-          out[(size_t)y * A.CH + q] = hit ? compose_chunk(A, lay, hit, y, q) : A.bg[(size_t)y * A.CH + q];
+          out[(size_t)y * A.CH + q] = hit ? compose_chunk(A, lay, hit, y, q, A.bg[(size_t)y * A.CH + q])
+                                : A.bg[(size_t)y * A.CH + q];
         }
       }
     }
