@@ -28,7 +28,7 @@ NUM_ACTIONS = 9
 # every symbol include/tg_amd.h declares (tests check the library exports all of them)
 EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_available_mask",
            "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing",
-           "tg_get_stats", "tg_stats_reset", "tg_read_state", "tg_render_init", "tg_frame_shape",
+           "tg_get_stats", "tg_stats_reset", "tg_read_state", "tg_write_state", "tg_render_init", "tg_frame_shape",
            "tg_render", "tg_last_error", "tg_version")
 
 
@@ -81,7 +81,8 @@ def load():
         "tg_set_timing": (i32, [P, i32]),
         "tg_get_stats": (i32, [P, ctypes.POINTER(Stats)]),
         "tg_stats_reset": (i32, [P]),
-        "tg_read_state": (i32, [P, P, P, P, P, P, P]),
+        "tg_read_state": (i32, [P, P, P, P, P, P, P, P]),
+        "tg_write_state": (i32, [P, P, P, P, P, P, P, P]),
         "tg_render_init": (i32, [P, P, i32, i32]),
         "tg_frame_shape": (i32, [P, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "tg_render": (i32, [P, i64, i64, P, P]),

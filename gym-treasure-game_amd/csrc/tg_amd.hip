@@ -360,6 +360,12 @@ __global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t 
               (lds_u32*)scratch[threadIdx.x >> 6]);
 }
 
+// the random() values of the first half (words [0, 624)) of every env (tg_write_state)
+__global__ __launch_bounds__(BLOCK) void k_gen_doubles(Soa S, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i < n) gen_doubles(S.mt + i * MT_WORDS, S.mtd + i * MT_DOUBLES);
+}
+
 __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
                                                   const uint8_t* __restrict__ mask,
                                                   double* __restrict__ obs) {
@@ -1150,7 +1156,7 @@ int tg_stats_reset(tg_batch* h) {
 }
 
 int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, double* ang,
-                  uint32_t* mt, uint32_t* mt_pos) {
+                  uint32_t* mt, uint32_t* mt_pos, int32_t* ep) {
   BIND(h);
   HIP_TRY(hipDeviceSynchronize());
   const int64_t n = h->n;
@@ -1173,18 +1179,67 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
     }
   }
   if (ang) HIP_TRY(hipMemcpy(ang, h->S.ang, sizeof(double2) * n, hipMemcpyDeviceToHost));
+  if (ep) HIP_TRY(hipMemcpy(ep, h->S.ep, sizeof(int2) * n, hipMemcpyDeviceToHost));
   if (mt || mt_pos) {
     // CPython's (mt[624], index) equivalent: the generation holding the position
     std::vector<uint4> st((size_t)n);
     HIP_TRY(hipMemcpy(st.data(), h->S.st4, sizeof(uint4) * n, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; ++i) {
-      const uint32_t p = st[(size_t)i].w;
+      const uint32_t p = st[(size_t)i].w & MT_POS_MASK;  // MT_STALE: the OTHER half is stale
       if (mt_pos) mt_pos[i] = p % MT_N;
       if (mt)
         HIP_TRY(hipMemcpy(mt + i * MT_N, h->S.mt + i * MT_WORDS + mt_half(p), sizeof(uint32_t) * MT_N,
                           hipMemcpyDeviceToHost));
     }
   }
+  return TG_OK;
+}
+
+int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const int32_t* objs,
+                   const double* ang, const uint32_t* mt, const uint32_t* mt_pos,
+                   const int32_t* ep) {
+  BIND(h);
+  if (!pos || !flags || !objs || !ang || !mt || !mt_pos)
+    return fail(TG_E_INVAL, "tg_write_state: pos, flags, objs, ang, mt and mt_pos are required");
+  const int64_t n = h->n;
+  std::vector<uint4> st((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t p = mt_pos[i];
+    if (p > (uint32_t)MT_N || (p & 1u))
+      return fail(TG_E_INVAL, "tg_write_state: env %lld: mt_pos %u (must be even, <= 624: "
+                  "random() consumes words in pairs)", (long long)i, p);
+    for (int k = 0; k < 2; ++k)
+      if (pos[2 * i + k] < -32768 || pos[2 * i + k] > 32767)
+        return fail(TG_E_INVAL, "tg_write_state: env %lld: position out of range", (long long)i);
+    for (int k = 0; k < 4; ++k)
+      if (objs[4 * i + k] < -128 || objs[4 * i + k] > 127)
+        return fail(TG_E_INVAL, "tg_write_state: env %lld: object cell out of range", (long long)i);
+    Env e{};
+    e.px = pos[2 * i], e.py = pos[2 * i + 1];
+    e.f = flags[i];
+    e.kx = objs[4 * i], e.ky = objs[4 * i + 1], e.gx = objs[4 * i + 2], e.gy = objs[4 * i + 3];
+    // the given generation goes to half 0, its successor to half 1 (fresh); index 624 is the
+    // start of the successor (CPython twists before its next draw)
+    e.mti = p;
+    uint4 w;
+    w.x = ((uint32_t)e.px & 0xFFFFu) | ((uint32_t)e.py << 16);
+    w.y = e.f;
+    w.z = ((uint32_t)e.kx & 0xFF) | (((uint32_t)e.ky & 0xFF) << 8) | (((uint32_t)e.gx & 0xFF) << 16) |
+          ((uint32_t)e.gy << 24);
+    w.w = e.mti;
+    st[(size_t)i] = w;
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h->S.st4, st.data(), sizeof(uint4) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->S.ang, ang, sizeof(double2) * n, hipMemcpyHostToDevice));
+  if (ep) HIP_TRY(hipMemcpy(h->S.ep, ep, sizeof(int2) * n, hipMemcpyHostToDevice));
+  else HIP_TRY(hipMemset(h->S.ep, 0, sizeof(int2) * n));
+  HIP_TRY(hipMemcpy2D(h->S.mt, sizeof(uint32_t) * MT_WORDS, mt, sizeof(uint32_t) * MT_N,
+                      sizeof(uint32_t) * MT_N, (size_t)n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_gen_doubles, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n);
+  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, 0u);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
   return TG_OK;
 }
 

@@ -284,21 +284,56 @@ class TreasureGameVec:
               "tg_render")
         return out
 
+    STATE_KEYS = ("pos", "flags", "objs", "ang", "mt", "mt_pos", "ep")
+
     def read_state(self, mt=False):
-        """Host copy of the SoA state (checkpoints / tests)."""
+        """Host copy of the SoA state (checkpoints / tests); ``mt=True`` adds each env's
+        ``random.getstate()`` equivalent (624 MT words + index)."""
         n = self.num_envs
         out = {"pos": np.zeros((n, 2), np.int32), "flags": np.zeros(n, np.uint32),
                "objs": np.zeros((n, 4), np.int32), "ang": np.zeros((n, 2), np.float64),
-               "mt_pos": np.zeros(n, np.uint32)}
+               "mt_pos": np.zeros(n, np.uint32), "ep": np.zeros((n, 2), np.int32)}
         if mt:
             out["mt"] = np.zeros((n, 624), np.uint32)
 
         def p(k):
             return out[k].ctypes.data_as(ctypes.c_void_p) if k in out else None
 
-        check(self._L.tg_read_state(self.handle, p("pos"), p("flags"), p("objs"), p("ang"),
-                                    p("mt"), p("mt_pos")), "tg_read_state")
+        check(self._L.tg_read_state(self.handle, *[p(k) for k in self.STATE_KEYS]),
+              "tg_read_state")
         return out
+
+    def write_state(self, state):
+        """Restore a ``read_state(mt=True)`` snapshot (same num_envs): every env continues
+        bit-exactly from it."""
+        n = self.num_envs
+        shapes = {"pos": (n, 2), "flags": (n,), "objs": (n, 4), "ang": (n, 2), "mt": (n, 624),
+                  "mt_pos": (n,), "ep": (n, 2)}
+        dt = {"pos": np.int32, "flags": np.uint32, "objs": np.int32, "ang": np.float64,
+              "mt": np.uint32, "mt_pos": np.uint32, "ep": np.int32}
+        arrs = {}
+        for k in self.STATE_KEYS:
+            if k not in state:
+                if k == "ep":
+                    continue
+                raise KeyError("state lacks %r (use read_state(mt=True))" % k)
+            a = np.ascontiguousarray(state[k], dt[k])
+            if a.shape != shapes[k]:
+                raise ValueError("state[%r] has shape %s, expected %s" % (k, a.shape, shapes[k]))
+            arrs[k] = a
+        torch.cuda.synchronize(self.device)
+        check(self._L.tg_write_state(self.handle, *[arrs[k].ctypes.data_as(ctypes.c_void_p)
+                                                    if k in arrs else None
+                                                    for k in self.STATE_KEYS]), "tg_write_state")
+
+    def save(self, path):
+        """Checkpoint every env's state (np.savez)."""
+        np.savez(path, **self.read_state(mt=True))
+
+    def load(self, path):
+        """Resume from a ``save`` checkpoint."""
+        with np.load(path) as z:
+            self.write_state({k: z[k] for k in z.files})
 
 
 class TreasureGame:

@@ -309,3 +309,44 @@ def test_every_env_hash_vs_oracle(tg, oracle, mode):
         g = run_gpu(tg, 11, 0, n, steps, a0, 0, True, hash_only=True, mode=mode)
         bad = np.flatnonzero(g["hash"] != r["hash"])
         assert len(bad) == 0, "run %d: %d envs differ, first %s" % (rep, len(bad), bad[:8].tolist())
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_checkpoint_restore_continues_bit_exact(tg, oracle, tmp_path, mode):
+    """read_state(mt=True) -> write_state into another batch (other seed): both continue
+    identically, and equal the oracle's uninterrupted run (masked policy, auto-reset)."""
+    n, t0, t1, a0 = 2048, 30, 45, 0xC4EC
+    a = tg.TreasureGameVec(n, seed=0, autoreset=True, mode=mode)
+    a.reset()
+    for t in range(t0):
+        a.step(a.policy_actions(t, a0, "masked"))
+    snap = a.read_state(mt=True)
+    path = str(tmp_path / "ckpt.npz")
+    a.save(path)
+    b = tg.TreasureGameVec(n, seed=987654, autoreset=True, mode=mode)
+    b.load(path)
+    ref = oracle.run(0, 0, n, t0 + t1, a0, 1, True)
+    for t in range(t0, t0 + t1):
+        oa, ra, va, da, _ = a.step(a.policy_actions(t, a0, "masked"))
+        ob, rb, vb, db, _ = b.step(b.policy_actions(t, a0, "masked"))
+        got = ob.cpu().numpy()
+        assert np.array_equal(oa.cpu().numpy().view(np.uint64), got.view(np.uint64))
+        assert np.array_equal(got.view(np.uint64), ref["obs"][:, t + 1].view(np.uint64)), t
+        assert torch.equal(ra, rb) and torch.equal(va, vb) and torch.equal(da, db)
+        assert np.array_equal(rb.cpu().numpy(), ref["reward"][:, t + 1])
+    sa, sb = a.read_state(mt=True), b.read_state(mt=True)
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    assert a.errors() == 0 and b.errors() == 0
+    # the snapshot's RNG part is CPython's getstate(): Python's random accepts it as a state
+    import random
+    r = random.Random()
+    r.setstate((3, tuple(int(w) for w in snap["mt"][5]) + (int(snap["mt_pos"][5]),), None))
+    assert 0.0 <= r.random() < 1.0
+    bad = dict(snap)
+    bad["mt_pos"] = snap["mt_pos"].copy()
+    bad["mt_pos"][3] |= 1
+    with pytest.raises(tg.TgError):
+        b.write_state(bad)
+    a.close()
+    b.close()
