@@ -28,4 +28,11 @@ step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$TAG" -o run --
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$TAG" -o run --output-format csv -- python3 bench.py $PMC_ARGS
 step pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d "$OUT/pmc_sq1_$TAG" -o run --output-format csv -- python3 bench.py $PMC_ARGS
 step pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2_$TAG" -o run --output-format csv -- python3 bench.py $PMC_ARGS
+if [ "${C5:-0}" = 1 ]; then  # config C5: the same passes over the render workload
+  C5_ARGS="--workload c5 --steps 10 --warmup 2 --cpu-seconds 0"
+  step bench_c5 600 python bench.py --workload c5 --steps 30 --warmup 3
+  step trace_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_${TAG}c5" -o run --output-format csv -- python3 bench.py $C5_ARGS
+  step pmc_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_${TAG}c5" -o run --output-format csv -- python3 bench.py $C5_ARGS
+  step pmc_write_c5 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_${TAG}c5" -o run --output-format csv -- python3 bench.py $C5_ARGS
+fi
 echo "== all done"

@@ -55,7 +55,11 @@ def main():
     ap.add_argument("--envs", type=int, default=1 << 20)
     ap.add_argument("--policy", default="uniform")
     ap.add_argument("--mode", default="compact")
+    ap.add_argument("--render", action="store_true",
+                    help="the C5 passes (<tag>c5): k_render -> profiles/traffic_render.json")
     a = ap.parse_args()
+    if a.render:
+        return render_summary(a)
     res = {"tag": a.tag, "envs": a.envs, "policy": a.policy}
     ks = kernel_stats(os.path.join(a.out, "trace_" + a.tag, "run_kernel_stats.csv"))
     res["kernel_trace"] = ks
@@ -99,6 +103,36 @@ def main():
     with open(os.path.join(ROOT, "profiles", "%s_summary.json" % a.tag), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps({k: res[k] for k in res if k in ("hbm", "step_kernels_avg_ns")}, indent=1))
+
+
+def render_summary(a):
+    """k_render's HBM bytes per launch from the C5 passes (bench.py --workload c5)."""
+    tag = a.tag + "c5"
+    envs = a.envs if a.envs != 1 << 20 else 65536
+    ks = kernel_stats(os.path.join(a.out, "trace_" + tag, "run_kernel_stats.csv"))
+    pm = {}
+    for p in ("fetch", "write"):
+        path = os.path.join(a.out, "pmc_%s_%s" % (p, tag), "run_counter_collection.csv")
+        avg, _ = counters(path)
+        for k, d in avg.items():
+            pm.setdefault(k, {}).update(d)
+    known = 16.0 * envs  # k_errors (vec.errors() at the end of the bench): 16 B per env
+    raw_err = pm["k_errors"]["FETCH_SIZE"] * 1024.0
+    cal = known / raw_err if raw_err > 0 else 1.0
+    fr = pm["k_render"]["FETCH_SIZE"] * 1024.0
+    wr = pm["k_render"]["WRITE_SIZE"] * 1024.0
+    res = {"tag": tag, "envs": envs, "kernel_trace": ks, "pmc_avg_per_dispatch": pm,
+           "k_render": {"fetch_bytes_raw": fr, "fetch_bytes": fr * cal, "write_bytes": wr,
+                        "frame_bytes_algorithmic": 1257984 * envs,
+                        "avg_ns": ks["k_render"]["avg_ns"]},
+           "fetch_calibration": cal}
+    with open(os.path.join(ROOT, "profiles", "%s_summary.json" % tag), "w") as f:
+        json.dump(res, f, indent=1)
+    tj = {"envs": envs, "kernel": "k_render", "hbm_bytes_per_launch": fr * cal + wr,
+          "avg_ns": ks["k_render"]["avg_ns"], "source": "profiles/%s_summary.json" % tag}
+    with open(os.path.join(ROOT, "profiles", "traffic_render.json"), "w") as f:
+        json.dump(tj, f, indent=1)
+    print(json.dumps(res["k_render"], indent=1))
 
 
 if __name__ == "__main__":
