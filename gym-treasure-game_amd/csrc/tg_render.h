@@ -38,9 +38,12 @@ constexpr int NLAYER = 9;                  // 8 objects in file order + the hero
 // Everything the composition reads besides the env's state words.
 struct RenderArgs {
   const uint4* bg;       // static layer, RGB bytes [Hpx][Wpx*3] as 16-B chunks
+  const uint4* tiles;    // static layer + one cell-aligned sprite, per (cell, D_* sprite):
+                         // [H*W][D_COUNT][48 rows][9 chunks]
   const uint32_t* spr;   // dynamic sprites [D_COUNT][48*48] ARGB
   uint32_t* err;         // device error word (TG_ERR_RENDER)
   int Wpx, Hpx, CH, H;   // pixels, 16-B chunks per row, cell rows (= bands)
+  int W;                 // cell columns
   uint64_t knob;         // knob half width + 1 per scanline dy = -4..4, 4 bits each
   int8_t door_cx[3], door_cy[3], handle_cx[2], handle_cy[2], bolt_cx, bolt_cy;
 };
@@ -53,7 +56,11 @@ struct Layer {
   // t = 0..dM-1 (major / minor axis steps); the 5 lines are it shifted by k*(ux, uy),
   // k in {0, 1, -1, 2, -2}; knob centre (ex, ey).  handle == 0: a plain sprite.
   int handle, lx, ly, mx, my, nx, ny, dM, dm, magic, ux, uy, ex, ey;
+  int sx0, sx1, sy0, sy1;  // the shaft + knob's own bounding box (handles)
 };
+constexpr int CELL_CHUNKS = RS * 3 / 16;  // 9: a cell row is 144 B, whole 16-B chunks
+constexpr uint32_t HERO_ITEM = 1u << 8, HANDLE_ITEMS = (1u << 3) | (1u << 4);
+constexpr uint16_t SRC_STATIC = 0xFFFFu, SRC_COMPOSE = 0xFFFEu;  // per-cell source selectors
 
 TG_HD uint32_t blend_px(uint32_t d, uint32_t s) {
   const uint32_t a = s >> 24;
@@ -128,10 +135,12 @@ TG_HD uint32_t make_layer(const RenderArgs& A, int i, const uint4 st, const doub
     const bool off_y = iabs(dx) > iabs(dy);  // clip_and_draw_line_width's xinc / yinc
     l.ux = off_y ? 0 : 1, l.uy = off_y ? 1 : 0;
     l.ex = x2, l.ey = y2;
-    l.x0 = imin(l.x0, imin(imin(x1, x2) - 2 * l.ux, x2 - KNOB_R));
-    l.x1 = imax(l.x1, imax(imax(x1, x2) + 2 * l.ux + 1, x2 + KNOB_R + 1));
-    l.y0 = imin(l.y0, imin(imin(y1, y2) - 2 * l.uy, y2 - KNOB_R));
-    l.y1 = imax(l.y1, imax(imax(y1, y2) + 2 * l.uy + 1, y2 + KNOB_R + 1));
+    l.sx0 = imin(imin(x1, x2) - 2 * l.ux, x2 - KNOB_R);
+    l.sx1 = imax(imax(x1, x2) + 2 * l.ux + 1, x2 + KNOB_R + 1);
+    l.sy0 = imin(imin(y1, y2) - 2 * l.uy, y2 - KNOB_R);
+    l.sy1 = imax(imax(y1, y2) + 2 * l.uy + 1, y2 + KNOB_R + 1);
+    l.x0 = imin(l.x0, l.sx0), l.x1 = imax(l.x1, l.sx1);
+    l.y0 = imin(l.y0, l.sy0), l.y1 = imax(l.y1, l.sy1);
     if (l.x0 < 0 || l.y0 < 0 || l.x1 > A.Wpx || l.y1 > A.Hpx) err |= TG_ERR_RENDER;
   }
   return err;
@@ -238,6 +247,44 @@ TG_HD uint32_t chunk_items(const Layer* lay, uint32_t row, int q) {
     if (p0 < lay[i].x1 && p0 + 5 >= lay[i].x0) hit |= 1u << i;
   }
   return hit;
+}
+
+// Source of each cell of band `band` for one env: SRC_STATIC, the tile of the one
+// cell-aligned item there (doors, handle bases, key, bolt, gold all sit on whole cells), or
+// SRC_COMPOSE where two share a cell.  sel has W entries.
+TG_HD void cell_sources(const Layer* lay, uint32_t live, int band, int W, uint16_t* sel) {
+  for (int c = 0; c < W; ++c) sel[c] = SRC_STATIC;
+  for (uint32_t m = live & 0xFFu; m; m &= m - 1) {
+    const Layer& l = lay[__builtin_ctz(m)];
+    if (l.oy != band * RS) continue;
+    const int c = l.ox / RS;
+    sel[c] = sel[c] == SRC_STATIC ? (uint16_t)l.spr : SRC_COMPOSE;
+  }
+}
+
+// The 16 frame bytes [16q, 16q+16) of row y (row r of band `band`) for one env: `rm` = its
+// items on the row, `sel` its cell sources, `v` the static chunk.  Chunks a handle's shaft or
+// knob touches (or a two-item cell) are composed from the static layer with every item in
+// draw order; elsewhere the cell's tile (static + its item) is the base and only the hero,
+// drawn last, is composited over it.
+TG_HD uint4 render_chunk(const RenderArgs& A, const Layer* lay, uint32_t rm, const uint16_t* sel,
+                         int band, int r, int q, const uint4 v) {
+  const uint32_t hit = rm ? chunk_items(lay, rm, q) : 0u;
+  if (!hit) return v;
+  const int y = band * RS + r, cc = q / CELL_CHUNKS;
+  const uint16_t s = sel[cc];
+  bool full = s == SRC_COMPOSE;
+  const int p0 = (16 * q) / 3;
+  for (uint32_t m = hit & HANDLE_ITEMS; m; m &= m - 1) {
+    const Layer& l = lay[__builtin_ctz(m)];
+    full |= y >= l.sy0 && y < l.sy1 && p0 < l.sx1 && p0 + 5 >= l.sx0;
+  }
+  if (full) return compose_chunk(A, lay, hit, y, q, v);
+  const uint4 src = s == SRC_STATIC
+                        ? v
+                        : A.tiles[((size_t)(band * A.W + cc) * D_COUNT + s) * (RS * CELL_CHUNKS) +
+                                  (size_t)r * CELL_CHUNKS + (q - cc * CELL_CHUNKS)];
+  return (hit & HERO_ITEM) ? compose_chunk(A, lay, HERO_ITEM, y, q, src) : src;
 }
 
 // ---- host: the static layer (tg_render_init) ---------------------------------------------
@@ -361,6 +408,26 @@ inline std::vector<uint32_t> dynamic_sprites(const std::vector<uint32_t>& sc) {
         dyn[(size_t)d * RS2 + v * RS + u] =
             sc[(size_t)src_of[d] * RS2 + v * RS + (d == D_HERO_FLIP ? RS - 1 - u : u)];
   return dyn;
+}
+
+// Tiles: every cell of the static layer with each cell-aligned sprite blended over it
+// ([W*H][D_COUNT][48][48] XRGB; the hero slots are unused), as RGB bytes by rgb_bytes().
+inline std::vector<uint32_t> cell_tiles(const std::vector<uint32_t>& bg, int W, int H,
+                                        const std::vector<uint32_t>& dyn) {
+  const int Wpx = W * RS;
+  std::vector<uint32_t> t((size_t)W * H * D_COUNT * RS2);
+  for (int i = 0; i < H; ++i)
+    for (int j = 0; j < W; ++j)
+      for (int d = 0; d < D_COUNT; ++d) {
+        uint32_t* o = &t[((size_t)(i * W + j) * D_COUNT + d) * RS2];
+        const bool hero = d == D_HERO || d == D_HERO_FLIP;
+        for (int v = 0; v < RS; ++v)
+          for (int u = 0; u < RS; ++u) {
+            const uint32_t b = bg[(size_t)(i * RS + v) * Wpx + j * RS + u];
+            o[v * RS + u] = hero ? b : blend_px(b, dyn[(size_t)d * RS2 + v * RS + u]);
+          }
+      }
+  return t;
 }
 
 inline std::vector<uint8_t> rgb_bytes(const std::vector<uint32_t>& px) {

@@ -16,12 +16,12 @@
 //     file order (3 doors open/closed, 2 handles = 5-px shaft + r=4 knob + base sprite, key
 //     and gold unless moved off-screen, bolt open/locked), then the hero (mirrored when facing
 //     left).  They cover ~6 % of the pixels.
-// k_render: one workgroup per (group of 8 envs, band of 48 pixel rows), one wave per row,
+// k_render: one workgroup per (group of 4 envs, band of 48 pixel rows), one wave per row,
 // one lane per 16-B chunk of the row's RGB bytes (coalesced, every byte of every frame written
-// exactly once).  The lane loads its static chunk once and stores it into the 8 frames,
+// exactly once).  The lane loads its static chunk once and stores it into the 4 frames,
 // except where a dynamic item touches the chunk: there it composites the chunk's 6 pixels in
 // draw order and repacks.  The kernel is HBM-write bound: 1,257,984 B per frame of the
-// default level; the static layer is read once per 8 frames (from L2 / Infinity Cache).
+// default level; the static layer is read once per 4 frames (from L2 / Infinity Cache).
 //
 // The per-chunk composition and the static-layer construction live in tg_render.h (shared
 // with the host-only check build); the pixel rules are listed there.  PARITY UNPINNED against
@@ -37,18 +37,22 @@
 
 namespace tg {
 
-constexpr int RBLOCK = 256;  // 4 waves
+#ifndef TG_RENDER_BLOCK
+#define TG_RENDER_BLOCK 256  // 4 waves
+#endif
+constexpr int RBLOCK = TG_RENDER_BLOCK;
 
 struct RenderState {
   int Wpx = 0, Hpx = 0, CH = 0;  // pixels, 16-B chunks per row
   uint4* bg = nullptr;           // static layer, RGB bytes [Hpx][Wpx*3]
+  uint4* tiles = nullptr;        // static layer + each cell-aligned sprite, per cell
   uint32_t* spr = nullptr;       // [D_COUNT][48*48] ARGB
   uint64_t knob = 0;             // knob half widths + 1, 4 bits per row dy = -4..4
 };
 
 void render_free(RenderState* rs) {
   if (!rs) return;
-  void* bufs[] = {rs->bg, rs->spr};
+  void* bufs[] = {rs->bg, rs->tiles, rs->spr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete rs;
@@ -56,30 +60,34 @@ void render_free(RenderState* rs) {
 
 namespace {
 
-#ifndef TG_RENDER_NT
-#define TG_RENDER_NT 1  // non-temporal frame stores (streamed once, never re-read here)
-#endif
+#ifndef TG_RENDER_STORE
+#define TG_RENDER_STORE 1  // frame stores: 0 plain, 1 non-temporal (streamed once, never
+#endif                     // re-read here); A/B only: 2 sc1, 3 sc0 sc1, 4 nt sc1
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void store16(uint4* p, const uint4 x) {
   u32x4 v = {x.x, x.y, x.z, x.w};
-#if TG_RENDER_NT
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-#else
+#if TG_RENDER_STORE == 0
   *reinterpret_cast<u32x4*>(p) = v;
+#elif TG_RENDER_STORE == 1
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+#elif TG_RENDER_STORE == 2
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#elif TG_RENDER_STORE == 3
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+#else
+  asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
 #endif
 }
 
 #ifndef TG_RENDER_DIAG_NOCOMPOSE
 #define TG_RENDER_DIAG_NOCOMPOSE 0  // DIAGNOSTIC ONLY (wrong frames): store the static chunk
 #endif                               // where items are, to price the composition
-#ifndef TG_RENDER_ENV_OUTER
-#define TG_RENDER_ENV_OUTER 0
-#endif
 #ifndef TG_RENDER_G
-#define TG_RENDER_G 8  // envs per workgroup: each static-layer chunk is loaded once per G frames
+#define TG_RENDER_G 4  // envs per workgroup: each static-layer chunk is loaded once per G frames
 #endif
 constexpr int RG = TG_RENDER_G;
+constexpr int MAX_W = 128;  // cell columns (levels are at most 120 wide, tg_level.h)
 
 // block = (group of RG envs, band of 48 rows): lane l of wave w renders chunks 64w + l,
 // 64(w + 4) + l, ... of the band, for each env of the group in turn: the static chunk is
@@ -91,6 +99,11 @@ __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __
   __shared__ Layer lay[RG][NLAYER];
   __shared__ uint32_t live[RG];
   __shared__ uint16_t rows[RG][RS];  // items covering each row of the band, per env
+  __shared__ uint16_t sel[RG][MAX_W];  // each cell's source, per env
+#ifdef TG_RENDER_LDS_PAD  // A/B only: cap the workgroups per CU
+  __shared__ uint8_t pad[TG_RENDER_LDS_PAD];
+  if (threadIdx.x == 0) pad[blockIdx.x % TG_RENDER_LDS_PAD] = 0;
+#endif
   const int64_t grp = blockIdx.x / A.H;
   const int band = (int)(blockIdx.x - grp * A.H);
   const int ylo = band * RS;
@@ -117,6 +130,8 @@ __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __
     const int k = t / RS, r = t - k * RS;
     rows[k][r] = (uint16_t)(k < ne ? row_items(lay[k], live[k], ylo + r) : 0u);
   }
+  if (threadIdx.x < RG && (int)threadIdx.x < ne)
+    cell_sources(lay[threadIdx.x], live[threadIdx.x], band, A.W, sel[threadIdx.x]);
   __syncthreads();
   // The band is one contiguous, 128-B aligned run of 48 * CH chunks in every frame (a frame
   // row, 2,016 B, is not a whole number of 128-B lines): waves take 1-KB segments of it, so
@@ -126,41 +141,25 @@ __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __
   const int band_chunks = RS * A.CH;
   uint4* const base = out + e0 * frame_chunks + (int64_t)ylo * A.CH;
   const uint4* const bgb = A.bg + (int64_t)ylo * A.CH;
-#if TG_RENDER_ENV_OUTER
-  // env by env: the block's stores stay inside one frame band at a time (DRAM page locality);
-  // the static chunk is re-read per env (an L2 hit)
-  for (int k = 0; k < ne; ++k) {
-    uint4* const fb = base + k * frame_chunks;
-    for (int c0 = wave * 64; c0 < band_chunks; c0 += RBLOCK) {
-      const int c = c0 + lane;
-      if (c >= band_chunks) break;
-      const int rs = c0 / A.CH;                            // wave-uniform first row
-      const int r = c - rs * A.CH >= A.CH ? rs + 1 : rs;  // this lane's row
-      const uint32_t rm = rows[k][r];
-      const uint32_t hit = rm ? chunk_items(lay[k], rm, c - r * A.CH) : 0u;
-      store16(fb + c, hit ? compose_chunk(A, lay[k], hit, ylo + r, c - r * A.CH, bgb[c]) : bgb[c]);
-    }
-  }
-#else
   for (int c0 = wave * 64; c0 < band_chunks; c0 += RBLOCK) {
     const int c = c0 + lane;
     if (c >= band_chunks) break;
     const int rs = c0 / A.CH;                            // wave-uniform first row of the segment
     const int r = c - rs * A.CH >= A.CH ? rs + 1 : rs;  // this lane's row
-    const int q = c - r * A.CH, y = ylo + r;
+    const int q = c - r * A.CH;
     const uint4 v = bgb[c];
     uint4* dst = base + c;
     for (int k = 0; k < ne; ++k, dst += frame_chunks) {
       const uint32_t rm = rows[k][r];
-      const uint32_t hit = rm ? chunk_items(lay[k], rm, q) : 0u;
 #if TG_RENDER_DIAG_NOCOMPOSE
+      const uint32_t hit = rm ? chunk_items(lay[k], rm, q) : 0u;
+      (void)sel;
       store16(dst, hit ? make_uint4(v.x ^ hit, v.y, v.z, v.w) : v);
 #else
-      store16(dst, hit ? compose_chunk(A, lay[k], hit, y, q, v) : v);
+      store16(dst, rm ? render_chunk(A, lay[k], rm, sel[k], band, r, q, v) : v);
 #endif
     }
   }
-#endif
 }
 
 }  // namespace
@@ -191,6 +190,7 @@ int tg_render_init(tg_batch* h, const uint8_t* sprites, int32_t sw, int32_t sh) 
   const std::vector<uint32_t> bg32 = static_layer(desc, W, H, sc);
   const std::vector<uint8_t> rgb = rgb_bytes(bg32);
   const std::vector<uint32_t> dyn = dynamic_sprites(sc);
+  const std::vector<uint8_t> tiles = rgb_bytes(cell_tiles(bg32, W, H, dyn));
   RenderState* rs = new RenderState();
   rs->Wpx = Wpx, rs->Hpx = Hpx, rs->CH = Wpx * 3 / 16;  // W * 144 bytes per row: whole chunks
   rs->knob = knob_table(KNOB_R);
@@ -199,9 +199,11 @@ int tg_render_init(tg_batch* h, const uint8_t* sprites, int32_t sw, int32_t sh) 
     return code;
   };
   if (hipMalloc((void**)&rs->bg, rgb.size()) != hipSuccess ||
+      hipMalloc((void**)&rs->tiles, tiles.size()) != hipSuccess ||
       hipMalloc((void**)&rs->spr, dyn.size() * 4) != hipSuccess)
     return undo(fail(TG_E_NOMEM, "tg_render_init: device allocation failed"));
   if (hipMemcpy(rs->bg, rgb.data(), rgb.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(rs->tiles, tiles.data(), tiles.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(rs->spr, dyn.data(), dyn.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return undo(fail(TG_E_HIP, "tg_render_init: upload failed"));
   render_free(h->rs);
@@ -226,8 +228,8 @@ int tg_render(tg_batch* h, int64_t first, int64_t count, uint8_t* rgb, void* str
   if (!count) return TG_OK;
   const RenderState* rs = h->rs;
   RenderArgs A;
-  A.bg = rs->bg, A.spr = rs->spr, A.err = h->err;
-  A.Wpx = rs->Wpx, A.Hpx = rs->Hpx, A.CH = rs->CH, A.H = h->L.H;
+  A.bg = rs->bg, A.tiles = rs->tiles, A.spr = rs->spr, A.err = h->err;
+  A.Wpx = rs->Wpx, A.Hpx = rs->Hpx, A.CH = rs->CH, A.H = h->L.H, A.W = h->L.W;
   A.knob = rs->knob;
   for (int k = 0; k < 3; ++k) A.door_cx[k] = h->L.door_cx[k], A.door_cy[k] = h->L.door_cy[k];
   for (int k = 0; k < 2; ++k) A.handle_cx[k] = h->L.handle_cx[k], A.handle_cy[k] = h->L.handle_cy[k];

@@ -191,9 +191,12 @@ int hc_render_run(const char* dom, const char* objs, const char* inter, uint64_t
   const std::vector<uint32_t> bg32 = static_layer(desc, L->W, L->H, sc);
   const std::vector<uint8_t> bg = rgb_bytes(bg32);
   const std::vector<uint32_t> dyn = dynamic_sprites(sc);
+  const std::vector<uint8_t> tiles = rgb_bytes(cell_tiles(bg32, L->W, L->H, dyn));
   uint32_t err = 0;
   RenderArgs A;
   A.bg = reinterpret_cast<const uint4*>(bg.data());
+  A.tiles = reinterpret_cast<const uint4*>(tiles.data());
+  A.W = L->W;
   A.spr = dyn.data();
   A.err = &err;
   A.Wpx = L->W * RS, A.Hpx = L->H * RS, A.CH = A.Wpx * 3 / 16, A.H = L->H;
@@ -256,13 +259,14 @@ int hc_render_run(const char* dom, const char* objs, const char* inter, uint64_t
         live = live && lay[k].y1 > ylo && lay[k].y0 < ylo + RS && lay[k].x1 > 0 && lay[k].x0 < A.Wpx;
         live_mask |= (uint32_t)live << k;
       }
+      std::vector<uint16_t> sel((size_t)A.W);
+      cell_sources(lay, live_mask, band, A.W, sel.data());
       for (int r = 0; r < RS; ++r) {
         const int y = ylo + r;
         const uint32_t rm = row_items(lay, live_mask, y);
         for (int q = 0; q < A.CH; ++q) {
-          const uint32_t hit = rm ? chunk_items(lay, rm, q) : 0u;
-          out[(size_t)y * A.CH + q] = hit ? compose_chunk(A, lay, hit, y, q, A.bg[(size_t)y * A.CH + q])
-                                : A.bg[(size_t)y * A.CH + q];
+          const uint4 v = A.bg[(size_t)y * A.CH + q];
+          out[(size_t)y * A.CH + q] = rm ? render_chunk(A, lay, rm, sel.data(), band, r, q, v) : v;
         }
       }
     }

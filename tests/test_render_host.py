@@ -4,6 +4,7 @@ frame composition (csrc/tg_render.h, host-only build in tests/native, driven ban
 chunk by chunk as k_render's lanes are).  The renderer's parity with the reference itself is
 UNPINNED: pygame is absent from this image."""
 import ctypes
+import os
 import random
 
 import numpy as np
@@ -16,10 +17,21 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def hc_frames(lib, envs, steps, a0, policy, autoreset, sprites, seed_base=0):
+OVERLAP = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels",
+                       "render_overlap")
+
+
+def level_texts(level_dir):
+    if level_dir is None:
+        return None, None, None
+    return tuple(open(os.path.join(level_dir, f), "rb").read()
+                 for f in ("domain.txt", "domain-objects.txt", "domain-interactions.txt"))
+
+
+def hc_frames(lib, envs, steps, a0, policy, autoreset, sprites, seed_base=0, level_dir=None):
     envs = np.ascontiguousarray(envs, np.int64)
     out = np.zeros((len(envs), 624, 672, 3), np.uint8)
-    rc = lib.hc_render_run(None, None, None, seed_base, _p(envs), len(envs), steps, a0, policy,
+    rc = lib.hc_render_run(*level_texts(level_dir), seed_base, _p(envs), len(envs), steps, a0, policy,
                            int(autoreset), _p(sprites), sprites.shape[2], sprites.shape[1], _p(out))
     assert rc == 0
     return out
@@ -66,6 +78,16 @@ def test_composition_covers_every_item(hostcheck, oracle):
     want = oracle.run_render(0, envs, 150, 0xBEEF, 1, False, sprites)
     np.testing.assert_array_equal(got, want)
     assert len({g.tobytes() for g in got}) > 32
+
+
+@pytest.mark.parametrize("steps", [0, 20, 80])
+def test_composition_vs_oracle_overlapping_items(hostcheck, oracle, steps):
+    """Two items on one cell (key on the bolt) and a shaft crossing a later item's cell."""
+    sprites = R.synthetic_sprites(seed=3)
+    envs = np.arange(16)
+    got = hc_frames(hostcheck, envs, steps, 5, 1, True, sprites, level_dir=OVERLAP)
+    want = oracle.run_render(0, envs, steps, 5, 1, True, sprites, level_dir=OVERLAP)
+    np.testing.assert_array_equal(got, want)
 
 
 def test_real_sprites_if_present(hostcheck, oracle):
