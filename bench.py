@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--mode", default="compact", choices=["compact", "direct"],
                     help="step implementation (bit-identical): two-pass compacted or one-pass")
     ap.add_argument("--run-blocks", type=int, default=0, help="k_run workgroups (0 = default)")
+    ap.add_argument("--rollout", type=int, default=0,
+                    help="K > 0: tg_rollout, K steps per call with the policy evaluated inside "
+                         "the step kernels (episodes drained / gathered every K steps); 0: the "
+                         "per-step API (tg_policy_actions + tg_step + drain every step)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU-baseline sample (0 disables it)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_step.json"),
@@ -176,9 +180,22 @@ def main():
         frames = torch.empty((count,) + vec.frame_shape, dtype=torch.uint8, device=dev)
     timing = [False]
 
+    K = args.rollout
+    if K:
+        if c5 or args.steps % K or args.warmup % K:
+            raise SystemExit("--rollout K: c3 only, with --steps and --warmup multiples of K")
+        roll = [torch.empty((K, count), dtype=d, device=dev)
+                for d in (torch.int32, torch.uint8, torch.uint8)]
+
     def one_step(t):
-        tg._lib.check(L.tg_policy_actions(h, ACTION_SEED, t, pol, p(act), stream), "actions")
-        tg._lib.check(L.tg_step(*args_step), "tg_step")
+        if K:  # steps t .. t+K-1 in one call
+            if t % K:
+                return
+            tg._lib.check(L.tg_rollout(h, K, ACTION_SEED, t, pol, flags, None, None,
+                                       p(roll[0]), p(roll[1]), p(roll[2]), stream), "rollout")
+        else:
+            tg._lib.check(L.tg_policy_actions(h, ACTION_SEED, t, pol, p(act), stream), "actions")
+            tg._lib.check(L.tg_step(*args_step), "tg_step")
         tg._lib.check(L.tg_episodes(h, p(ep_rows), p(ep_cnt), EP_CAP, stream), "episodes")
         if c5:
             if timing[0]:  # k_render alone, on the stream it is launched on
@@ -273,6 +290,8 @@ def main():
             "config": {"workload": workload,
                        "envs_per_gpu": args.envs, "total_envs": total, "policy": args.policy,
                        "autoreset": autoreset, "step_mode": args.mode,
+                       "api": ("tg_rollout x%d (policy inside the step kernels)" % K if K
+                               else "tg_policy_actions + tg_step per step"),
                        "parallelism": "env-shard x%d" % world},
             "ticks_per_s": node["ticks"] / dt,
             "valid_step_frac": node["valid_steps"] / max(node["steps"], 1),

@@ -400,13 +400,41 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
 }
 
 struct StepIO {
-  const int32_t* __restrict__ actions;
+  int32_t* __restrict__ actions;   // input; with policy >= 0 the step's actions are written here
   double* __restrict__ obs;
   int32_t* __restrict__ reward;
   uint8_t* __restrict__ valid;
   uint8_t* __restrict__ done;
   double* __restrict__ final_obs;  // may be null
+  int policy;                      // -1: actions given; else TG_POLICY_* evaluated in the step
+  uint64_t a0;                     // the policy's action seed and step index
+  int64_t t;
 };
+
+__device__ __forceinline__ uint64_t sm64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+// the synthetic policies (tg_policy_actions): a[t, g] = h(a0, g, t) % 9, or the k-th set bit
+// of available_mask with k = h % popcount (masked-uniform; h % 9 when nothing can run)
+__device__ __forceinline__ int policy_action(const Level& L, const Map& m, const Env& e,
+                                             int policy, uint64_t a0, int64_t g, int64_t t) {
+  const uint64_t h = sm64(sm64(a0 ^ sm64((uint64_t)g)) ^ (uint64_t)t);
+  int a = (int)(h % 9ull);
+  if (policy == TG_POLICY_MASKED) {
+    const uint32_t mk = available_mask(L, m, e);
+    const int c = __popc(mk);
+    if (c) {
+      uint32_t k = (uint32_t)(h % (uint64_t)c);
+      uint32_t mm = mk;
+      while (k--) mm &= mm - 1u;
+      a = __ffs(mm) - 1;
+    }
+  }
+  return a;
+}
 struct EpQueue {
   tg_episode* __restrict__ eps;
   int32_t* count;
@@ -507,7 +535,14 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
     RngRing rng(S.mt + i * MT_WORDS, S.mtd + i * MT_DOUBLES, e.mti, wring);
-    r = env_step(L, trig, m, e, io.actions[i], rng);
+    int act;
+    if (io.policy >= 0) {
+      act = policy_action(L, m, e, io.policy, io.a0, g0 + i, io.t);
+      if (io.actions) io.actions[i] = act;
+    } else {
+      act = io.actions[i];
+    }
+    r = env_step(L, trig, m, e, act, rng);
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish();
     draws = rng.draws;
@@ -575,7 +610,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   int2 ep = make_int2(0, 0);
   if (live) {
     s4 = S.st4[i];
-    act = io.actions[i];
+    if (io.policy < 0) act = io.actions[i];
     a2 = S.ang[i];
     ep = S.ep[i];
   }
@@ -589,6 +624,10 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   e.mti = 0u;
   if (live) {
     unpack_st4(s4, e);
+    if (io.policy >= 0) {  // the rollout's on-device policy (tg_rollout)
+      act = policy_action(L, m, e, io.policy, io.a0, g0 + i, io.t);
+      if (io.actions) io.actions[i] = act;
+    }
     k = option_index(act);
     runs = k >= 0 && can_run(L, m, e, k);
   }
@@ -805,13 +844,6 @@ __global__ __launch_bounds__(BLOCK) void k_observe(Soa S, int64_t n, Level L,
   store_obs(obs, i, o);
 }
 
-__device__ __forceinline__ uint64_t sm64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
 // a[t, g] = h(a0, g, t) % 9, or the k-th set bit of available_mask (masked-uniform)
 __global__ __launch_bounds__(BLOCK) void k_actions(Soa S, int64_t n, Level L,
                                                     const uint32_t* __restrict__ grid,
@@ -821,22 +853,10 @@ __global__ __launch_bounds__(BLOCK) void k_actions(Soa S, int64_t n, Level L,
   if (policy == TG_POLICY_MASKED) stage_level(lv, grid, L);  // uniform branch
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
-  const uint64_t h = sm64(sm64(a0 ^ sm64((uint64_t)(g0 + i))) ^ (uint64_t)t);
-  int a = (int)(h % 9ull);
-  if (policy == TG_POLICY_MASKED) {
-    const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
-    Env e;
-    unpack(S.st4[i], S.ang[i], e);
-    const uint32_t mk = available_mask(L, m, e);
-    const int c = __popc(mk);
-    if (c) {
-      uint32_t k = (uint32_t)(h % (uint64_t)c);
-      uint32_t mm = mk;
-      while (k--) mm &= mm - 1u;
-      a = __ffs(mm) - 1;
-    }
-  }
-  out[i] = a;
+  const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
+  Env e{};
+  if (policy == TG_POLICY_MASKED) unpack(S.st4[i], S.ang[i], e);
+  out[i] = policy_action(L, m, e, policy, a0, g0 + i, t);
 }
 
 // move up to `cap` completed-episode records to `out`, keep the rest queued (device only,
@@ -990,8 +1010,9 @@ void tg_destroy(tg_batch* h) {
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   for (auto ev : h->ev) (void)hipEventDestroy(ev);
   render_free(h->rs);
-  void* bufs[] = {h->grid, h->genrand, h->S.st4, h->S.ang,   h->S.ep, h->S.mt, h->S.mtd,
-                  h->eps,  h->eps_count, h->stats, h->err, h->wl,   h->wctr, h->refill, h->nrefill};
+  void* bufs[] = {h->grid,  h->genrand, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
+                  h->S.mtd, h->eps,     h->eps_count, h->stats, h->err,  h->wl,
+                  h->wctr,  h->refill,  h->nrefill,   h->obs_scratch};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete h;
@@ -1005,14 +1026,12 @@ int tg_reset(tg_batch* h, const uint8_t* mask, double* obs, void* stream) {
   return TG_OK;
 }
 
-int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, uint8_t* valid,
-            uint8_t* done, double* final_obs, uint32_t flags, void* stream) {
-  BIND(h);
-  if (!actions || !obs || !reward || !valid || !done)
-    return fail(TG_E_INVAL, "tg_step: actions/obs/reward/valid/done are required");
-  hipStream_t st = (hipStream_t)stream;
-  const bool ar = flags & TG_STEP_AUTORESET;
-  const bool fo = final_obs != nullptr;
+}  // extern "C"
+
+namespace {
+// one step's kernels on `st`, timed with HIP events when enabled
+int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
+  const bool fo = io.final_obs != nullptr;
   if (h->timing) {
     while (h->ev.size() < h->ev_used + 2) {
       hipEvent_t ev;
@@ -1021,7 +1040,6 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
     }
     HIP_TRY(hipEventRecord(h->ev[h->ev_used], st));
   }
-  const StepIO io{actions, obs, reward, valid, done, final_obs};
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   const dim3 grid(grid_for(h->n)), block(BLOCK);
   if (h->mode == TG_MODE_DIRECT) {
@@ -1051,6 +1069,41 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
     HIP_TRY(hipEventRecord(h->ev[h->ev_used + 1], st));
     h->ev_used += 2;
     if (h->ev_used >= 4096) return flush_timing(h);
+  }
+  return TG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, uint8_t* valid,
+            uint8_t* done, double* final_obs, uint32_t flags, void* stream) {
+  BIND(h);
+  if (!actions || !obs || !reward || !valid || !done)
+    return fail(TG_E_INVAL, "tg_step: actions/obs/reward/valid/done are required");
+  const StepIO io{const_cast<int32_t*>(actions), obs, reward, valid, done, final_obs, -1, 0, 0};
+  return launch_step(h, io, (flags & TG_STEP_AUTORESET) != 0, (hipStream_t)stream);
+}
+
+int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int policy,
+               uint32_t flags, int32_t* actions, double* obs, int32_t* reward, uint8_t* valid,
+               uint8_t* done, void* stream) {
+  BIND(h);
+  if (steps < 0 || !reward || !valid || !done ||
+      (policy != TG_POLICY_UNIFORM && policy != TG_POLICY_MASKED))
+    return fail(TG_E_INVAL, "tg_rollout: bad arguments");
+  const int64_t n = h->n;
+  if (!obs && !h->obs_scratch)  // the step kernels always write an obs row
+    if (hipMalloc((void**)&h->obs_scratch, sizeof(double) * 9 * (size_t)n) != hipSuccess)
+      return fail(TG_E_NOMEM, "tg_rollout: obs scratch");
+  const bool ar = (flags & TG_STEP_AUTORESET) != 0;
+  for (int32_t s = 0; s < steps; ++s) {
+    const StepIO io{actions ? actions + (size_t)s * n : nullptr,
+                    obs ? obs + (size_t)s * n * 9 : h->obs_scratch,
+                    reward + (size_t)s * n, valid + (size_t)s * n, done + (size_t)s * n,
+                    nullptr, policy, action_seed, t0 + s};
+    const int rc = launch_step(h, io, ar, (hipStream_t)stream);
+    if (rc) return rc;
   }
   return TG_OK;
 }

@@ -70,6 +70,7 @@ struct tg_batch {
   size_t ev_used = 0;
   double kernel_ms_done = 0.0;
   std::string domain;              // domain.txt text (the renderer's cell sprites)
+  double* obs_scratch = nullptr;   // tg_rollout without an obs output
   tg::RenderState* rs = nullptr;   // tg_render_init
 };
 

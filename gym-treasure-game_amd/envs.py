@@ -187,6 +187,29 @@ class TreasureGameVec:
         return (self._out(self._obs), self._out(self._rew), self._out(self._valid),
                 self._out(self._done), info)
 
+    def rollout(self, steps, t0=0, action_seed=0x5EED0001, policy="uniform", obs=True,
+                actions=True):
+        """``steps`` env-steps in one call with the on-device synthetic policy (tg_rollout):
+        step t0 + s takes ``policy_actions(t0 + s, action_seed, policy)``, evaluated inside the
+        step kernels.  Returns step-major device tensors: reward i32 [K, N], valid / done u8
+        [K, N], and (optionally) obs f64 [K, N, 9], actions i32 [K, N].  With auto-reset the
+        obs rows are the post-reset ones and finished episodes queue for ``episodes()``."""
+        pol = {"uniform": _lib.TG_POLICY_UNIFORM, "masked": _lib.TG_POLICY_MASKED}[policy]
+        k, n, dev = int(steps), self.num_envs, self.device
+        out = {"reward": torch.empty((k, n), dtype=torch.int32, device=dev),
+               "valid": torch.empty((k, n), dtype=torch.uint8, device=dev),
+               "done": torch.empty((k, n), dtype=torch.uint8, device=dev)}
+        if obs:
+            out["obs"] = torch.empty((k, n, 9), dtype=torch.float64, device=dev)
+        if actions:
+            out["actions"] = torch.empty((k, n), dtype=torch.int32, device=dev)
+        check(self._L.tg_rollout(self.handle, k, action_seed, int(t0), pol,
+                                 _lib.TG_STEP_AUTORESET if self.autoreset else 0,
+                                 _ptr(out.get("actions")), _ptr(out.get("obs")),
+                                 _ptr(out["reward"]), _ptr(out["valid"]), _ptr(out["done"]),
+                                 self._stream()), "tg_rollout")
+        return out
+
     def available_mask(self):
         """available_mask (TG/:83-89) as bits: int16 [N], bit k == option k can run."""
         check(self._L.tg_available_mask(self.handle, _ptr(self._mask), self._stream()),

@@ -350,3 +350,37 @@ def test_checkpoint_restore_continues_bit_exact(tg, oracle, tmp_path, mode):
         b.write_state(bad)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("policy", ["uniform", "masked"])
+def test_rollout_equals_step_loop_and_oracle(tg, oracle, mode, policy):
+    """tg_rollout (the on-device policy inside the step kernels, K steps per call, continued
+    across calls) == the per-step API loop == the oracle, bit for bit."""
+    n, k1, k, a0 = 4096, 20, 37, 0xF00D
+    pol = 1 if policy == "masked" else 0
+    a = tg.TreasureGameVec(n, seed=0, autoreset=True, mode=mode)
+    a.reset()
+    r1 = a.rollout(k1, t0=0, action_seed=a0, policy=policy)
+    r2 = a.rollout(k - k1, t0=k1, action_seed=a0, policy=policy)
+    ref = oracle.run(0, 0, n, k, a0, pol, True)
+    obs = torch.cat([r1["obs"], r2["obs"]]).cpu().numpy().transpose(1, 0, 2)
+    assert np.array_equal(np.ascontiguousarray(obs).view(np.uint64), ref["obs"][:, 1:].view(np.uint64))
+    for key in ("reward", "valid", "done"):
+        got = torch.cat([r1[key], r2[key]]).cpu().numpy().T
+        assert np.array_equal(got, ref[key][:, 1:]), key
+    b = tg.TreasureGameVec(n, seed=0, autoreset=True, mode=mode)
+    b.reset()
+    for t in range(k):
+        act = b.policy_actions(t, a0, policy)
+        want = (r1 if t < k1 else r2)["actions"][t if t < k1 else t - k1]
+        assert torch.equal(act, want), t
+        b.step(act)
+    sa, sb = a.read_state(mt=True), b.read_state(mt=True)
+    for key in sa:
+        assert np.array_equal(sa[key], sb[key]), key
+    assert a.stats()["steps"] == n * k and a.errors() == 0
+    r0 = a.rollout(0)
+    assert r0["reward"].shape == (0, n)
+    a.close()
+    b.close()
