@@ -407,6 +407,7 @@ struct StepIO {
   uint8_t* __restrict__ done;
   double* __restrict__ final_obs;  // may be null
   int policy;                      // -1: actions given; else TG_POLICY_* evaluated in the step
+                                   // (selects the kernels' POL instantiation)
   uint64_t a0;                     // the policy's action seed and step index
   int64_t t;
 };
@@ -515,7 +516,9 @@ __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int6
 }
 
 // ---- one-pass step: one lane per env, the option runs in place (TG_MODE_DIRECT) ----------
-template <bool AUTORESET, bool FINAL>
+// POL: -1 actions given; else the TG_POLICY_* evaluated here (tg_rollout).  A template
+// parameter, so the per-step kernels carry none of the policy's code or registers.
+template <bool AUTORESET, bool FINAL, int POL = -1>
 __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
                                                  const uint32_t* __restrict__ grid, StepIO io,
                                                  EpQueue q, int64_t g0,
@@ -536,8 +539,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     ep = S.ep[i];
     RngRing rng(S.mt + i * MT_WORDS, S.mtd + i * MT_DOUBLES, e.mti, wring);
     int act;
-    if (io.policy >= 0) {
-      act = policy_action(L, m, e, io.policy, io.a0, g0 + i, io.t);
+    if constexpr (POL >= 0) {
+      act = policy_action(L, m, e, POL, io.a0, g0 + i, io.t);
       if (io.actions) io.actions[i] = act;
     } else {
       act = io.actions[i];
@@ -592,7 +595,7 @@ __constant__ int kOrder[O_COUNT] = {O_GO_LEFT,   O_GO_RIGHT,   O_JUMP_LEFT,   O_
                                     O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
                                     O_INTERACT};
 
-template <bool AUTORESET, bool FINAL>
+template <bool AUTORESET, bool FINAL, int POL = -1>
 __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      const uint32_t* __restrict__ grid,
                                                      StepIO io, EpQueue q, Work w, int64_t g0,
@@ -610,7 +613,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   int2 ep = make_int2(0, 0);
   if (live) {
     s4 = S.st4[i];
-    if (io.policy < 0) act = io.actions[i];
+    if constexpr (POL < 0) act = io.actions[i];
     a2 = S.ang[i];
     ep = S.ep[i];
   }
@@ -624,8 +627,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   e.mti = 0u;
   if (live) {
     unpack_st4(s4, e);
-    if (io.policy >= 0) {  // the rollout's on-device policy (tg_rollout)
-      act = policy_action(L, m, e, io.policy, io.a0, g0 + i, io.t);
+    if constexpr (POL >= 0) {  // the rollout's on-device policy (tg_rollout)
+      act = policy_action(L, m, e, POL, io.a0, g0 + i, io.t);
       if (io.actions) io.actions[i] = act;
     }
     k = option_index(act);
@@ -1043,8 +1046,16 @@ int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   const dim3 grid(grid_for(h->n)), block(BLOCK);
   if (h->mode == TG_MODE_DIRECT) {
-    auto kern = ar ? (fo ? k_step<true, true> : k_step<true, false>)
-                   : (fo ? k_step<false, true> : k_step<false, false>);
+    decltype(&k_step<true, true>) kern;
+    if (io.policy == TG_POLICY_UNIFORM)
+      kern = ar ? (fo ? k_step<true, true, 0> : k_step<true, false, 0>)
+                : (fo ? k_step<false, true, 0> : k_step<false, false, 0>);
+    else if (io.policy == TG_POLICY_MASKED)
+      kern = ar ? (fo ? k_step<true, true, 1> : k_step<true, false, 1>)
+                : (fo ? k_step<false, true, 1> : k_step<false, false, 1>);
+    else
+      kern = ar ? (fo ? k_step<true, true> : k_step<true, false>)
+                : (fo ? k_step<false, true> : k_step<false, false>);
     hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, h->g0,
                        h->stats, h->err);
   } else {
@@ -1054,8 +1065,16 @@ int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
     int32_t* const nxt = h->wctr + (h->parity ? 0 : NSEG * CTR_STRIDE);
     h->parity ^= 1;
     const Work w{h->wl, cur, nxt, h->refill, h->nrefill, h->shard_cap};
-    auto kc = ar ? (fo ? k_classify<true, true> : k_classify<true, false>)
-                 : (fo ? k_classify<false, true> : k_classify<false, false>);
+    decltype(&k_classify<true, true>) kc;
+    if (io.policy == TG_POLICY_UNIFORM)
+      kc = ar ? (fo ? k_classify<true, true, 0> : k_classify<true, false, 0>)
+              : (fo ? k_classify<false, true, 0> : k_classify<false, false, 0>);
+    else if (io.policy == TG_POLICY_MASKED)
+      kc = ar ? (fo ? k_classify<true, true, 1> : k_classify<true, false, 1>)
+              : (fo ? k_classify<false, true, 1> : k_classify<false, false, 1>);
+    else
+      kc = ar ? (fo ? k_classify<true, true> : k_classify<true, false>)
+              : (fo ? k_classify<false, true> : k_classify<false, false>);
     auto kr = ar ? (fo ? k_run<true, true> : k_run<true, false>)
                  : (fo ? k_run<false, true> : k_run<false, false>);
     hipLaunchKernelGGL(kc, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, w, h->g0,
@@ -1089,6 +1108,7 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
                uint32_t flags, int32_t* actions, double* obs, int32_t* reward, uint8_t* valid,
                uint8_t* done, void* stream) {
   BIND(h);
+  if (steps == 0) return TG_OK;
   if (steps < 0 || !reward || !valid || !done ||
       (policy != TG_POLICY_UNIFORM && policy != TG_POLICY_MASKED))
     return fail(TG_E_INVAL, "tg_rollout: bad arguments");
