@@ -468,32 +468,23 @@ __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, 
   }
 }
 
-// Launch counters without global atomics: the block reduces its waves' sums in LDS and its
-// thread 0 adds them into the block's own slot of `part` ([grid][ST_COUNT]); every step
-// kernel uses the same grid, so slots never race.  The host sums the slots on demand.
-// (One counter word per launch took ~32k same-line atomics: ~370 us at ~88 atomics/us.)
-// Must be reached by every thread of the block.
-__device__ __forceinline__ void block_stats(unsigned long long* __restrict__ part, int steps,
-                                            int valid, int ticks, int draws, int episodes,
-                                            int regens = 0) {
-  __shared__ int acc[5];
-  if (threadIdx.x < 5) acc[threadIdx.x] = 0;
-  __syncthreads();
-  const int s0 = wave_sum(steps), s1 = wave_sum(valid), s2 = wave_sum(ticks),
-            s3 = wave_sum(draws), s4 = wave_sum(episodes);
+// Launch counters: every step kernel has a per-block slot of `part` ([grid][ST_COUNT]) and the
+// host sums the slots on demand (one counter word per launch took ~32k same-line atomics:
+// ~370 us at ~88 atomics/us).  Each wave's lane 0 adds its sums into its block's slot with
+// returnless atomics (no contention across blocks; no barrier, so every wave exits as soon as
+// it is done).  Must be reached by every lane of the wave.
+__device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ part, int steps,
+                                           int valid, int ticks, int draws, int episodes,
+                                           int regens = 0) {
+  const int v[5] = {wave_sum(steps), wave_sum(valid), wave_sum(ticks), wave_sum(draws),
+                    wave_sum(episodes)};
   if ((threadIdx.x & 63) == 0) {
-    if (s0) atomicAdd(&acc[0], s0);
-    if (s1) atomicAdd(&acc[1], s1);
-    if (s2) atomicAdd(&acc[2], s2);
-    if (s3) atomicAdd(&acc[3], s3);
-    if (s4) atomicAdd(&acc[4], s4);
-    // wave-uniform counts (one per wave, lane 0): regenerations
-    if (regens) atomicAdd((unsigned long long*)&part[(size_t)blockIdx.x * ST_COUNT + ST_REGENS],
-                          (unsigned long long)regens);
+    unsigned long long* const slot = part + (size_t)blockIdx.x * ST_COUNT;
+#pragma unroll
+    for (int c = 0; c < 5; ++c)
+      if (v[c]) atomicAdd(&slot[c], (unsigned long long)v[c]);
+    if (regens) atomicAdd(&slot[ST_REGENS], (unsigned long long)regens);
   }
-  __syncthreads();
-  if (threadIdx.x < 5 && acc[threadIdx.x])
-    part[(size_t)blockIdx.x * ST_COUNT + threadIdx.x] += (unsigned long long)acc[threadIdx.x];
 }
 
 // finish one env-step: obs/reward/valid/done rows, episode counters, optional auto-reset
@@ -563,7 +554,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     S.ang[i] = make_double2(e.ang0, e.ang1);
     S.ep[i] = ep;
   }
-  block_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
+  wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
               __popcll(need));
 }
 
@@ -696,7 +687,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   if (threadIdx.x < O_COUNT) bbase[threadIdx.x] = my_base;
   __syncthreads();
   if (runs) w.lists[(int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot] = (int32_t)i;
-  block_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
+  wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
               AUTORESET ? (live && !runs && dn) : 0);
 }
 
@@ -798,7 +789,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
       }
     }
   }
-  block_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0, regens);
+  wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0, regens);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
   {
