@@ -10,8 +10,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _frames_vs_oracle(oracle, got, envs, steps, a0, policy, autoreset, sprites):
-    want = oracle.run_render(0, envs, steps, a0, policy, autoreset, sprites)
+def _frames_vs_oracle(oracle, got, envs, steps, a0, policy, autoreset, sprites, level_dir=None):
+    want = oracle.run_render(0, envs, steps, a0, policy, autoreset, sprites, level_dir=level_dir)
     for i, g in enumerate(envs):
         if not np.array_equal(got[i], want[i]):
             bad = np.argwhere((got[i] != want[i]).any(-1))
@@ -119,3 +119,21 @@ def test_vec_observation_wrapper(tg, oracle):
         assert info["world_state"].shape == (n, 9)
     _frames_vs_oracle(oracle, frames.cpu().numpy(), np.arange(n), 6, a0, 1, True, sprites)
     w.close()
+
+
+def test_render_other_level_vs_oracle(tg, oracle):
+    """A 44 x 5-cell level (frames 240 x 2,112, 396 chunks per row) through the C ABI."""
+    import os
+    level = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", "corridor")
+    sprites = tg.synthetic_sprites(seed=21, size=40)
+    n, a0 = 40, 0x3C
+    vec = tg.TreasureGameVec(n, seed=0, autoreset=True, level_dir=level)
+    vec.render_init(sprites)
+    assert vec.frame_shape == (240, 2112, 3)
+    vec.reset()
+    for t in range(8):
+        vec.step(vec.policy_actions(t, a0, "masked"))
+    _frames_vs_oracle(oracle, vec.render().cpu().numpy(), np.arange(n), 8, a0, 1, True, sprites,
+                      level_dir=level)
+    assert vec.errors() == 0
+    vec.close()

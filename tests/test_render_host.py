@@ -28,9 +28,21 @@ def level_texts(level_dir):
                  for f in ("domain.txt", "domain-objects.txt", "domain-interactions.txt"))
 
 
+CORRIDOR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels",
+                        "corridor")
+
+
+def frame_shape(level_dir):
+    if level_dir is None:
+        return 624, 672
+    rows = [r.strip() for r in open(os.path.join(level_dir, "domain.txt")).read().split("\n")]
+    rows = [r for r in rows if r]
+    return len(rows) * 48, len(rows[0]) * 48
+
+
 def hc_frames(lib, envs, steps, a0, policy, autoreset, sprites, seed_base=0, level_dir=None):
     envs = np.ascontiguousarray(envs, np.int64)
-    out = np.zeros((len(envs), 624, 672, 3), np.uint8)
+    out = np.zeros((len(envs),) + frame_shape(level_dir) + (3,), np.uint8)
     rc = lib.hc_render_run(*level_texts(level_dir), seed_base, _p(envs), len(envs), steps, a0, policy,
                            int(autoreset), _p(sprites), sprites.shape[2], sprites.shape[1], _p(out))
     assert rc == 0
@@ -87,6 +99,16 @@ def test_composition_vs_oracle_overlapping_items(hostcheck, oracle, steps):
     envs = np.arange(16)
     got = hc_frames(hostcheck, envs, steps, 5, 1, True, sprites, level_dir=OVERLAP)
     want = oracle.run_render(0, envs, steps, 5, 1, True, sprites, level_dir=OVERLAP)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_composition_vs_oracle_other_level_size(hostcheck, oracle):
+    """A 44 x 5-cell level (frames 240 x 2,112): other row lengths and band counts."""
+    sprites = R.synthetic_sprites(seed=4, size=24)
+    envs = np.arange(12)
+    got = hc_frames(hostcheck, envs, 6, 9, 1, True, sprites, level_dir=CORRIDOR)
+    want = oracle.run_render(0, envs, 6, 9, 1, True, sprites, level_dir=CORRIDOR)
+    assert got.shape == (12, 240, 2112, 3)
     np.testing.assert_array_equal(got, want)
 
 
