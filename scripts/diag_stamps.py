@@ -21,10 +21,9 @@ SO = os.path.join(ROOT, "gym-treasure-game_amd",
 
 
 def main():
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                           "-ffp-contract=off", "-fPIC", "-shared", "-DTG_DIAG_STAMPS",
-                           "-Wno-bitwise-instead-of-logical"] + FLAGS + ["-o", SO,
-                           os.path.join(ROOT, "gym-treasure-game_amd", "csrc", "tg_amd.hip")])
+    from gym_treasure_game_amd import build as B
+    if not (os.environ.get("NOBUILD") and os.path.exists(SO)):
+        subprocess.check_call([B.HIPCC] + B.FLAGS + ["-DTG_DIAG_STAMPS"] + FLAGS + ["-o", SO] + B.SRCS)
     _lib._lib = None
     _lib.LIB_PATH = SO
     L = _lib.load()
