@@ -80,6 +80,9 @@ __device__ __forceinline__ void store16(uint4* p, const uint4 x) {
 #endif
 }
 
+#ifndef TG_RENDER_DIAG_COPY
+#define TG_RENDER_DIAG_COPY 0
+#endif
 #ifndef TG_RENDER_DIAG_NOCOMPOSE
 #define TG_RENDER_DIAG_NOCOMPOSE 0  // DIAGNOSTIC ONLY (wrong frames): store the static chunk
 #endif                               // where items are, to price the composition
@@ -151,7 +154,11 @@ __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __
     uint4* dst = base + c;
     for (int k = 0; k < ne; ++k, dst += frame_chunks) {
       const uint32_t rm = rows[k][r];
-#if TG_RENDER_DIAG_NOCOMPOSE
+#if TG_RENDER_DIAG_COPY  // DIAGNOSTIC ONLY (wrong frames): the static chunk everywhere
+      (void)rm;
+      (void)sel;
+      store16(dst, v);
+#elif TG_RENDER_DIAG_NOCOMPOSE
       const uint32_t hit = rm ? chunk_items(lay[k], rm, q) : 0u;
       (void)sel;
       store16(dst, hit ? make_uint4(v.x ^ hit, v.y, v.z, v.w) : v);
