@@ -8,8 +8,8 @@
 One "step" = one TreasureGame.step() (TG/:91-96) of EVERY env of the batch: the on-device
 synthetic policy writes the actions (uniform over the 9 options, counter hash keyed by the
 global env index), tg_step runs each env's option to completion with auto-reset (k_classify
-then k_run), completed episodes are drained on the device and, for N > 1, all-gathered over
-RCCL.  Per-GPU work is fixed (1,048,576 envs per GPU = config C3, C4 at 8 GPUs), so scaling
+then k_run).  Every G steps (--gather-every, default 10) the completed episodes are drained
+from the device queue and, for N > 1, all-gathered over RCCL.  Per-GPU work is fixed (1,048,576 envs per GPU = config C3, C4 at 8 GPUs), so scaling
 is weak.  Inputs are resident in HBM when the timed region starts.
 
 Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (tg_step's kernels:
@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 METRIC = "env-steps/sec (whole node) at 1M batched envs, 1/2/4/8 MI355X; bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ACTION_SEED = 0x5EED0001
-EP_CAP = 4096          # episode records gathered per rank per step (padded)
+EP_CAP = 4096          # episode records gathered per rank per step of a drain interval (padded)
 # algorithmic bytes of one tg_step, per launch:
 #   every env: action 4 + state word 16 read (classify)
 #   reward-None env: angles 16 + episode 8 read; episode 8 + obs 72 + reward/valid/done 6 written
@@ -71,7 +71,11 @@ def parse():
     ap.add_argument("--rollout", type=int, default=0,
                     help="K > 0: tg_rollout, K steps per call with the policy evaluated inside "
                          "the step kernels (episodes drained / gathered every K steps); 0: the "
-                         "per-step API (tg_policy_actions + tg_step + drain every step)")
+                         "per-step API (tg_policy_actions + tg_step per step)")
+    ap.add_argument("--gather-every", type=int, default=10,
+                    help="per-step API: drain (and, N > 1, all-gather) the completed episodes "
+                         "every G steps (SURVEY §8e: batched gather; 1 = every step). "
+                         "--rollout K drains every K steps")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU-baseline sample (0 disables it)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_step.json"),
@@ -159,10 +163,16 @@ def main():
     vec.set_mode(args.mode, args.run_blocks)
     vec.autoreset = autoreset  # final_obs is not requested: obs/reward/valid/done only
     vec.reset()
-    ep_rows = torch.empty((EP_CAP, 2), dtype=torch.int64, device=dev)
+    K = args.rollout
+    G = K if K else args.gather_every
+    if G < 1:
+        raise SystemExit("--gather-every must be >= 1")
+    ep_cap = EP_CAP * G  # records per rank per drain (padded; the rest stays queued)
+    ep_rows = torch.empty((ep_cap, 2), dtype=torch.int64, device=dev)
     ep_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    gathered = torch.zeros(1, dtype=torch.int64, device=dev)  # records seen by this rank
     if world > 1:
-        all_rows = torch.empty((world * EP_CAP, 2), dtype=torch.int64, device=dev)
+        all_rows = torch.empty((world * ep_cap, 2), dtype=torch.int64, device=dev)
         all_cnt = torch.empty(world, dtype=torch.int32, device=dev)
     L, h = vec._L, vec.handle
     obs, rew, val, don = vec._obs, vec._rew, vec._valid, vec._done
@@ -180,7 +190,6 @@ def main():
         frames = torch.empty((count,) + vec.frame_shape, dtype=torch.uint8, device=dev)
     timing = [False]
 
-    K = args.rollout
     if K:
         if c5 or args.steps % K or args.warmup % K:
             raise SystemExit("--rollout K: c3 only, with --steps and --warmup multiples of K")
@@ -196,7 +205,8 @@ def main():
         else:
             tg._lib.check(L.tg_policy_actions(h, ACTION_SEED, t, pol, p(act), stream), "actions")
             tg._lib.check(L.tg_step(*args_step), "tg_step")
-        tg._lib.check(L.tg_episodes(h, p(ep_rows), p(ep_cnt), EP_CAP, stream), "episodes")
+        if (t + 1) % G == 0 or K:
+            drain()
         if c5:
             if timing[0]:  # k_render alone, on the stream it is launched on
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -205,13 +215,21 @@ def main():
             if timing[0]:
                 ev[1].record()
                 rev.append(ev)
+
+    def drain():
+        tg._lib.check(L.tg_episodes(h, p(ep_rows), p(ep_cnt), ep_cap, stream), "episodes")
         if world > 1:  # the one collective: completed episodes over RCCL/xGMI
             dist.all_gather_into_tensor(all_cnt, ep_cnt)
             dist.all_gather_into_tensor(all_rows, ep_rows)
+            gathered.add_(all_cnt.sum())
+        else:
+            gathered.add_(ep_cnt[0])
 
     for t in range(args.warmup):
         one_step(t)
+    drain()  # empty the queue, so the timed region's records are its own
     torch.cuda.synchronize(dev)
+    gathered.zero_()
     vec.stats_reset()
     vec.set_timing(True)
     timing[0] = True
@@ -297,6 +315,7 @@ def main():
             "valid_step_frac": node["valid_steps"] / max(node["steps"], 1),
             "draws_per_step": node["draws"] / max(node["steps"], 1),
             "episodes": node["episodes"], "error_flags": errs,
+            "gather_every": G, "episodes_gathered": int(gathered.item()),
             "regens_per_step": st["regens"] / launches,
             "roofline": roof,
         }

@@ -487,10 +487,12 @@ __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ part
   }
 }
 
-// finish one env-step: obs/reward/valid/done rows, episode counters, optional auto-reset
+// finish one env-step: obs/reward/valid/done rows, episode counters, optional auto-reset.
+// keep != nullptr: the obs row is returned there instead of stored (the caller stores it).
 template <bool AUTORESET, bool FINAL, class R>
 __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int64_t i,
-                                            const StepResult& r, int2& ep, const StepIO& io) {
+                                            const StepResult& r, int2& ep, const StepIO& io,
+                                            double* keep = nullptr) {
   double o[9];
   observe(L, e, o);  // get_state (TG/:94)
   io.reward[i] = r.reward;
@@ -503,7 +505,36 @@ __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int6
     reset_env(L, e, rng);
     observe(L, e, o);
   }
-  store_obs(io.obs, i, o);
+  if (keep) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) keep[k] = o[k];
+  } else {
+    store_obs(io.obs, i, o);
+  }
+}
+
+#ifndef TG_CLASSIFY_STAGE_OBS
+#define TG_CLASSIFY_STAGE_OBS 1
+#endif
+// The obs rows of a wave's 64 consecutive envs (4,608 B) through LDS: lane l stores the
+// 8-B words l, l+64, ... of the span, so each store instruction writes 512 contiguous bytes
+// (a lane storing its own 72-B row touches ~36 cache lines per instruction).  Rows of envs
+// not in `mask` are left alone.  Every lane of the wave must reach it.
+__device__ __forceinline__ void store_obs_wave(double* __restrict__ out, int64_t wave_first,
+                                               unsigned long long mask, const double o[9],
+                                               double* __restrict__ stage) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) stage[lane * 9 + k] = o[k];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double* const dst = out + wave_first * 9;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int w = j * 64 + lane;
+    if ((mask >> (w / 9)) & 1ull) __builtin_nontemporal_store(stage[w], dst + w);
+  }
 }
 
 // ---- one-pass step: one lane per env, the option runs in place (TG_MODE_DIRECT) ----------
@@ -593,6 +624,10 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      unsigned long long* __restrict__ stats,
                                                      uint32_t* __restrict__ err_or) {
   __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
+#if TG_CLASSIFY_STAGE_OBS
+  __shared__ double ostage[BLOCK * 9];
+  double orow[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
   const int lane = threadIdx.x & 63;
@@ -670,12 +705,20 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     dn = is_done(e);
     Rng rng(S.mt + i * MT_WORDS, e.mti, S.mtd + i * MT_DOUBLES);
     StepResult r{0, 0, (int)dn, 0};
+#if TG_CLASSIFY_STAGE_OBS
+    finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io, orow);
+#else
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
+#endif
     e.mti = rng.finish_queued();  // the stale half, if any, is on the refill list
     draws = rng.draws;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, q, stats);
+#if TG_CLASSIFY_STAGE_OBS
+  store_obs_wave(io.obs, i - lane, __ballot(live && !runs), orow,
+                 ostage + (threadIdx.x & ~63) * 9);
+#endif
   if (live && !runs) {
     const uint4 s4n = pack(e);
     if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w) {  // reset / flag
