@@ -625,8 +625,18 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      uint32_t* __restrict__ err_or) {
   __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
 #if TG_CLASSIFY_STAGE_OBS
-  __shared__ double ostage[BLOCK * 9];
+  // the obs staging reuses the level's LDS: nothing reads the grid after the first barrier
+  // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
+  // keeps 8 waves per SIMD
+  __shared__ union {
+    LdsLevel lv;
+    double ostage[BLOCK * 9];
+  } lds;
+  LdsLevel& lv = lds.lv;
+  double* const ostage = lds.ostage;
   double orow[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#else
+  __shared__ LdsLevel lv;
 #endif
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
@@ -645,8 +655,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   }
   if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
   if (blockIdx.x == 0 && threadIdx.x < NSEG) w.ctr_next[threadIdx.x * CTR_STRIDE] = 0;
-  LEVEL_IN_LDS();  // includes the barrier
-  (void)trig;
+  stage_level(lv, grid, L);  // includes the barrier
+  const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
   int k = -1;
   bool runs = false;
   Env e;
