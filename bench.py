@@ -249,12 +249,13 @@ def main():
         dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         dt = float(dt_t.item())
-        tot = torch.tensor([st["steps"], st["ticks"], st["draws"], st["valid_steps"],
-                            st["episodes"]], dtype=torch.int64, device=dev)
+        keys = ["steps", "ticks", "draws", "valid_steps", "episodes", "wave_ticks"]
+        tot = torch.tensor([st[k] for k in keys], dtype=torch.int64, device=dev)
         dist.all_reduce(tot)
-        node = dict(zip(["steps", "ticks", "draws", "valid_steps", "episodes"], tot.tolist()))
+        node = dict(zip(keys, tot.tolist()))
     else:
-        node = {k: st[k] for k in ("steps", "ticks", "draws", "valid_steps", "episodes")}
+        node = {k: st[k] for k in ("steps", "ticks", "draws", "valid_steps", "episodes",
+                                   "wave_ticks")}
 
     if rank == 0:
         env_steps = total * args.steps
@@ -312,6 +313,8 @@ def main():
                                else "tg_policy_actions + tg_step per step"),
                        "parallelism": "env-shard x%d" % world},
             "ticks_per_s": node["ticks"] / dt,
+            # ticks executed / lane-ticks issued by the tick loops' wavefronts
+            "lane_efficiency": node["ticks"] / max(64 * node["wave_ticks"], 1),
             "valid_step_frac": node["valid_steps"] / max(node["steps"], 1),
             "draws_per_step": node["draws"] / max(node["steps"], 1),
             "episodes": node["episodes"], "error_flags": errs,

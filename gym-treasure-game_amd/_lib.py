@@ -46,7 +46,8 @@ class Stats(ctypes.Structure):
                 ("ticks", ctypes.c_int64), ("draws", ctypes.c_int64),
                 ("episodes", ctypes.c_int64), ("episodes_dropped", ctypes.c_int64),
                 ("launches", ctypes.c_int64),
-                ("kernel_ms", ctypes.c_double), ("regens", ctypes.c_int64)]
+                ("kernel_ms", ctypes.c_double), ("regens", ctypes.c_int64),
+                ("wave_ticks", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -332,7 +332,15 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
-enum { ST_STEPS, ST_VALID, ST_TICKS, ST_DRAWS, ST_EPISODES, ST_EP_OVERFLOW, ST_REGENS, ST_COUNT };
+enum { ST_STEPS, ST_VALID, ST_TICKS, ST_DRAWS, ST_EPISODES, ST_EP_OVERFLOW, ST_REGENS, ST_WTICKS,
+       ST_COUNT };
+
+// 64-lane max (wave64)
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
 
 // ------------------------------------------------------------------------------------------
 // kernels
@@ -473,17 +481,20 @@ __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, 
 // ~370 us at ~88 atomics/us).  Each wave's lane 0 adds its sums into its block's slot with
 // returnless atomics (no contention across blocks; no barrier, so every wave exits as soon as
 // it is done).  Must be reached by every lane of the wave.
+// wave_ticks: the wave's longest lane's ticks (the tick loop's trip count, lane efficiency).
 __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ part, int steps,
                                            int valid, int ticks, int draws, int episodes,
-                                           int regens = 0) {
+                                           int regens = 0, bool wave_ticks = false) {
   const int v[5] = {wave_sum(steps), wave_sum(valid), wave_sum(ticks), wave_sum(draws),
                     wave_sum(episodes)};
+  const int wt = wave_ticks ? wave_max(ticks) : 0;
   if ((threadIdx.x & 63) == 0) {
     unsigned long long* const slot = part + (size_t)blockIdx.x * ST_COUNT;
 #pragma unroll
     for (int c = 0; c < 5; ++c)
       if (v[c]) atomicAdd(&slot[c], (unsigned long long)v[c]);
     if (regens) atomicAdd(&slot[ST_REGENS], (unsigned long long)regens);
+    if (wt) atomicAdd(&slot[ST_WTICKS], (unsigned long long)wt);
   }
 }
 
@@ -586,7 +597,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     S.ep[i] = ep;
   }
   wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
-              __popcll(need));
+              __popcll(need), true);
 }
 
 // ---- two-pass compacted step (TG_MODE_COMPACT) -------------------------------------------
@@ -842,7 +853,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
       }
     }
   }
-  wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0, regens);
+  wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0, regens, true);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
   {
@@ -1260,6 +1271,7 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   out->launches = out->steps / (h->n ? h->n : 1);
   out->kernel_ms = h->kernel_ms_done;
   out->regens = (int64_t)s[ST_REGENS];
+  out->wave_ticks = (int64_t)s[ST_WTICKS];
   return TG_OK;
 }
 

@@ -118,6 +118,8 @@ def test_golden_hashes(tg, name, policy, mode):
     assert st["ticks"] == int(d["ticks"].sum())
     assert st["valid_steps"] == int(d["valid_steps"].sum())
     assert st["steps"] == len(d["hash"]) * int(d["steps"])
+    # every wavefront's trip count is its longest lane's ticks: 64 x it bounds the lanes' ticks
+    assert st["ticks"] <= 64 * st["wave_ticks"] <= 64 * st["ticks"]
 
 
 @pytest.mark.parametrize("mode", MODES)
