@@ -176,7 +176,8 @@ struct RngRing {
   lds_u8* cell;    // this lane's 16-B cell in slot 0 of the wave's ring
   uint32_t m0;     // LDS address of slot 0 of the wave's ring (wave-uniform)
   uint32_t pos;    // [0, MT_WORDS), even: the next draw is double pos / 2
-  uint32_t rot;    // slot of chunk c = (c - rot) % R, rot = the first chunk's c % R (prime)
+  uint32_t rot;    // slot of chunk c = (c - rot) % R (set by prime, see slot_of)
+  uint32_t ph;     // the draws that fetch: o == ph, the first draw's o (0 or 2; prime)
   uint32_t draws;
   double nx;       // the next draw, read from the ring one draw ahead
   bool primed, loaded, crossed, entered;  // crossed / entered: as tg::Rng
@@ -184,7 +185,7 @@ struct RngRing {
   __device__ __forceinline__ RngRing(uint32_t* m, double* d, uint32_t state, lds_u8* wave_ring)
       : mt(m), md(d), cell(wave_ring + (threadIdx.x & 63) * 16),
         m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_ring)),
-        pos(state & MT_POS_MASK), rot(0u), draws(0u), nx(0.0), primed(false), loaded(false),
+        pos(state & MT_POS_MASK), rot(0u), ph(0u), draws(0u), nx(0.0), primed(false), loaded(false),
         crossed((state & MT_STALE) != 0u), entered(false) {}
 
   __device__ __forceinline__ void fetch(uint32_t c) {
@@ -199,16 +200,15 @@ struct RngRing {
     // chunk c = doubles 2c, 2c+1: the same 16 bytes as words 4c..4c+3 of the word array
     ring_fetch(m0, slot_of(c), reinterpret_cast<const uint32_t*>(md) + c * 4u);
   }
-  // Slots count from the lane's first chunk, not from chunk 0: lanes that fetch in the same
-  // iteration of a tick loop have drawn as often since their first chunk, so they share one
-  // slot and ring_fetch takes one branch (M0 is per slot) instead of up to R.  312 % R == 0
-  // keeps the mapping across the wrap (chunk c and c + 312 are the same slot).
+  // Slots and fetch draws count from the lane's first draw, not from chunk 0: a lane whose
+  // first draw is at o = 2 fetches at its o = 2 draws (chunk c + R from (c, 2), one draw
+  // before (c + 1, 0) would fetch it: the same ring state), and its slots count from chunk
+  // c + 1.  Lanes that draw in lockstep in a tick loop then fetch on the same iterations
+  // (every other draw, not every draw for half of them) and into the same slot, so ring_fetch
+  // takes one branch (M0 is per slot) instead of up to R.  312 % R == 0 keeps the mapping
+  // across the wrap (chunk c and c + 312 are the same slot).
   __device__ __forceinline__ uint32_t slot_of(uint32_t c) const {
-#ifdef TG_RING_ABS  // A/B: slots by absolute chunk index
-    return c % RING_SLOTS;
-#else
     return (c + RING_SLOTS - rot) % RING_SLOTS;
-#endif
   }
   // the double at pos from the ring (its chunk has landed: see the vmcnt argument above)
   __device__ __forceinline__ double ring_read() const {
@@ -219,10 +219,16 @@ struct RngRing {
     return *(const lds_f64*)(cell + slot_of(pos >> 2) * RING_SLOT_BYTES + (pos & 2u) * 4u);
   }
   __device__ __forceinline__ void prime() {
-    // chunks c .. c+R-2, and c+R-1 too when the first draw is at o = 2 (no o = 0 draw in
-    // chunk c will fetch it); chunk c-1's slot is free
+    // chunks c .. c+R-2, and c+R-1 too when the first draw is at o = 2 (its first fetch, at
+    // that draw, is chunk c+R); chunk c-1's slot is free
     const uint32_t c = pos >> 2;
-    rot = c % RING_SLOTS;
+#ifdef TG_RING_ABS
+    rot = 0u;
+    ph = 0u;
+#else
+    ph = pos & 2u;
+    rot = (c + (ph >> 1)) % RING_SLOTS;
+#endif
 #pragma unroll
     for (int j = 0; j < RING_SLOTS - 1; ++j) fetch(c + j);
     if (pos & 2u) fetch(c + RING_SLOTS - 1);
@@ -254,11 +260,13 @@ struct RngRing {
     // read the next draw BEFORE this draw's fetch: vmcnt counts the wave's VMEM instructions
     // in issue order, so a wait placed after a fetch would wait for that very fetch
     nx = ring_read();
-    if (!o) {  // first draw in chunk c: chunk c-1's slot (read draws ago) takes chunk c+R-1
+    if (o == ph) {
+      // o = 0: chunk c-1's slot (read draws ago) takes chunk c+R-1; o = 2 (ph = 2): chunk c's
+      // slot (its last value read a draw ago) takes chunk c+R
       asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");  // all but the read just issued
       const uint32_t p = pos;
       pos = c * 4u;  // fetch() tests the half of the chunk being read
-      fetch(c + RING_SLOTS - 1);
+      fetch(c + RING_SLOTS - 1 + (ph >> 1));
       pos = p;
     }
     return v;
