@@ -31,10 +31,7 @@ constexpr int INCR = S / 10;   // x_incr / y_incr (IM/:46-47)
 constexpr int HALFW = S / 4;   // player_width // 2 (IM/:49)
 constexpr int MT_N = 624, MT_M = 397;
 constexpr int TICK_CAP = 1 << 14;  // the reference has no cap (OP/:28-31); observed max 105
-constexpr int PAD = 2;
-#ifndef TG_FULL_BATCH
-#define TG_FULL_BATCH 64  // lanes that must be waiting before a go wave runs the full tick
-#endif             // WALL cells around the grid in LDS (probes reach <= 60 px out)
+constexpr int PAD = 2;         // WALL cells around the grid in LDS (probes reach <= 60 px out)
 
 // Cell bits in the LDS grid.  A door object's cell carries only its one-hot door bit: its type
 // is 'D' or ' ' by the door's state (update_map overwrites whatever the file had there).
@@ -816,30 +813,35 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
   if constexpr (K == O_GO_LEFT || K == O_GO_RIGHT) {
     constexpr int DIR = K == O_GO_LEFT ? -1 : 1;
     int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
+    // Two phases per round.  Plain phase: every lane inside its span takes plain ticks until
+    // it leaves it (a wavefront loops while any lane is in a span, so its body is just the
+    // plain tick).  Full phase: then no lane of the wave is in a span, and each takes one full
+    // tick, which may open a new span.  Each lane's own tick sequence is the reference's; only
+    // the interleaving across lanes differs, and the full tick's code runs once per round.
+    bool capped = false;
     do {
-      const bool plain = DIR > 0 ? e.px <= lim : e.px >= lim;
-      // A lane whose next tick must be a full one waits until enough lanes of the wave do
-      // (or none can take a plain tick): each lane's own tick sequence is unchanged, only the
-      // interleaving across lanes, so the wave runs the full tick's code rarely.
 #ifdef __HIP_DEVICE_COMPILE__
-      const unsigned long long want = __ballot(!plain), can = __ballot(plain);
-      const bool run_full = !plain && (__popcll(want) >= TG_FULL_BATCH || can == 0ull);
+      while (__ballot(DIR > 0 ? e.px <= lim : e.px >= lim) != 0ull) {
 #else
-      const bool run_full = !plain;
+      while (DIR > 0 ? e.px <= lim : e.px >= lim) {
 #endif
-      if (plain) {  // a plain tick (see go_plain_limit)
-        const double rr = rng.random();
-        e.px += (int)rint((DIR < 0 ? -4.0 : 2.0) + 2.0 * rr);
-        e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
-        r.reward += -1;
-        if (DIR > 0 ? e.px > lim : e.px < lim) pickups(L, e);  // left the span: as the full tick
-      } else if (run_full) {
-        const int prim = policy<K>(L, m, e, o);
-        r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
-        if (!o.done) lim = go_plain_limit<DIR>(m, e, o.tx);
-      } else {
-        continue;  // waits for the batch (no tick)
+        if (DIR > 0 ? e.px <= lim : e.px >= lim) {  // a plain tick (see go_plain_limit)
+          const double rr = rng.random();
+          e.px += (int)rint((DIR < 0 ? -4.0 : 2.0) + 2.0 * rr);
+          e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
+          r.reward += -1;
+          if (DIR > 0 ? e.px > lim : e.px < lim) pickups(L, e);  // left the span: as the full tick
+          if (++r.ticks >= TICK_CAP) {
+            e.f |= E_TICKCAP;
+            capped = true;
+            lim = DIR > 0 ? -0x40000000 : 0x40000000;  // out of the plain phase
+          }
+        }
       }
+      if (capped) break;
+      const int prim = policy<K>(L, m, e, o);
+      r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
+      if (!o.done) lim = go_plain_limit<DIR>(m, e, o.tx);
       if (++r.ticks >= TICK_CAP) {
         e.f |= E_TICKCAP;
         break;
