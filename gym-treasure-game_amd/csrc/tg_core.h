@@ -814,28 +814,24 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
     constexpr int DIR = K == O_GO_LEFT ? -1 : 1;
     int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
     // Two phases per round.  Plain phase: every lane inside its span takes plain ticks until
-    // it leaves it (a wavefront loops while any lane is in a span, so its body is just the
-    // plain tick).  Full phase: then no lane of the wave is in a span, and each takes one full
+    // it leaves it (the loop body is just the plain tick).  Full phase: then no lane of the wave is in a span, and each takes one full
     // tick, which may open a new span.  Each lane's own tick sequence is the reference's; only
     // the interleaving across lanes differs, and the full tick's code runs once per round.
     bool capped = false;
     do {
-#ifdef __HIP_DEVICE_COMPILE__
-      while (__ballot(DIR > 0 ? e.px <= lim : e.px >= lim) != 0ull) {
-#else
-      while (DIR > 0 ? e.px <= lim : e.px >= lim) {
-#endif
-        if (DIR > 0 ? e.px <= lim : e.px >= lim) {  // a plain tick (see go_plain_limit)
-          const double rr = rng.random();
-          e.px += (int)rint((DIR < 0 ? -4.0 : 2.0) + 2.0 * rr);
-          e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
-          r.reward += -1;
-          if (DIR > 0 ? e.px > lim : e.px < lim) pickups(L, e);  // left the span: as the full tick
-          if (++r.ticks >= TICK_CAP) {
-            e.f |= E_TICKCAP;
-            capped = true;
-            lim = DIR > 0 ? -0x40000000 : 0x40000000;  // out of the plain phase
-          }
+      // a lane leaves when its span ends; the wave when all have (a per-lane loop: a
+      // ballot-driven one, with the idle lanes kept inside, made the compiler copy ~26
+      // loop-carried registers per iteration and was slower)
+      while (DIR > 0 ? e.px <= lim : e.px >= lim) {  // a plain tick (see go_plain_limit)
+        const double rr = rng.random();
+        e.px += (int)rint((DIR < 0 ? -4.0 : 2.0) + 2.0 * rr);
+        e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
+        r.reward += -1;
+        if (DIR > 0 ? e.px > lim : e.px < lim) pickups(L, e);  // left the span: as the full tick
+        if (++r.ticks >= TICK_CAP) {
+          e.f |= E_TICKCAP;
+          capped = true;
+          lim = DIR > 0 ? -0x40000000 : 0x40000000;  // out of the plain phase
         }
       }
       if (capped) break;
