@@ -5,27 +5,43 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+``--gpus N`` without an external launcher starts its N ranks itself (fresh child processes,
+before anything touches a GPU; dist.spawn_ranks) and returns rank 0's exit code.
+
 One "step" = one TreasureGame.step() (TG/:91-96) of EVERY env of the batch: the on-device
 synthetic policy writes the actions (uniform over the 9 options, counter hash keyed by the
 global env index), tg_step runs each env's option to completion with auto-reset (k_classify
 then k_run).  Every G steps (--gather-every, default 10) the completed episodes are drained
-from the device queue and, for N > 1, all-gathered over RCCL.  Per-GPU work is fixed (1,048,576 envs per GPU = config C3, C4 at 8 GPUs), so scaling
-is weak.  Inputs are resident in HBM when the timed region starts.
+from the device queue and all-gathered over RCCL (dist.gather_padded: the one collective of
+SURVEY §8e); rank 0 keeps them and reports their number and an order-independent digest of
+(env, return, length), which does not depend on the number of GPUs.  Per-GPU work is fixed
+(1,048,576 envs per GPU = config C3; C4 at 8 GPUs), so scaling is weak.  Inputs are resident
+in HBM when the timed region starts.
+
+Before timing: W warm-up steps, then ``--burn-in`` steps (default 300) so that the envs'
+positions in their MT19937 generations are spread out and the timed steps regenerate
+generations at the steady-state rate (N x draws per env-step / 312 per step); the line
+reports the measured and the expected rate.
 
 Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (tg_step's kernels:
-algorithmic bytes per launch over their HIP-event-timed duration vs the 8 TB/s HBM peak) and
-``cpu_baseline`` (the C oracle timed on this box's host cores, a bounded sample).
+algorithmic bytes per launch over their HIP-event-timed duration vs the 8 TB/s HBM peak),
+``cpu_baseline`` (the C oracle timed on this box's host cores, a bounded sample) and, at
+N = 1, ``parity_check`` (4,096 envs x 200 steps replayed on the GPU and compared bit-for-bit
+with the oracle's run in the cpu_baseline leg) and ``masked_policy`` (the same measurement
+with the masked-uniform policy: every step runs an option).
 
 ``--workload c5`` is config C5 instead: 65,536 envs per GPU whose step also renders every
 env's screen (ObservationWrapper, TG/:38-51: tg_render -> k_render, 1,257,984 B per frame,
 synthetic sprite sheet); its roofline is k_render's frame bytes over its HIP-event time.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -36,16 +52,21 @@ METRIC = "env-steps/sec (whole node) at 1M batched envs, 1/2/4/8 MI355X; bit-exa
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ACTION_SEED = 0x5EED0001
 EP_CAP = 4096          # episode records gathered per rank per step of a drain interval (padded)
-# algorithmic bytes of one tg_step, per launch:
+# algorithmic bytes of one tg_step for THIS data layout, per launch:
 #   every env: action 4 + state word 16 read (classify)
 #   reward-None env: angles 16 + episode 8 read; episode 8 + obs 72 + reward/valid/done 6 written
 #   valid env: worklist index 4 + 4, state 16 + 16, angles 16 + 16, episode 8 + 8, obs 72, rows 6
 #   random() draw: one 8-B value (the pre-twisted generation's doubles)
 #   MT regeneration: 624 words read, 624 words + 312 values written
 BYTES_ENV, BYTES_INVALID, BYTES_VALID, BYTES_DRAW, BYTES_REGEN = 20, 110, 166, 8, 7488
+# SURVEY.md §8(d)'s layout-independent count per env-step: action 4 + obs 72 + reward 4 +
+# valid 1 + done 1 + state read/write 2 x 40 = 162, plus 24 per random() draw (8 B of MT words
+# read + 16 B amortised twist read/write)
+SURVEY_BYTES_STEP, SURVEY_BYTES_DRAW = 162, 24
 # algorithmic bytes of one k_render launch per env: the frame written (H*48 x W*48 x 3 =
 # 1,257,984 for the default level) + the env's state words read (st4 16 + angles 16)
 BYTES_RENDER_STATE = 32
+MT_DRAWS_PER_GEN = 312  # random() values per MT19937 generation
 
 
 def alg_bytes(st):
@@ -54,11 +75,18 @@ def alg_bytes(st):
             BYTES_DRAW * st["draws"] + BYTES_REGEN * st["regens"])
 
 
-def parse():
+def survey_bytes(st):
+    return SURVEY_BYTES_STEP * st["steps"] + SURVEY_BYTES_DRAW * st["draws"]
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--burn-in", type=int, default=None,
+                    help="untimed steps after the warm-up so that MT regenerations reach their "
+                         "steady-state rate (default 300 uniform / 60 masked; 0 disables)")
     ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
                     help="c3: vector-obs step (default, the headline); c5: step + RGB render")
     ap.add_argument("--envs", type=int, default=None,
@@ -73,19 +101,24 @@ def parse():
                          "the step kernels (episodes drained / gathered every K steps); 0: the "
                          "per-step API (tg_policy_actions + tg_step per step)")
     ap.add_argument("--gather-every", type=int, default=10,
-                    help="per-step API: drain (and, N > 1, all-gather) the completed episodes "
-                         "every G steps (SURVEY §8e: batched gather; 1 = every step). "
-                         "--rollout K drains every K steps")
+                    help="per-step API: drain and gather the completed episodes every G steps "
+                         "(SURVEY §8e: batched gather; 1 = every step); --rollout K drains "
+                         "every K steps")
+    ap.add_argument("--secondary-steps", type=int, default=30,
+                    help="N = 1, c3: steps of the masked-policy line (0 disables it)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="target duration of the CPU-baseline sample (0 disables it)")
+                    help="target duration of the CPU-baseline sample (0 disables it and the "
+                         "parity check)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_step.json"),
                     help="PMC-derived HBM bytes per tg_step (profiles/), if measured")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(seconds, policy):
+# ---- CPU legs (the oracle is loaded here only: bench's cpu_baseline leg) ------------------
+def cpu_baseline(seconds, policy, parity_envs=0):
     """The C oracle (oracle/, the CPU restatement of the reference) on this box's host cores:
-    a bounded sample of the same workload (same seeds, action stream and auto-reset)."""
+    a bounded sample of the same workload (same seeds, action stream and auto-reset).  Also
+    returns the per-env rolling hashes of the first ``parity_envs`` envs after 200 steps."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # noqa: E402 — bench's cpu_baseline leg only
     O.build()
@@ -97,22 +130,30 @@ def cpu_baseline(seconds, policy):
     t0 = time.perf_counter()
     O.run(0, 0, n, steps, ACTION_SEED, pol, True, full=False, nthreads=threads)
     dt = time.perf_counter() - t0
-    n = max(threads * 64, int(n * seconds / max(dt, 1e-3)))
+    n = max(threads * 64, parity_envs, int(n * seconds / max(dt, 1e-3)))
     t0 = time.perf_counter()
-    O.run(0, 0, n, steps, ACTION_SEED, pol, True, full=False, nthreads=threads)
+    r = O.run(0, 0, n, steps, ACTION_SEED, pol, True, full=False, nthreads=threads)
     dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": "C oracle (oracle/tg_oracle.c, CPU restatement of the reference step path), "
-                      "envs 0..%d x %d steps, %s policy, auto-reset, %d OpenMP threads, %.1f s"
-                      % (n - 1, steps, policy, threads, dt),
-            "reference_python_1core_measured_in_build_container": 14400.0}
+    out = {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+           "sample": "C oracle (oracle/tg_oracle.c, CPU restatement of the reference step path), "
+                     "envs 0..%d x %d steps, %s policy, auto-reset, %d OpenMP threads, %.1f s"
+                     % (n - 1, steps, policy, threads, dt)}
+    return out, r["hash"][:parity_envs], steps
+
+
+def python_baseline(seconds, policy):
+    """The pure-Python structural restatement of the reference step path (oracle/pyref.py:
+    the reference's pixel loops, object graph and random module), on 1 process and on one
+    process per host core, same seeds / actions / auto-reset."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyref  # noqa: E402 — bench's cpu_baseline leg only
+    return pyref.throughput(seconds, policy, ACTION_SEED)
 
 
 def cpu_baseline_render(seconds, policy):
     """C5's CPU leg: the oracle's renderer restatement (plus construct/reset and one step per
     env) on this box's host cores, synthetic sprites."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
     import oracle as O  # noqa: E402 — bench's cpu_baseline leg only
     from gym_treasure_game_amd.render import synthetic_sprites
     O.build()
@@ -135,18 +176,251 @@ def cpu_baseline_render(seconds, policy):
                       % (policy, n - 1, threads, dt)}
 
 
+# ---- parity spot check: the product on the GPU, hashed like tests/golden/make_golden.py -----
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _sm64(x):
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def _rec_hash(h, obs, rew, valid, done):
+    bits = np.ascontiguousarray(obs).view(np.uint64)
+    with np.errstate(over="ignore"):
+        for k in range(9):
+            h = _sm64(h ^ bits[:, k])
+        w = (rew.astype(np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)) | \
+            (valid.astype(np.uint64) << np.uint64(32)) | (done.astype(np.uint64) << np.uint64(40))
+        return _sm64(h ^ w)
+
+
+def gpu_hashes(tg, n, steps, policy, mode, dev):
+    """Per-env rolling hashes of envs 0..n-1 (seed 0, the bench's action stream, auto-reset)
+    after ``steps`` steps, through the product API."""
+    vec = tg.TreasureGameVec(n, seed=0, autoreset=True, mode=mode, device=dev)
+    h = np.arange(n, dtype=np.uint64)
+    z32, z8 = np.zeros(n, np.int32), np.zeros(n, np.uint8)
+    h = _rec_hash(h, vec.reset().cpu().numpy(), z32, z8, z8)
+    for t in range(steps):
+        o, r, v, d, info = vec.step(vec.policy_actions(t, ACTION_SEED, policy))
+        h = _rec_hash(h, info["final_obs"].cpu().numpy(), r.cpu().numpy(), v.cpu().numpy(),
+                      d.cpu().numpy())
+    errs = vec.errors()
+    vec.close()
+    return h, errs
+
+
+# ---- the measured loop ------------------------------------------------------------------------
+class Runner:
+    """One rank's batch and its step loop (per-step API or tg_rollout), with the episode
+    drain + gather every G steps."""
+
+    def __init__(self, tg, D, args, policy, count, offset, world, dev, keep_log):
+        self.tg, self.D, self.args, self.world, self.dev = tg, D, args, world, dev
+        self.count = count
+        self.autoreset = not args.no_autoreset
+        vec = tg.TreasureGameVec(count, seed=0, global_offset=offset, autoreset=False, device=dev)
+        vec.set_mode(args.mode, args.run_blocks)
+        vec.autoreset = self.autoreset  # final_obs is not requested: obs/reward/valid/done only
+        vec.reset()
+        self.vec = vec
+        self.K = args.rollout
+        self.G = self.K if self.K else args.gather_every
+        if self.G < 1:
+            raise SystemExit("--gather-every must be >= 1")
+        self.ep_cap = EP_CAP * self.G  # records per rank per drain (padded; the rest stays queued)
+        self.ep_rows = torch.zeros((self.ep_cap, 2), dtype=torch.int64, device=dev)
+        self.ep_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.all_rows = self.all_cnt = None
+        if world > 1:
+            self.all_rows = torch.empty((world * self.ep_cap, 2), dtype=torch.int64, device=dev)
+            self.all_cnt = torch.empty(world, dtype=torch.int32, device=dev)
+        drains = args.steps // self.G + 2
+        self.log = D.EpisodeLog(drains, world, self.ep_cap, dev, keep=keep_log)
+        L, h = vec._L, vec.handle
+        self.L, self.h = L, h
+        self.flags = tg._lib.TG_STEP_AUTORESET if self.autoreset else 0
+        p = self.p
+        self.stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        self.pol = tg._lib.TG_POLICY_MASKED if policy == "masked" else tg._lib.TG_POLICY_UNIFORM
+        self.args_step = (h, p(vec._act), p(vec._obs), p(vec._rew), p(vec._valid), p(vec._done),
+                          None, self.flags, self.stream)
+        if self.K:
+            if args.workload == "c5" or args.steps % self.K or args.warmup % self.K:
+                raise SystemExit("--rollout K: c3 only, with --steps and --warmup multiples of K")
+            self.roll = [torch.empty((self.K, count), dtype=d, device=dev)
+                         for d in (torch.int32, torch.uint8, torch.uint8)]
+        self.frames, self.rev, self.timing = None, [], False
+        if args.workload == "c5":  # ObservationWrapper.step: render every env after its step
+            vec.render_init(tg.synthetic_sprites(seed=1))
+            self.frames = torch.empty((count,) + vec.frame_shape, dtype=torch.uint8, device=dev)
+
+    @staticmethod
+    def p(t):
+        return ctypes.c_void_p(t.data_ptr())
+
+    def drain(self, log=True):
+        chk, L, p = self.tg._lib.check, self.L, self.p
+        chk(L.tg_episodes(self.h, p(self.ep_rows), p(self.ep_cnt), self.ep_cap, self.stream),
+            "episodes")
+        rows, cnt = self.D.gather_padded(self.ep_rows, self.ep_cnt, self.all_rows, self.all_cnt)
+        if log:
+            self.log.add(rows, cnt)
+        return cnt
+
+    def drain_all(self, log):
+        """drain until every rank's queue is empty (untimed; synchronises)"""
+        while True:
+            cnt = self.drain(log)
+            if int(cnt.sum().item()) == 0:
+                return
+
+    def step(self, t):
+        chk, L, p = self.tg._lib.check, self.L, self.p
+        K = self.K
+        if K:  # steps t .. t+K-1 in one call
+            if t % K:
+                return
+            chk(L.tg_rollout(self.h, K, ACTION_SEED, t, self.pol, self.flags, None, None,
+                             p(self.roll[0]), p(self.roll[1]), p(self.roll[2]), self.stream),
+                "rollout")
+        else:
+            chk(L.tg_policy_actions(self.h, ACTION_SEED, t, self.pol, p(self.vec._act),
+                                    self.stream), "actions")
+            chk(L.tg_step(*self.args_step), "tg_step")
+        if (t + 1) % self.G == 0 or K:
+            self.drain()
+        if self.frames is not None:
+            if self.timing:  # k_render alone, on the stream it is launched on
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            chk(L.tg_render(self.h, 0, self.count, p(self.frames), self.stream), "tg_render")
+            if self.timing:
+                ev[1].record()
+                self.rev.append(ev)
+
+    def measure(self, warmup, burn_in, steps):
+        """warm-up + burn-in (untimed), then EXACTLY ``steps`` timed steps between barriers;
+        returns the max-over-ranks wall time and this rank's stats."""
+        t = 0
+        for _ in range(warmup + burn_in):
+            self.step(t)
+            t += 1
+        self.drain_all(log=False)  # the timed region's records are its own
+        torch.cuda.synchronize(self.dev)
+        self.log.reset()
+        vec = self.vec
+        vec.stats_reset()
+        vec.set_timing(True)
+        self.timing = True
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step(t)
+            t += 1
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        self.timing = False
+        vec.set_timing(False)
+        st = vec.stats()
+        self.drain_all(log=True)  # records of the timed steps still queued (untimed)
+        if self.world > 1:
+            dt_t = torch.tensor([dt], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+            dt = float(dt_t.item())
+        return dt, st
+
+
+def node_totals(st, world, dev):
+    keys = ["steps", "ticks", "draws", "valid_steps", "episodes", "episodes_dropped",
+            "wave_ticks", "regens"]
+    if world == 1:
+        return {k: st[k] for k in keys}
+    tot = torch.tensor([st[k] for k in keys], dtype=torch.int64, device=dev)
+    dist.all_reduce(tot)
+    return dict(zip(keys, tot.tolist()))
+
+
+def load_pmc(path, envs, policy, mode, regens_per_step, burn_in):
+    """profiles/traffic_step.json (scripts/prof_summary.py) when its PMC source run matches
+    this run: same envs, policy and step mode, and a regeneration rate within 10 %."""
+    if not os.path.exists(path):
+        return None
+    tj = json.load(open(path))
+    if (tj.get("envs") != envs or tj.get("policy") != policy or tj.get("mode") != mode):
+        return None
+    ref = tj.get("regens_per_step")
+    if ref is None or abs(regens_per_step - ref) > 0.1 * max(ref, 1.0):
+        return None
+    return tj
+
+
+def step_line(args, runner, dt, st, node, world, total):
+    """the bench line's roofline / counters for the c3 step measurement"""
+    env_steps = total * args.steps
+    assert node["steps"] == env_steps, (node, env_steps)
+    launches = max(st["launches"], 1)
+    kern_s = st["kernel_ms"] / 1e3 / launches
+    alg = alg_bytes(st) / launches
+    surv = survey_bytes(st) / launches
+    achieved = alg / kern_s / 1e9
+    d = node["draws"] / max(node["steps"], 1)
+    regens = st["regens"] / launches
+    regens_expected = runner.count * d / MT_DRAWS_PER_GEN
+    lane_eff = node["ticks"] / max(64 * node["wave_ticks"], 1)
+    pmc = load_pmc(args.traffic_json, args.envs, args.policy_used, args.mode, regens,
+                   args.burn_in_used)
+    roof = {"bound": "hbm",
+            "kernel": ("tg_step = k_classify + k_run" if args.mode == "compact"
+                       else "tg_step = k_step"),
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+            "traffic_source": pmc["source"] if pmc else None,
+            "kernel_ms": kern_s * 1e3,
+            "alg_bytes_per_launch": alg,
+            "alg_bytes_per_launch_survey": surv,
+            "achieved_survey": surv / kern_s / 1e9,
+            "frac_survey": surv / kern_s / 1e9 / HBM_PEAK_GBS,
+            # what ends the kernels (DESIGN.md §3.5): the go waves' dependent per-tick chains,
+            # not HBM bandwidth; the counters below are the evidence
+            "limiter": "issue-latency of the option tick loops (lane_efficiency, valu_util)",
+            "valu_util": pmc.get("valu_util") if pmc else None,
+            "lane_efficiency": lane_eff}
+    return {
+        "ticks_per_s": node["ticks"] / dt,
+        # SURVEY §8d: ticks executed / lane-ticks issued by the tick loops' wavefronts
+        "lane_efficiency": lane_eff,
+        "valid_step_frac": node["valid_steps"] / max(node["steps"], 1),
+        "draws_per_step": d,
+        "regens_per_step": regens,
+        "regens_per_step_steady_state": regens_expected,
+        "roofline": roof,
+    }
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0 and args.gpus > 1:
+        # no external launcher: start the ranks as fresh processes before any GPU call
+        import gym_treasure_game_amd.dist as D
+        sys.exit(D.spawn_ranks(args.gpus, sys.argv[1:]))
+    world = max(world, 1)
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     c5 = args.workload == "c5"
     if args.envs is None:
         args.envs = 65536 if c5 else 1 << 20
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus %d needs torch.distributed.run with %d processes"
-                             % (args.gpus, args.gpus))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -158,132 +432,29 @@ def main():
 
     total = args.envs * world
     offset, count = D.shard(total, rank, world)
-    autoreset = not args.no_autoreset
-    vec = tg.TreasureGameVec(count, seed=0, global_offset=offset, autoreset=False, device=dev)
-    vec.set_mode(args.mode, args.run_blocks)
-    vec.autoreset = autoreset  # final_obs is not requested: obs/reward/valid/done only
-    vec.reset()
-    K = args.rollout
-    G = K if K else args.gather_every
-    if G < 1:
-        raise SystemExit("--gather-every must be >= 1")
-    ep_cap = EP_CAP * G  # records per rank per drain (padded; the rest stays queued)
-    ep_rows = torch.empty((ep_cap, 2), dtype=torch.int64, device=dev)
-    ep_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    gathered = torch.zeros(1, dtype=torch.int64, device=dev)  # records seen by this rank
-    if world > 1:
-        all_rows = torch.empty((world * ep_cap, 2), dtype=torch.int64, device=dev)
-        all_cnt = torch.empty(world, dtype=torch.int32, device=dev)
-    L, h = vec._L, vec.handle
-    obs, rew, val, don = vec._obs, vec._rew, vec._valid, vec._done
-    act = vec._act
-    flags = tg._lib.TG_STEP_AUTORESET if autoreset else 0
-    import ctypes
-    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    pol = tg._lib.TG_POLICY_MASKED if args.policy == "masked" else tg._lib.TG_POLICY_UNIFORM
-    args_step = (h, p(act), p(obs), p(rew), p(val), p(don), None, flags, stream)
+    args.policy_used = args.policy
+    args.burn_in_used = (args.burn_in if args.burn_in is not None
+                         else (300 if args.policy == "uniform" else 60))
+    run = Runner(tg, D, args, args.policy, count, offset, world, dev, keep_log=(rank == 0))
+    dt, st = run.measure(args.warmup, args.burn_in_used, args.steps)
+    node = node_totals(st, world, dev)
+    errs = run.vec.errors()
+    rec, digest = run.log.digest() if rank == 0 else (None, None)
+    autoreset = run.autoreset
 
-    frames, rev = None, []
-    if c5:  # ObservationWrapper.step: render every env's screen after its step
-        vec.render_init(tg.synthetic_sprites(seed=1))
-        frames = torch.empty((count,) + vec.frame_shape, dtype=torch.uint8, device=dev)
-    timing = [False]
-
-    if K:
-        if c5 or args.steps % K or args.warmup % K:
-            raise SystemExit("--rollout K: c3 only, with --steps and --warmup multiples of K")
-        roll = [torch.empty((K, count), dtype=d, device=dev)
-                for d in (torch.int32, torch.uint8, torch.uint8)]
-
-    def one_step(t):
-        if K:  # steps t .. t+K-1 in one call
-            if t % K:
-                return
-            tg._lib.check(L.tg_rollout(h, K, ACTION_SEED, t, pol, flags, None, None,
-                                       p(roll[0]), p(roll[1]), p(roll[2]), stream), "rollout")
-        else:
-            tg._lib.check(L.tg_policy_actions(h, ACTION_SEED, t, pol, p(act), stream), "actions")
-            tg._lib.check(L.tg_step(*args_step), "tg_step")
-        if (t + 1) % G == 0 or K:
-            drain()
-        if c5:
-            if timing[0]:  # k_render alone, on the stream it is launched on
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ev[0].record()
-            tg._lib.check(L.tg_render(h, 0, count, p(frames), stream), "tg_render")
-            if timing[0]:
-                ev[1].record()
-                rev.append(ev)
-
-    def drain():
-        tg._lib.check(L.tg_episodes(h, p(ep_rows), p(ep_cnt), ep_cap, stream), "episodes")
-        if world > 1:  # the one collective: completed episodes over RCCL/xGMI
-            dist.all_gather_into_tensor(all_cnt, ep_cnt)
-            dist.all_gather_into_tensor(all_rows, ep_rows)
-            gathered.add_(all_cnt.sum())
-        else:
-            gathered.add_(ep_cnt[0])
-
-    for t in range(args.warmup):
-        one_step(t)
-    drain()  # empty the queue, so the timed region's records are its own
-    torch.cuda.synchronize(dev)
-    gathered.zero_()
-    vec.stats_reset()
-    vec.set_timing(True)
-    timing[0] = True
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for t in range(args.warmup, args.warmup + args.steps):
-        one_step(t)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    st = vec.stats()
-    errs = vec.errors()
-    if world > 1:
-        dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-        dt = float(dt_t.item())
-        keys = ["steps", "ticks", "draws", "valid_steps", "episodes", "wave_ticks"]
-        tot = torch.tensor([st[k] for k in keys], dtype=torch.int64, device=dev)
-        dist.all_reduce(tot)
-        node = dict(zip(keys, tot.tolist()))
-    else:
-        node = {k: st[k] for k in ("steps", "ticks", "draws", "valid_steps", "episodes",
-                                   "wave_ticks")}
-
+    line = None
     if rank == 0:
         env_steps = total * args.steps
-        assert node["steps"] == env_steps, (node, env_steps)
-        launches = max(st["launches"], 1)
-        kern_s = st["kernel_ms"] / 1e3 / launches
-        alg = alg_bytes(st) / launches
-        achieved = alg / kern_s / 1e9
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            tj = json.load(open(args.traffic_json))
-            if (tj.get("envs") == args.envs and tj.get("policy") == args.policy
-                    and tj.get("mode", "direct") == args.mode):
-                traffic = tj.get("hbm_bytes_per_launch")
-        roof = {"bound": "hbm",
-                "kernel": ("tg_step = k_classify + k_run" if args.mode == "compact"
-                           else "tg_step = k_step"),
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic, "kernel_ms": kern_s * 1e3,
-                "alg_bytes_per_launch": alg}
+        if autoreset:
+            # every episode the step kernels counted reached rank 0 through the gather
+            assert rec == node["episodes"] - node["episodes_dropped"], (rec, node)
         workload = ("C3/C4: %d batched treasure_game-v0 envs per GPU, vector obs, %s random "
                     "options, auto-reset%s" % (args.envs, args.policy,
                                                " + RCCL episode gather" if world > 1 else ""))
-        extra = {}
+        extra = step_line(args, run, dt, st, node, world, total)
         if c5:
-            fh, fw, _ = vec.frame_shape
-            r_ms = sum(a.elapsed_time(b) for a, b in rev) / max(len(rev), 1)
+            fh, fw, _ = run.vec.frame_shape
+            r_ms = sum(a.elapsed_time(b) for a, b in run.rev) / max(len(run.rev), 1)
             r_alg = count * (fh * fw * 3 + BYTES_RENDER_STATE)
             r_ach = r_alg / (r_ms / 1e3) / 1e9
             r_traffic = None
@@ -292,10 +463,11 @@ def main():
                 tj = json.load(open(tj_path))
                 if tj.get("envs") == count:
                     r_traffic = tj.get("hbm_bytes_per_launch")
-            extra["step_roofline"] = roof
-            roof = {"bound": "hbm", "kernel": "k_render (tg_render)", "achieved": r_ach,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r_ach / HBM_PEAK_GBS,
-                    "traffic": r_traffic, "kernel_ms": r_ms, "alg_bytes_per_launch": r_alg}
+            extra["step_roofline"] = extra.pop("roofline")
+            extra["roofline"] = {"bound": "hbm", "kernel": "k_render (tg_render)",
+                                 "achieved": r_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": r_ach / HBM_PEAK_GBS, "traffic": r_traffic,
+                                 "kernel_ms": r_ms, "alg_bytes_per_launch": r_alg}
             workload = ("C5: %d batched treasure_game-v0 envs per GPU, ObservationWrapper RGB "
                         "render (%dx%dx3 u8 frames, synthetic sprites) after every step, %s "
                         "random options, auto-reset" % (args.envs, fh, fw, args.policy))
@@ -309,25 +481,55 @@ def main():
             "config": {"workload": workload,
                        "envs_per_gpu": args.envs, "total_envs": total, "policy": args.policy,
                        "autoreset": autoreset, "step_mode": args.mode,
-                       "api": ("tg_rollout x%d (policy inside the step kernels)" % K if K
-                               else "tg_policy_actions + tg_step per step"),
+                       "api": ("tg_rollout x%d (policy inside the step kernels)" % args.rollout
+                               if args.rollout else "tg_policy_actions + tg_step per step"),
                        "parallelism": "env-shard x%d" % world},
-            "ticks_per_s": node["ticks"] / dt,
-            # ticks executed / lane-ticks issued by the tick loops' wavefronts
-            "lane_efficiency": node["ticks"] / max(64 * node["wave_ticks"], 1),
-            "valid_step_frac": node["valid_steps"] / max(node["steps"], 1),
-            "draws_per_step": node["draws"] / max(node["steps"], 1),
-            "episodes": node["episodes"], "error_flags": errs,
-            "gather_every": G, "episodes_gathered": int(gathered.item()),
-            "regens_per_step": st["regens"] / launches,
-            "roofline": roof,
+            "burn_in": args.burn_in_used,
         }
         line.update(extra)
-        if args.cpu_seconds > 0 and world == 1:
-            line["cpu_baseline"] = (cpu_baseline_render if c5 else cpu_baseline)(
-                args.cpu_seconds, args.policy)
+        line.update({"episodes": node["episodes"], "episodes_dropped": node["episodes_dropped"],
+                     "episodes_gathered": rec, "episode_digest": digest,
+                     "gather_every": run.G, "error_flags": errs})
+    run.vec.close()
+    del run
+
+    if rank == 0 and world == 1 and not c5 and args.secondary_steps > 0:
+        # the masked-uniform policy: every step runs an option (report it beside
+        # the uniform headline), same batch size, its own burn-in
+        other = "masked" if args.policy == "uniform" else "uniform"
+        a2 = parse(sys.argv[1:])
+        a2.envs, a2.policy, a2.policy_used = args.envs, other, other
+        a2.steps = args.secondary_steps
+        a2.burn_in_used = 60 if other == "masked" else 300
+        r2 = Runner(tg, D, a2, other, count, offset, world, dev, keep_log=True)
+        dt2, st2 = r2.measure(min(args.warmup, 5), a2.burn_in_used, a2.steps)
+        n2 = node_totals(st2, 1, dev)
+        sec = {"policy": other, "value": total * a2.steps / dt2, "unit": "env-steps/s",
+               "steps": a2.steps, "burn_in": a2.burn_in_used,
+               "ms_per_step": dt2 / a2.steps * 1e3}
+        sec.update(step_line(a2, r2, dt2, st2, n2, 1, total))
+        sec["episodes"] = n2["episodes"]
+        r2.vec.close()
+        line[other + "_policy"] = sec
+
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        if c5:
+            line["cpu_baseline"] = cpu_baseline_render(args.cpu_seconds, args.policy)
+        else:
+            pe, ps = 4096, 200
+            cb, ref_h, steps_h = cpu_baseline(args.cpu_seconds, args.policy, parity_envs=pe)
+            try:
+                cb["reference_python"] = python_baseline(min(args.cpu_seconds, 10.0), args.policy)
+            except ImportError:
+                cb["reference_python"] = None
+            line["cpu_baseline"] = cb
+            got, gerr = gpu_hashes(tg, pe, steps_h, args.policy, args.mode, dev)
+            bad = int(np.count_nonzero(got != ref_h))
+            line["parity_check"] = {"envs": pe, "steps": steps_h, "policy": args.policy,
+                                    "autoreset": True, "mismatched_envs": bad,
+                                    "error_flags": gerr, "bit_exact": bad == 0 and gerr == 0}
+    if rank == 0:
         print(json.dumps(line), flush=True)
-    vec.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

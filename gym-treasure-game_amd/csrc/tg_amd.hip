@@ -472,6 +472,12 @@ struct EpQueue {
 };
 
 // Completed episodes (auto-reset): wavefront ballot, popcount prefix, one atomic per wave.
+// The queue is drained by tg_episodes; if nobody drains it, the count must not run away (an
+// int32 that wraps would turn the bound check into an out-of-bounds store): a wave whose
+// records do not all fit clamps the count back to cap (atomicMin) after its add.  Between an
+// add and its clamp other waves can add, so the count stays below cap + the records of the
+// waves in flight (<= cap + n < 2^31 with cap <= 2^28 and n < 2^30); slots are compared
+// unsigned.  The records that do not fit are counted per wave in the wave's own block slot.
 // Must be reached by every lane of the wave.
 __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, const EpQueue& q,
                                                 unsigned long long* stats) {
@@ -479,19 +485,26 @@ __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, 
   if (!b) return;
   const int lane = threadIdx.x & 63;
   const int first = __ffsll((long long)b) - 1;
+  const int cnt = __popcll(b);
   int base = 0;
-  if (lane == first) base = atomicAdd(q.count, __popcll(b));
+  if (lane == first) {
+    base = atomicAdd(q.count, cnt);
+    if ((uint32_t)base + (uint32_t)cnt > (uint32_t)q.cap) {
+      atomicMin(q.count, q.cap);
+      const uint32_t lost = (uint32_t)base >= (uint32_t)q.cap
+                                ? (uint32_t)cnt : (uint32_t)base + (uint32_t)cnt - (uint32_t)q.cap;
+      atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + ST_EP_OVERFLOW], (unsigned long long)lost);
+    }
+  }
   base = __shfl(base, first, 64);
   if (mine) {
-    const int slot = base + __popcll(b & ((1ull << lane) - 1ull));
-    if (slot < q.cap) {
+    const uint32_t slot = (uint32_t)base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+    if (slot < (uint32_t)q.cap) {
       tg_episode r;
       r.env = g;
       r.ret = ep.x;
       r.len = ep.y;
       q.eps[slot] = r;
-    } else {
-      atomicAdd(&stats[ST_EP_OVERFLOW], 1ull);  // rare: block 0's slot
     }
     ep = make_int2(0, 0);
   }
@@ -946,7 +959,7 @@ __global__ __launch_bounds__(BLOCK) void k_drain_episodes(tg_episode* __restrict
                                                            int32_t* __restrict__ count,
                                                            int32_t cap) {
   int32_t n = *eps_count;
-  if (n > eps_cap) n = eps_cap;
+  if ((uint32_t)n > (uint32_t)eps_cap) n = eps_cap;  // see record_episodes: never above cap + n
   const int32_t m = n < cap ? n : cap;
   for (int32_t k = threadIdx.x; k < m; k += BLOCK) out[k] = eps[k];
   __syncthreads();
@@ -962,6 +975,43 @@ __global__ __launch_bounds__(BLOCK) void k_drain_episodes(tg_episode* __restrict
     *eps_count = n - m;
     *count = m;
   }
+}
+
+// The six collision predicates (IM/:232-288) at every pixel of [x0, x1) x [y0, y1) with the
+// doors closed per door_bits, bit order as the reference's predicate listing: up_clear, can_go_up,
+// can_go_down, can_go_left, can_go_right, can_fall.  The device build of Map (mul24 / div48
+// take the __umul24 path only here), pinned against the reference's F2 truth tables.
+__global__ __launch_bounds__(BLOCK) void k_predicates(Level L, const uint32_t* __restrict__ grid,
+                                                       int x0, int x1, int y0, int y1,
+                                                       uint32_t door_bits,
+                                                       uint8_t* __restrict__ out) {
+  LEVEL_IN_LDS();
+  (void)trig;
+  const int64_t w = x1 - x0;
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= w * (int64_t)(y1 - y0)) return;
+  Env e{};
+  e.px = x0 + (int)(i % w);
+  e.py = y0 + (int)(i / w);
+  e.f = (door_bits & 7u) << F_OBJ;
+  out[i] = (uint8_t)((unsigned)m.up_clear(e) | (unsigned)m.can_go_up(e) << 1 |
+                     (unsigned)m.can_go_down(e) << 2 | (unsigned)m.can_go_side(e, -1) << 3 |
+                     (unsigned)m.can_go_side(e, +1) << 4 | (unsigned)m.can_fall(e) << 5);
+}
+
+// tg_read_state's MT part: the generation holding each env's position (CPython's mt[]),
+// envs [first, first + count) -> dst [count][624] (contiguous), 16 B per lane
+__global__ __launch_bounds__(BLOCK) void k_gather_mt(Soa S, int64_t first, int64_t count,
+                                                      uint32_t* __restrict__ dst) {
+  constexpr int Q = MT_N / 4;  // 156 uint4 per generation
+  const int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (t >= count * Q) return;
+  const int64_t k = t / Q;
+  const int q = (int)(t - k * Q);
+  const int64_t i = first + k;
+  const uint32_t half = mt_half(S.st4[i].w & MT_POS_MASK);
+  const uint4* src = reinterpret_cast<const uint4*>(S.mt + i * MT_WORDS + half);
+  reinterpret_cast<uint4*>(dst)[t] = src[q];
 }
 
 __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4, int64_t n,
@@ -1001,6 +1051,9 @@ int64_t tg_num_envs(const tg_batch* h) { return h ? h->n : 0; }
 int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offset, int device,
               const char* dom, const char* objs, const char* inter) {
   if (!out || n <= 0 || global_offset < 0) return fail(TG_E_INVAL, "tg_create: bad arguments");
+  // every env's seed seed_base + global_offset + i must be a 64-bit init_by_array key
+  if ((uint64_t)global_offset > ~seed_base || (uint64_t)(n - 1) > ~(seed_base + (uint64_t)global_offset))
+    return fail(TG_E_INVAL, "tg_create: seed_base + global_offset + num_envs - 1 exceeds 2^64 - 1");
   *out = nullptr;
   if (!dom && !objs && !inter) {
     dom = kDefaultDomain;
@@ -1270,6 +1323,32 @@ int tg_set_timing(tg_batch* h, int enable) {
   return TG_OK;
 }
 
+int tg_set_episode_capacity(tg_batch* h, int32_t cap) {
+  BIND(h);
+  if (cap < 1 || cap > (1 << 28)) return fail(TG_E_INVAL, "tg_set_episode_capacity: cap %d", cap);
+  HIP_TRY(hipDeviceSynchronize());
+  tg_episode* eps = nullptr;
+  if (hipMalloc((void**)&eps, sizeof(tg_episode) * (size_t)cap) != hipSuccess)
+    return fail(TG_E_NOMEM, "tg_set_episode_capacity: %d records", cap);
+  (void)hipFree(h->eps);
+  h->eps = eps;
+  h->eps_cap = cap;
+  HIP_TRY(hipMemset(h->eps_count, 0, sizeof(int32_t)));
+  return TG_OK;
+}
+
+int tg_predicate_table(tg_batch* h, int32_t x0, int32_t x1, int32_t y0, int32_t y1,
+                       uint32_t door_bits, uint8_t* out, void* stream) {
+  BIND(h);
+  if (!out || x1 <= x0 || y1 <= y0 || x0 < -4096 || x1 > 32000 || y0 < -4096 || y1 > 32000)
+    return fail(TG_E_INVAL, "tg_predicate_table: bad box or null output");
+  const int64_t cells = (int64_t)(x1 - x0) * (y1 - y0);
+  hipLaunchKernelGGL(k_predicates, dim3((unsigned)((cells + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                     (hipStream_t)stream, h->L, h->grid, x0, x1, y0, y1, door_bits, out);
+  HIP_TRY(hipGetLastError());
+  return TG_OK;
+}
+
 int tg_get_stats(tg_batch* h, tg_stats* out) {
   BIND(h);
   if (!out) return fail(TG_E_INVAL, "tg_get_stats: null output");
@@ -1310,9 +1389,12 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
   BIND(h);
   HIP_TRY(hipDeviceSynchronize());
   const int64_t n = h->n;
-  if (pos || flags || objs) {
-    std::vector<uint4> st((size_t)n);
+  std::vector<uint4> st;
+  if (pos || flags || objs || mt || mt_pos) {
+    st.resize((size_t)n);
     HIP_TRY(hipMemcpy(st.data(), h->S.st4, sizeof(uint4) * n, hipMemcpyDeviceToHost));
+  }
+  if (pos || flags || objs) {
     for (int64_t i = 0; i < n; ++i) {
       const uint4 s = st[(size_t)i];
       if (pos) {
@@ -1330,17 +1412,31 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
   }
   if (ang) HIP_TRY(hipMemcpy(ang, h->S.ang, sizeof(double2) * n, hipMemcpyDeviceToHost));
   if (ep) HIP_TRY(hipMemcpy(ep, h->S.ep, sizeof(int2) * n, hipMemcpyDeviceToHost));
-  if (mt || mt_pos) {
-    // CPython's (mt[624], index) equivalent: the generation holding the position
-    std::vector<uint4> st((size_t)n);
-    HIP_TRY(hipMemcpy(st.data(), h->S.st4, sizeof(uint4) * n, hipMemcpyDeviceToHost));
-    for (int64_t i = 0; i < n; ++i) {
-      const uint32_t p = st[(size_t)i].w & MT_POS_MASK;  // MT_STALE: the OTHER half is stale
-      if (mt_pos) mt_pos[i] = p % MT_N;
-      if (mt)
-        HIP_TRY(hipMemcpy(mt + i * MT_N, h->S.mt + i * MT_WORDS + mt_half(p), sizeof(uint32_t) * MT_N,
-                          hipMemcpyDeviceToHost));
+  if (mt_pos) {
+    // CPython's index into the generation holding the position (MT_STALE: the OTHER half)
+    for (int64_t i = 0; i < n; ++i) mt_pos[i] = (st[(size_t)i].w & MT_POS_MASK) % MT_N;
+  }
+  if (mt) {
+    // the generations, gathered on the device into a bounded staging buffer (<= 64 Ki envs,
+    // 160 MB) and copied out in one transfer per chunk
+    const int64_t chunk = n < (1 << 16) ? n : (1 << 16);
+    uint32_t* stage = nullptr;
+    if (hipMalloc((void**)&stage, sizeof(uint32_t) * MT_N * (size_t)chunk) != hipSuccess)
+      return fail(TG_E_NOMEM, "tg_read_state: staging buffer");
+    int rc = TG_OK;
+    for (int64_t first = 0; first < n && rc == TG_OK; first += chunk) {
+      const int64_t cnt = n - first < chunk ? n - first : chunk;
+      const int64_t threads = cnt * (MT_N / 4);
+      hipLaunchKernelGGL(k_gather_mt, dim3((unsigned)((threads + BLOCK - 1) / BLOCK)), dim3(BLOCK),
+                         0, 0, h->S, first, cnt, stage);
+      hipError_t e = hipGetLastError();
+      if (e == hipSuccess)
+        e = hipMemcpy(mt + first * MT_N, stage, sizeof(uint32_t) * MT_N * (size_t)cnt,
+                      hipMemcpyDeviceToHost);
+      if (e != hipSuccess) rc = fail(TG_E_HIP, "tg_read_state: %s", hipGetErrorString(e));
     }
+    (void)hipFree(stage);
+    if (rc) return rc;
   }
   return TG_OK;
 }

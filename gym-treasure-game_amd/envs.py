@@ -113,12 +113,21 @@ class TreasureGameVec:
         self.num_envs = int(num_envs)
         self.seed = int(seed)
         self.global_offset = int(global_offset)
+        if self.num_envs <= 0 or self.global_offset < 0:
+            raise ValueError("num_envs must be > 0 and global_offset >= 0")
+        # env g is random.seed(seed + global_offset + g); the device seeds init_by_array with
+        # a key of at most two 32-bit words, so every env's seed must lie in [0, 2^64)
+        # (CPython's abs() of a negative seed is not monotone in g: TreasureGame maps it)
+        if self.seed < 0 or self.seed + self.global_offset + self.num_envs - 1 >= 2**64:
+            raise ValueError("seed + global_offset + g must lie in [0, 2**64) for every env "
+                             "(got seed=%d, global_offset=%d, num_envs=%d)"
+                             % (self.seed, self.global_offset, self.num_envs))
         self.autoreset = bool(autoreset)
         self.copy = bool(copy)
         texts = read_level(level_dir) if level_dir else (None, None, None)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            check(self._L.tg_create(ctypes.byref(h), self.num_envs, self.seed & (2**64 - 1),
+            check(self._L.tg_create(ctypes.byref(h), self.num_envs, self.seed,
                                     self.global_offset, self.device.index, *texts), "tg_create")
         self._h = h
         n, dev = self.num_envs, self.device
@@ -233,6 +242,15 @@ class TreasureGameVec:
     def drain_episodes(self, out, count):
         """Asynchronous device drain: up to out.shape[0] records -> ``out`` (int64 [cap, 2],
         the raw 16-B tg_episode rows), their number -> ``count`` (int32 [1])."""
+        if not (isinstance(out, torch.Tensor) and out.dtype == torch.int64 and out.dim() == 2
+                and out.size(1) == 2 and out.is_contiguous() and out.device == self.device):
+            raise ValueError("out must be a contiguous int64 [cap, 2] tensor on %s" % self.device)
+        if not (isinstance(count, torch.Tensor) and count.dtype == torch.int32
+                and count.numel() >= 1 and count.is_contiguous() and count.device == self.device):
+            raise ValueError("count must be a contiguous int32 tensor of >= 1 element on %s"
+                             % self.device)
+        if out.size(0) >= 2**31:
+            raise ValueError("out holds too many rows")
         check(self._L.tg_episodes(self.handle, _ptr(out), _ptr(count), out.shape[0],
                                   self._stream()), "tg_episodes")
 
@@ -262,6 +280,19 @@ class TreasureGameVec:
         runs in place); both are bit-identical."""
         m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT}[mode]
         check(self._L.tg_set_mode(self.handle, m, int(run_blocks)), "tg_set_mode")
+
+    def set_episode_capacity(self, cap):
+        """Resize the completed-episode queue (discards what it holds)."""
+        check(self._L.tg_set_episode_capacity(self.handle, int(cap)), "tg_set_episode_capacity")
+
+    def predicate_table(self, x0, x1, y0, y1, door_bits):
+        """The six collision predicates (IM/:232-288) evaluated on the device at every pixel
+        of [x0, x1) x [y0, y1) with doors closed per door_bits: uint8 [y1-y0, x1-x0] device
+        tensor, bit k = up_clear, can_go_up, can_go_down, can_go_left, can_go_right, can_fall."""
+        out = torch.empty((y1 - y0, x1 - x0), dtype=torch.uint8, device=self.device)
+        check(self._L.tg_predicate_table(self.handle, x0, x1, y0, y1, int(door_bits), _ptr(out),
+                                         self._stream()), "tg_predicate_table")
+        return out
 
     def set_timing(self, enable=True):
         check(self._L.tg_set_timing(self.handle, int(bool(enable))), "tg_set_timing")
@@ -379,6 +410,9 @@ class TreasureGame:
         self._sprites = sprites
         if seed is None:
             seed = random.getrandbits(64)
+        seed = abs(int(seed))  # random.seed(s) keys on abs(s) (CPython random_seed)
+        if seed >= 2**64:
+            raise ValueError("seed must satisfy |seed| < 2**64 (a two-word init_by_array key)")
         self._vec = TreasureGameVec(1, seed=seed, device=device, level_dir=level_dir)
         self.option_list = list(range(_lib.NUM_ACTIONS))
         self.option_names = list(OPTION_NAMES)

@@ -26,6 +26,9 @@ Fixture families:
   F2  predicates.npz     the 6 collision predicates (IM/:232-288) at every pixel position
                           px in [-24,696), py in [-56,680) with all doors open / all closed
   F5  resets.npz          obs after construct+reset for seeds 0..9999
+  F6  traj_level_<L>_{uniform,masked}.npz  16 envs x 400 uniform / 600 masked+auto-reset steps
+                          on levels/<L> (corridor, gen1-3: the reference constructor pointed
+                          at those files; gen* written by gen_level)
 
 Action streams come from a counter hash (see ``action_hash``), replicated bit-for-bit by
 oracle/tg_oracle.c and the device action generator.
@@ -149,6 +152,21 @@ class CountingRandom(random.Random):
         return super().random()
 
 
+_make_path = TG.make_path
+
+
+def use_level(level_dir):
+    """Point the UNMODIFIED TreasureGame constructor (TG/:63-76, which reads
+    make_path(dir, 'domain.txt') etc.) at another level's three files: the reference's own
+    constructor, reset_game (IM/:55-73, which re-reads the same paths) and loaders run; only
+    the paths differ.  None restores the default level."""
+    def mp(root, *args):
+        if level_dir is not None and args and str(args[-1]).endswith(".txt"):
+            return os.path.join(level_dir, str(args[-1]))
+        return _make_path(root, *args)
+    TG.make_path = mp
+
+
 def new_env(seed):
     rng = CountingRandom(seed)
     IM.random = rng
@@ -226,7 +244,8 @@ def make_rng_kat():
 # F3 full trajectories
 # ----------------------------------------------------------------------------------------
 def run_traj(args):
-    g, seed, steps, a0, masked, autoreset = args
+    g, seed, steps, a0, masked, autoreset = args[:6]
+    use_level(args[6] if len(args) > 6 else None)
     env, rng, obs = new_env(seed)
     T = steps
     O = np.zeros((T + 1, 9), np.float64)
@@ -265,17 +284,108 @@ def run_traj(args):
                 final_obs=FO, bag=np.array(bags))
 
 
-def make_traj(name, n_envs, steps, a0, masked, autoreset, jobs, seed0=0):
+def make_traj(name, n_envs, steps, a0, masked, autoreset, jobs, seed0=0, level_dir=None):
     with Pool(jobs) as p:
-        res = p.map(run_traj, [(g, seed0 + g, steps, a0, masked, autoreset)
+        res = p.map(run_traj, [(g, seed0 + g, steps, a0, masked, autoreset, level_dir)
                               for g in range(n_envs)])
     out = {k: np.stack([r[k] for r in res]) for k in res[0]}
     out["seed_base"] = np.int64(seed0)
     out["action_seed"] = np.uint64(a0)
     out["masked"] = np.uint8(masked)
     out["autoreset"] = np.uint8(autoreset)
+    if level_dir is not None:
+        out["level"] = np.array(os.path.basename(level_dir))
     np.savez_compressed(os.path.join(OUT, name), **out)
     return out
+
+
+# ----------------------------------------------------------------------------------------
+# F6 other levels: the reference constructor pointed at non-default level files
+# ----------------------------------------------------------------------------------------
+DEFAULT_INTERACTIONS = os.path.join(REF, "gym_treasure_game", "envs", "_treasure_game_impl",
+                                    "domain-interactions.txt")
+
+
+def gen_level(seed):
+    """A random level in the reference's formats with the reference's object roster (3 doors,
+    2 handles, key, bolt, gold; the default interactions file): k corridors between floors,
+    ladders (some running up through the corridor above), drop holes, the exit ladder in the
+    top wall.  The start is the top wall's ladder cell (the first non-wall cell, IM/:168-178)."""
+    r = random.Random(seed)
+    W = r.randint(12, 22)
+    k = r.randint(4, 7)
+    H = 2 * k + 1
+    g = [["/"] * W for _ in range(H)]
+    for i in range(k):
+        row = 1 + 2 * i
+        for x in range(1, W - 1):
+            g[row][x] = " "
+        if r.random() < 0.3:  # an interior wall stub splitting the corridor
+            g[row][r.randint(3, W - 4)] = "/"
+    g[0][r.randint(1, W - 2)] = "L"
+    for i in range(k - 1):
+        fl = 2 + 2 * i
+        for _ in range(r.randint(1, 2)):
+            c = r.randint(1, W - 2)
+            g[fl][c] = "L"
+            if r.random() < 0.5:
+                g[fl - 1][c] = "L"
+            if r.random() < 0.3:
+                g[fl + 1][c] = "L"
+        if r.random() < 0.6:  # a drop hole
+            c = r.randint(1, W - 2)
+            if g[fl][c] == "/":
+                g[fl][c] = " "
+    free = [(x, y) for y in range(1, H - 1, 2) for x in range(1, W - 1) if g[y][x] == " "]
+    r.shuffle(free)
+    cells = free[:8]
+    doors, handles, (key, bolt, gold) = cells[:3], cells[3:5], cells[5:8]
+    objs = ["door %d %d %s" % (x, y, r.choice(["True", "False"])) for x, y in doors]
+    objs += ["handle %d %d %s" % (x, y, r.choice(["True", "False"])) for x, y in handles]
+    objs += ["key %d %d" % key, "bolt %d %d True" % bolt, "gold %d %d" % gold]
+    dom = "\n".join("".join(row) for row in g) + "\n"
+    with open(DEFAULT_INTERACTIONS) as f:
+        inter = f.read()
+    return dom, "\n".join(objs) + "\n", inter
+
+
+def make_levels(jobs):
+    base = os.path.join(OUT, "levels")
+    for i in (1, 2, 3):
+        d = os.path.join(base, "gen%d" % i)
+        os.makedirs(d, exist_ok=True)
+        texts = gen_level(1000 + i)
+        for f, t in zip(("domain.txt", "domain-objects.txt", "domain-interactions.txt"), texts):
+            with open(os.path.join(d, f), "w") as fh:
+                fh.write(t)
+        with open(os.path.join(d, "README.md"), "w") as fh:
+            fh.write("Generated test level (tests/golden/make_golden.py gen_level(%d)): the "
+                     "reference's object roster and\ninteractions on a random layout.  "
+                     "traj_level_gen%d_*.npz hold the reference's trajectories on it.\n"
+                     % (1000 + i, i))
+    # a small hand-made level whose gold lies next to the exit ladder, so that random
+    # option sequences finish episodes on a non-default level (auto-reset path)
+    d = os.path.join(base, "exit")
+    os.makedirs(d, exist_ok=True)
+    dom = "////L///////\n/          /\n///////L////\n/       L  /\n////////////\n"
+    objs = ("door 9 3 True\ndoor 2 3 False\ndoor 10 1 False\nhandle 6 3 True\n"
+            "handle 4 3 False\nkey 1 3\nbolt 3 3 True\ngold 7 1\n")
+    with open(DEFAULT_INTERACTIONS) as f:
+        inter = f.read()
+    for f, t in zip(("domain.txt", "domain-objects.txt", "domain-interactions.txt"),
+                    (dom, objs, inter)):
+        with open(os.path.join(d, f), "w") as fh:
+            fh.write(t)
+    with open(os.path.join(d, "README.md"), "w") as fh:
+        fh.write("Hand-made test level (not from the reference): the gold lies next to the "
+                 "exit ladder, so random option\nsequences finish episodes on a non-default "
+                 "level.  traj_level_exit_*.npz hold the reference's\ntrajectories on it.\n")
+    for name in ("corridor", "gen1", "gen2", "gen3", "exit"):
+        d = os.path.join(base, name)
+        make_traj("traj_level_%s_uniform.npz" % name, 16, 400, ACTION_SEED_UNIFORM, False,
+                  False, jobs, seed0=0, level_dir=d)
+        make_traj("traj_level_%s_masked.npz" % name, 16, 600, ACTION_SEED_MASKED, True, True,
+                  jobs, seed0=50, level_dir=d)
 
 
 # ----------------------------------------------------------------------------------------
@@ -375,6 +485,8 @@ def main():
         make_traj("traj_autoreset.npz", 8, 4000, ACTION_SEED_MASKED, True, True, a.jobs, seed0=100)
     if not only or "pred" in only:
         make_predicates(a.jobs)
+    if not only or "levels" in only:
+        make_levels(a.jobs)
     if not only or "hash" in only:
         make_hash("hash_uniform.npz", 4096, 1000, ACTION_SEED_UNIFORM, False, a.jobs)
         make_hash("hash_masked.npz", 1024, 600, ACTION_SEED_MASKED, True, a.jobs)

@@ -132,3 +132,19 @@ def test_core_vs_oracle_corridor(hostcheck, oracle, policy, autoreset):
     assert_same(o, r)
     np.testing.assert_array_equal(o["ticks"], r["ticks"])
     assert r["draws"].max() > 624 * 4  # many multi-generation steps really happened
+
+
+LEVELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels")
+
+
+@pytest.mark.parametrize("level", ["corridor", "gen1", "gen2", "gen3", "exit"])
+@pytest.mark.parametrize("policy", ["uniform", "masked"])
+def test_core_vs_reference_levels(hostcheck, level, policy):
+    """F6: the product core's level loader + physics vs the reference on other levels."""
+    d = golden("traj_level_%s_%s.npz" % (level, policy))
+    n, t1 = d["valid"].shape
+    o = hc_run(hostcheck, int(d["seed_base"]), 0, n, t1 - 1, int(d["action_seed"]),
+               int(d["masked"]), bool(d["autoreset"]), level_dir=os.path.join(LEVELS, level))
+    g = {k: d[k] for k in ("obs", "final_obs", "reward", "valid", "done")}
+    assert_same(o, g, keys=list(g))
+    np.testing.assert_array_equal(o["draws"], d["draws"][:, -1])

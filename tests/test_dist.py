@@ -76,3 +76,153 @@ def test_gather_episodes_gloo(world):
     gathered = [v for _, v in res if isinstance(v, list)]
     assert len(gathered) == world and all(g == expect for g in gathered)
     assert all(v == 0 for _, v in res if isinstance(v, int))
+
+
+# ---- the bench's gather (dist.gather_padded + EpisodeLog), the exact functions bench.py runs --
+def _oracle_episodes(n, steps, a0):
+    """(env, return, length) of every episode of n envs (masked policy, auto-reset) from the
+    oracle's trajectories, in step order."""
+    import oracle as O
+    O.build()
+    r = O.run(0, 0, n, steps, a0, 1, True)
+    recs = []
+    for t in range(1, steps + 1):
+        for i in np.flatnonzero(r["done"][:, t]):
+            recs.append((t, int(i)))
+    # returns/lengths since the previous done of the same env
+    out = []
+    last = {}
+    for t, i in recs:
+        t0 = last.get(i, 0)
+        out.append((t, i, int(r["reward"][i, t0 + 1:t + 1].sum()), t - t0))
+        last[i] = t
+    return out
+
+
+def _gather_worker(rank, world, port, recs, cap, drains, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gym_treasure_game_amd.dist as D
+        log = D.EpisodeLog(drains, world, cap, torch.device("cpu"), keep=(rank == 0))
+        all_rows = torch.empty((world * cap, 2), dtype=torch.int64)
+        all_cnt = torch.empty(world, dtype=torch.int32)
+        for d in range(drains):  # this rank's records of drain interval d, padded to cap
+            mine = [x for x in recs if x[0] == d]
+            rows = torch.zeros((cap, 2), dtype=torch.int64)
+            for k, (_, env, ret, ln) in enumerate(mine):
+                rows[k, 0] = env
+                rows[k, 1] = (ret & 0xFFFFFFFF) | (ln << 32)
+            cnt = torch.tensor([len(mine)], dtype=torch.int32)
+            ar, ac = D.gather_padded(rows, cnt, all_rows if world > 1 else None,
+                                     all_cnt if world > 1 else None)
+            log.add(ar, ac)
+        q.put((rank, log.digest()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_gather(world, per_rank, cap, drains):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, per_rank[r], cap, drains, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_bench_gather_digest_independent_of_world(world):
+    """The bench's drain + gather path (gather_padded into EpisodeLog on rank 0) over gloo with
+    uneven per-rank counts: rank 0 receives every record, and the (records, digest) pair is
+    the same for every world size and equal to the digest of the oracle's episode list."""
+    import gym_treasure_game_amd.dist as D
+    n, steps, G = 192, 1200, 100
+    eps = _oracle_episodes(n, steps, 0x51)
+    assert len(eps) > 40
+    want = D.records_digest([e[1] for e in eps], [e[2] for e in eps], [e[3] for e in eps])
+    assert want[0] == len(eps)
+    drains = steps // G
+    cap = max(8, max(sum(1 for e in eps if (e[0] - 1) // G == d) for d in range(drains)))
+    per_rank = [[] for _ in range(world)]
+    for t, i, ret, ln in eps:
+        r = next(r for r in range(world) if D.shard(n, r, world)[0] <= i <
+                 sum(D.shard(n, r, world)))
+        per_rank[r].append(((t - 1) // G, i, ret, ln))
+    if world > 1:
+        assert len({len(p) for p in per_rank}) > 1  # uneven counts per rank
+    res = _run_gather(world, per_rank, cap, drains)
+    assert res[0] == want
+    # a record's digest term depends on (env, return, length) only
+    assert D.records_digest([1], [-5], [3]) != D.records_digest([1], [-5], [4])
+
+
+def test_episode_digest_checks_counts():
+    import gym_treasure_game_amd.dist as D
+    rows = torch.zeros((8, 2), dtype=torch.int64)
+    with pytest.raises(ValueError):
+        D.episode_digest(rows, torch.tensor([9]), 8)
+    assert D.episode_digest(rows, torch.tensor([0]), 8) == (0, 0)
+
+
+HELPER = r'''
+import os, sys, time
+r = int(os.environ["RANK"])
+with open(os.path.join(sys.argv[1], "rank%d.txt" % r), "w") as f:
+    f.write(" ".join(os.environ[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                               "MASTER_PORT")) + " " + " ".join(sys.argv[2:]))
+mode = sys.argv[2]
+if mode == "fail" and r == 1:
+    sys.exit(3)
+if mode == "fail":
+    time.sleep(120)
+sys.exit(0 if r == 0 else 0)
+'''
+
+
+def test_spawn_ranks_env_plumbing(tmp_path):
+    """bench.py --gpus N without a launcher: dist.spawn_ranks starts N fresh processes with the
+    torch.distributed.run environment and returns rank 0's code; a failing rank ends them all."""
+    import gym_treasure_game_amd.dist as D
+    helper = tmp_path / "helper.py"
+    helper.write_text(HELPER)
+    assert D.spawn_ranks(3, [str(tmp_path), "ok", "--x"], script=str(helper)) == 0
+    seen = [open(tmp_path / ("rank%d.txt" % r)).read().split() for r in range(3)]
+    assert [s[0] for s in seen] == ["0", "1", "2"] and [s[1] for s in seen] == ["0", "1", "2"]
+    assert all(s[2] == "3" and s[3] == "127.0.0.1" for s in seen)
+    assert len({s[4] for s in seen}) == 1 and all(s[5:] == ["ok", "--x"] for s in seen)
+    import time
+    t0 = time.time()
+    assert D.spawn_ranks(2, [str(tmp_path), "fail"], script=str(helper)) == 3
+    assert time.time() - t0 < 60
+
+
+def test_bench_spawns_its_ranks():
+    """bench.py --gpus 2 with no WORLD_SIZE goes through dist.spawn_ranks before any GPU call
+    (here each rank fails without a GPU; the parent reports the failure)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["HIP_VISIBLE_DEVICES"] = ""
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
+                        "1"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert "--gpus 2 but" not in p.stderr and "Traceback" in p.stderr

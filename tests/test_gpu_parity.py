@@ -386,3 +386,129 @@ def test_rollout_equals_step_loop_and_oracle(tg, oracle, mode, policy):
     assert r0["reward"].shape == (0, n)
     a.close()
     b.close()
+
+
+LEVELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels")
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("level", ["corridor", "gen1", "gen2", "gen3", "exit"])
+@pytest.mark.parametrize("policy", ["uniform", "masked"])
+def test_reference_levels(tg, level, policy, mode):
+    """F6: the kernels on other levels vs the REFERENCE's trajectories on them (the reference
+    constructor pointed at tests/golden/levels/<level>, tests/golden/make_golden.py)."""
+    d = golden("traj_level_%s_%s.npz" % (level, policy))
+    n, t1 = d["valid"].shape
+    o = run_gpu(tg, int(d["seed_base"]), 0, n, t1 - 1, int(d["action_seed"]), int(d["masked"]),
+                bool(d["autoreset"]), mode=mode, level_dir=os.path.join(LEVELS, level))
+    for k in ("obs", "final_obs", "reward", "valid", "done"):
+        assert_bits(o[k], d[k], k)
+    assert o["stats"]["draws"] == int((d["draws"][:, -1] - 8).sum())
+    assert o["errors"] == 0
+
+
+@pytest.mark.parametrize("level", [None, "corridor", "gen1", "exit"])
+def test_device_predicates(tg, oracle, level):
+    """The six predicates as the DEVICE computes them (mul24 / div48 take their __umul24 path
+    only in the device build) at every pixel of the F2 box, all 8 door states, vs the oracle's
+    pixel loops; the default level's all-open / all-closed tables vs the reference (F2)."""
+    d = golden("predicates.npz")
+    x0, x1, y0, y1 = (int(v) for v in d["box"])
+    ld = os.path.join(LEVELS, level) if level else None
+    vec = tg.TreasureGameVec(1, seed=0, level_dir=ld)
+    e = oracle.OracleEnv(0, level_dir=ld)
+    for db in range(8):
+        got = vec.predicate_table(x0, x1, y0, y1, db).cpu().numpy()
+        np.testing.assert_array_equal(got, e.predicate_table(x0, x1, y0, y1, db), err_msg=str(db))
+        if level is None and db in (0, 7):
+            np.testing.assert_array_equal(got, d["table"][0 if db == 0 else 1])
+    vec.close()
+
+
+def test_all_golden_resets(tg):
+    """F5: all 10,000 construct + reset states (seeds 0..9999) on the device, bit for bit
+    (gauss's log/cos/sin: OCML here, glibc in the reference)."""
+    d = golden("resets.npz")
+    n = len(d["obs"])
+    vec = tg.TreasureGameVec(n, seed=0)
+    obs = vec.reset().cpu().numpy()
+    assert_bits(obs, d["obs"], "reset obs")
+    np.testing.assert_array_equal(vec.read_state()["pos"], d["pos"])
+    assert vec.errors() == 0
+    vec.close()
+
+
+def test_episode_queue_full_without_drain(tg, oracle):
+    """An undrained queue never overflows: records beyond its capacity are dropped and
+    counted, the count stays at the capacity, the kept records are real episodes."""
+    n, steps, a0, cap = 256, 1500, 0x77, 16
+    vec = tg.TreasureGameVec(n, seed=0, autoreset=True)
+    vec.set_episode_capacity(cap)
+    vec.reset()
+    for t in range(steps):
+        vec.step(vec.policy_actions(t, a0, "masked"))
+    st = vec.stats()
+    assert st["episodes"] > cap
+    assert st["episodes_dropped"] == st["episodes"] - cap
+    eps = vec.episodes().cpu().numpy()
+    assert len(eps) == cap
+    assert len(vec.episodes()) == 0
+    r = oracle.run(0, 0, n, steps, a0, 1, True)
+    exp = set()
+    for i in range(n):
+        ret = ln = 0
+        for t in range(1, steps + 1):
+            ret += int(r["reward"][i, t])
+            ln += 1
+            if r["done"][i, t]:
+                exp.add((i, ret, ln))
+                ret = ln = 0
+    assert set(map(tuple, eps.tolist())) <= exp
+    with pytest.raises(ValueError):
+        vec.drain_episodes(torch.empty((4, 2), dtype=torch.int32, device=vec.device),
+                           torch.zeros(1, dtype=torch.int32, device=vec.device))
+    with pytest.raises(ValueError):
+        vec.drain_episodes(torch.empty((4, 2), dtype=torch.int64, device=vec.device),
+                           torch.zeros(1, dtype=torch.int64, device=vec.device))
+    with pytest.raises(tg.TgError):
+        vec.set_episode_capacity(0)
+    vec.close()
+
+
+def test_checkpoint_full_size_round_trip(tg):
+    """read_state(mt=True) at config C3 (1,048,576 envs): the MT generations are gathered on
+    the device (no per-env copies); save -> load into another batch -> identical state and
+    identical next steps."""
+    import time
+    n = 1 << 20
+    a = tg.TreasureGameVec(n, seed=0, autoreset=True)
+    a.reset()
+    for t in range(3):
+        a.step(a.policy_actions(t, 0x31, "masked"))
+    t0 = time.time()
+    snap = a.read_state(mt=True)
+    dt = time.time() - t0
+    assert dt < 30, dt
+    b = tg.TreasureGameVec(n, seed=12345, autoreset=True)
+    b.write_state(snap)
+    sb = b.read_state(mt=True)
+    for k in snap:
+        assert np.array_equal(snap[k], sb[k]), k
+    for t in range(3, 5):
+        oa = a.step(a.policy_actions(t, 0x31, "masked"))[0].clone()
+        ob = b.step(b.policy_actions(t, 0x31, "masked"))[0]
+        assert torch.equal(oa.view(torch.int64), ob.view(torch.int64))
+    a.close()
+    b.close()
+
+
+def test_seed_limits(tg):
+    with pytest.raises(ValueError):
+        tg.TreasureGameVec(4, seed=-1)
+    with pytest.raises(ValueError):
+        tg.TreasureGameVec(4, seed=2**64 - 2)
+    env = tg.TreasureGame(seed=-7)  # random.seed(-7) == random.seed(7)
+    ref = tg.TreasureGame(seed=7)
+    assert env.reset() == ref.reset()
+    env.close()
+    ref.close()
