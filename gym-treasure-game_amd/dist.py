@@ -122,8 +122,9 @@ class EpisodeLog:
         self.records.add_(all_count.sum())
         if not self.keep:
             return
-        if self.used >= self.rows.size(0):
-            raise RuntimeError("EpisodeLog: more drains than allocated")
+        if self.used >= self.rows.size(0):  # more drains than sized for: grow (allocates)
+            self.rows = torch.cat([self.rows, torch.zeros_like(self.rows)])
+            self.counts = torch.cat([self.counts, torch.zeros_like(self.counts)])
         self.rows[self.used].copy_(all_rows, non_blocking=True)
         self.counts[self.used].copy_(all_count, non_blocking=True)
         self.used += 1
