@@ -9,8 +9,8 @@ there is no CPU fallback.  Registration with gym / gymnasium happens on import w
 installed, mirroring gym_treasure_game/__init__.py:3-6.
 """
 from ._lib import TgError  # noqa: F401
-from .envs import (OPTION_NAMES, STATE_NAMES, ObservationWrapper, TreasureGame,  # noqa: F401
-                   TreasureGameVec, read_level)
+from .envs import (OPTION_NAMES, STATE_NAMES, GpuOption, ObservationWrapper,  # noqa: F401
+                   TreasureGame, TreasureGameVec, TreasureGameVectorEnv, make_vec, read_level)
 from .render import load_sprites, synthetic_sprites  # noqa: F401
 
 __version__ = "0.1.0"

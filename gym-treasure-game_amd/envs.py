@@ -30,8 +30,8 @@ LEVEL_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "levels", "
 def _spaces():
     for mod in ("gym.spaces", "gymnasium.spaces"):
         try:
-            m = __import__(mod, fromlist=["Discrete", "Box"])
-            return m.Discrete, m.Box
+            m = __import__(mod, fromlist=["Discrete", "Box", "MultiDiscrete"])
+            return m.Discrete, m.Box, m.MultiDiscrete
         except Exception:  # noqa: BLE001 — absent or broken install: use the stand-ins
             continue
 
@@ -70,10 +70,26 @@ def _spaces():
         def __repr__(self):
             return "Box(%s, %s, %s, %s)" % (self.low.min(), self.high.max(), self.shape, self.dtype)
 
-    return Discrete, Box
+    class MultiDiscrete:
+        def __init__(self, nvec):
+            self.nvec = np.asarray(nvec, np.int64)
+            self.shape = self.nvec.shape
+            self.dtype = np.int64
+
+        def sample(self):
+            return (np.random.random_sample(self.shape) * self.nvec).astype(np.int64)
+
+        def contains(self, x):
+            x = np.asarray(x)
+            return x.shape == self.shape and bool(np.all((x >= 0) & (x < self.nvec)))
+
+        def __repr__(self):
+            return "MultiDiscrete(%s)" % (self.nvec,)
+
+    return Discrete, Box, MultiDiscrete
 
 
-Discrete, Box = _spaces()
+Discrete, Box, MultiDiscrete = _spaces()
 
 
 def read_level(path=LEVEL_DIR):
@@ -390,6 +406,35 @@ class TreasureGameVec:
             self.write_state({k: z[k] for k in z.files})
 
 
+class GpuOption:
+    """One entry of ``TreasureGame.option_list``: the reference's option object
+    (``_Option`` / ``*_option``, _option.py:8-36, _move_options.py; create_options,
+    _treasure_game_impl.py:484-498) for an env that lives on the GPU.
+
+    ``can_run()`` is the device's ``can_run`` of this option for the env's current state, and
+    ``run()`` runs it to completion on the device, exactly as ``TreasureGame.step(k)`` does
+    (``option_list[k].run()``, TG/:91-96): it returns the summed tick rewards, or ``None``
+    when the option cannot run (OP/:20-23).  ``done`` is True after a run, as in the reference.
+    The per-tick ``policy_step`` is not exposed: the option's loop runs inside one kernel."""
+
+    def __init__(self, env, k):
+        self._env = env
+        self.index = k
+        self.name = OPTION_NAMES[k]
+        self.done = False
+
+    def can_run(self):
+        return bool(self._env._mask_bits() >> self.index & 1)
+
+    def run(self):
+        r = self._env._run(self.index)[1]
+        self.done = r is not None or self.done
+        return r
+
+    def __repr__(self):
+        return "<%s (GPU)>" % self.name
+
+
 class TreasureGame:
     """Drop-in for the reference ``TreasureGame`` (treasure_game.py:54-114), one env on the GPU.
 
@@ -414,7 +459,7 @@ class TreasureGame:
         if seed >= 2**64:
             raise ValueError("seed must satisfy |seed| < 2**64 (a two-word init_by_array key)")
         self._vec = TreasureGameVec(1, seed=seed, device=device, level_dir=level_dir)
-        self.option_list = list(range(_lib.NUM_ACTIONS))
+        self.option_list = [GpuOption(self, k) for k in range(_lib.NUM_ACTIONS)]
         self.option_names = list(OPTION_NAMES)
         self.action_space = Discrete(_lib.NUM_ACTIONS)
         self.observation_space = Box(np.float32(0.0), np.float32(1.0), shape=(_lib.OBS_DIM,))
@@ -424,22 +469,30 @@ class TreasureGame:
     def reset(self):
         return self._vec.reset().cpu().numpy()[0].tolist()
 
+    def _mask_bits(self):
+        return int(self._vec.available_mask().cpu().item()) & 0x1FF
+
     @property
     def available_mask(self):
-        m = int(self._vec.available_mask().cpu().item()) & 0x1FF
+        m = self._mask_bits()
         return np.array([(m >> k) & 1 for k in range(_lib.NUM_ACTIONS)])
 
-    def step(self, action):
-        a = operator.index(action)  # list indexing accepts ints only (TG/:92)
-        if not -_lib.NUM_ACTIONS <= a < _lib.NUM_ACTIONS:
-            raise IndexError("list index out of range")
+    def _run(self, a):
+        """option_list[a].run() on the device + get_state + done (TG/:91-96)"""
         self._act.fill_(a)
         obs, rew, valid, done, _ = self._vec.step(self._act)
         packed = torch.cat([obs[0], rew.to(torch.float64), valid.to(torch.float64),
                             done.to(torch.float64)]).cpu().numpy()
         state = packed[:9].tolist()
         r = int(packed[9]) if packed[10] else None
-        return state, r, bool(packed[11]), {}
+        return state, r, bool(packed[11])
+
+    def step(self, action):
+        a = operator.index(action)  # list indexing accepts ints only (TG/:92)
+        if not -_lib.NUM_ACTIONS <= a < _lib.NUM_ACTIONS:
+            raise IndexError("list index out of range")
+        state, r, done = self._run(a)
+        return state, r, done, {}
 
     def render(self, mode="human"):
         if mode != "rgb_array":
@@ -495,3 +548,82 @@ class ObservationWrapper:
         info = out[-1]
         info["world_state"] = out[0]
         return (self._screen(),) + tuple(out[1:])
+
+
+class TreasureGameVectorEnv:
+    """Gymnasium-style vector env over one ``TreasureGameVec``: the batch steps
+    on the device and every output is a device tensor.
+
+    ``reset(seed=None) -> (obs f64 [N, 9], info)``; ``step(actions) -> (obs, reward f32 [N],
+    terminated bool [N], truncated bool [N], info)``.  Auto-reset is same-step
+    (``metadata["autoreset_mode"] == "SameStep"``): an env that terminates (TG/:95: gold held
+    and back in row 0) or is truncated is reset inside the same call, ``obs`` holds its new
+    episode's first observation and ``info["final_obs"]`` the last one of the finished
+    episode (== ``obs`` for the others).  The reference's ``None`` reward (option could not run,
+    OP/:22-23) is reward 0 with ``info["valid"] == 0``.  ``truncated`` is set only when
+    ``max_episode_steps`` is given (the reference registers no TimeLimit); those envs are reset
+    by a masked ``tg_reset`` on the device, with no host synchronisation.
+    Env g of ``reset(seed=s)`` is ``random.seed(s + g); TreasureGame()`` (contract of
+    TreasureGameVec)."""
+
+    metadata = {"autoreset_mode": "SameStep", "render_modes": ["rgb_array"]}
+
+    def __init__(self, num_envs, seed=0, device=None, max_episode_steps=None, level_dir=None,
+                 mode="compact"):
+        self.num_envs = int(num_envs)
+        self._kw = dict(device=device, level_dir=level_dir, mode=mode)
+        self.max_episode_steps = None if max_episode_steps is None else int(max_episode_steps)
+        self.single_action_space = Discrete(_lib.NUM_ACTIONS)
+        self.single_observation_space = Box(np.float32(0.0), np.float32(1.0),
+                                            shape=(_lib.OBS_DIM,))
+        self.action_space = MultiDiscrete([_lib.NUM_ACTIONS] * self.num_envs)
+        self.observation_space = Box(np.float32(0.0), np.float32(1.0),
+                                     shape=(self.num_envs, _lib.OBS_DIM))
+        self._make(seed)
+
+    def _make(self, seed):
+        old = getattr(self, "env", None)
+        if old is not None:
+            old.close()
+        self.env = TreasureGameVec(self.num_envs, seed=seed, autoreset=True, **self._kw)
+        self.device = self.env.device
+        self._len = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+
+    def reset(self, seed=None, options=None):
+        if seed is not None:
+            self._make(int(seed))
+        obs = self.env.reset()
+        self._len.zero_()
+        return obs, {}
+
+    def step(self, actions):
+        obs, rew, valid, done, info = self.env.step(actions)
+        final = info["final_obs"]
+        terminated = done.bool()
+        self._len += 1
+        self._len.masked_fill_(terminated, 0)
+        if self.max_episode_steps is not None:
+            truncated = self._len >= self.max_episode_steps
+            self._len.masked_fill_(truncated, 0)
+            obs = self.env.reset(truncated.to(torch.uint8))  # masked reset, obs of every env
+        else:
+            truncated = torch.zeros_like(terminated)
+        return obs, rew.to(torch.float32), terminated, truncated, {"final_obs": final,
+                                                                   "valid": valid}
+
+    def available_mask(self):
+        return self.env.available_mask()
+
+    def episodes(self, cap=None):
+        """(env, return, length) of the terminated episodes (device queue, TreasureGameVec)"""
+        return self.env.episodes(cap)
+
+    def close(self):
+        self.env.close()
+
+
+def make_vec(id="treasure_game-v0", num_envs=1, **kwargs):
+    """gymnasium.make_vec stand-in: a TreasureGameVectorEnv of ``num_envs`` envs."""
+    if id != "treasure_game-v0":
+        raise KeyError("unknown env id %r" % (id,))
+    return TreasureGameVectorEnv(num_envs, **kwargs)

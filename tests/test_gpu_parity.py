@@ -512,3 +512,60 @@ def test_seed_limits(tg):
     assert env.reset() == ref.reset()
     env.close()
     ref.close()
+
+
+def test_option_objects_drive_the_gpu_env(tg, oracle):
+    """TreasureGame.option_list holds option objects (create_options, IM/:484-498): can_run()
+    and run() (-> int | None, OP/:20-36) drive the device env like the reference's demo loop
+    (IM/:515-518); the env's state then equals the oracle's."""
+    env = tg.TreasureGame(seed=11)
+    ref = oracle.OracleEnv(11)
+    env.reset()
+    assert [o.name for o in env.option_list] == tg.OPTION_NAMES
+    for t in range(150):
+        can = [o.can_run() for o in env.option_list]
+        assert can == [bool(ref.mask() >> k & 1) for k in range(9)]
+        a = oracle.pick_action(0xAB, 11, t, t % 3 != 0, ref.mask())
+        r = env.option_list[a].run()
+        _, rr, _, _ = ref.step(a)
+        assert r == rr
+        got = env._vec.observe().cpu().numpy()[0]
+        np.testing.assert_array_equal(got.view(np.uint64), ref.obs.view(np.uint64))
+    env.close()
+
+
+def test_vector_env_gymnasium_surface(tg, oracle):
+    """TreasureGameVectorEnv: (obs, reward, terminated, truncated, info) with same-step
+    auto-reset and a TimeLimit, vs the oracle driven the same way (reset after done or after
+    max_episode_steps steps of an episode)."""
+    n, steps, a0, tmax = 48, 400, 0x3C, 60
+    ve = tg.make_vec("treasure_game-v0", num_envs=n, seed=5, max_episode_steps=tmax)
+    assert ve.single_action_space.n == 9 and ve.single_observation_space.shape == (9,)
+    assert ve.observation_space.shape == (n, 9)
+    obs, info = ve.reset()
+    envs = [oracle.OracleEnv(5 + g) for g in range(n)]
+    lens = [0] * n
+    np.testing.assert_array_equal(obs.cpu().numpy().view(np.uint64),
+                                  np.stack([e.obs for e in envs]).view(np.uint64))
+    n_term = n_trunc = 0
+    for t in range(steps):
+        acts = [oracle.pick_action(a0, g, t, True, envs[g].mask()) for g in range(n)]
+        obs, rew, term, trunc, info = ve.step(torch.tensor(acts, dtype=torch.int32,
+                                                           device=ve.device))
+        obs, rew, term, trunc = (x.cpu().numpy() for x in (obs, rew, term, trunc))
+        fin, val = info["final_obs"].cpu().numpy(), info["valid"].cpu().numpy()
+        for g, e in enumerate(envs):
+            o, r, d, _ = e.step(acts[g])
+            lens[g] += 1
+            np.testing.assert_array_equal(fin[g].view(np.uint64), o.view(np.uint64))
+            assert (rew[g], bool(val[g]), bool(term[g])) == (float(r or 0), r is not None, d)
+            tr = (not d) and lens[g] >= tmax
+            assert bool(trunc[g]) == tr
+            if d or tr:
+                o = e.reset()
+                lens[g] = 0
+            np.testing.assert_array_equal(obs[g].view(np.uint64), o.view(np.uint64))
+        n_term += int(term.sum())
+        n_trunc += int(trunc.sum())
+    assert n_trunc > 0
+    ve.close()
