@@ -33,9 +33,6 @@ using namespace tg;
 namespace {
 
 constexpr int BLOCK = 256;
-#ifndef TG_RING_SLOTS
-#define TG_RING_SLOTS 4
-#endif
 
 // ------------------------------------------------------------------------------------------
 // SoA pack / unpack
@@ -93,52 +90,42 @@ __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o
 
 // ------------------------------------------------------------------------------------------
 // CPython random for the option loops (k_run, k_step): tg::Rng's read-only consumption of the
-// two pre-twisted generations, with a 16-B chunk window in LDS.
-//   Each wave owns a ring [slot R][lane 64] x 16 B.  Chunk c (words 4c..4c+3, 312 chunks over
-//   both halves) sits in slot c % R (312 % R == 0, so the ring survives the wrap).  A lane
-//   reading chunk c holds chunks c .. c+R-2; at its first draw in chunk c (o = 0) it fetches
-//   chunk c+R-1 into the slot of chunk c-1 with global_load_lds_dwordx4 (LDS-DMA: no VGPR
-//   destination).
-//   Why not a register window: one that rotates (c0 = c1; c1 = c2; c2 = load) makes the
-//   compiler copy the freshly loaded chunk at once, i.e. wait for the load it has just issued
-//   (ISA: s_waitcnt vmcnt(1)/(0) after each prefetch), so every shift paid a full HBM
-//   latency.  The DMAs are issued from inline asm, invisible to the compiler's waitcnt pass,
-//   and ordered by hand:
-//   * RAW: "s_waitcnt vmcnt(R-2)" before each draw's LDS read.  Chunk c was fetched at the
-//     first draw of chunk c-R+1 (or in prime(), before chunks c+1..); the lane's fetches at
-//     chunks c-R+2 .. c-1 (R-2 DMAs) were issued after it, and vmcnt counts every VMEM op of
-//     the wave in issue order (MI355X_MICROARCH.md §vmcnt), so "all but the R-2 youngest
-//     done" covers chunk c.
-//   * WAR: a DMA never targets a slot read in the same draw: chunk c-1's slot was last read a
-//     draw earlier, and "s_waitcnt lgkmcnt(0)" before the DMA retires that read (a DMA that
-//     hits in L1 lands in ~150 cycles, possibly before a queued ds_read executes).
+// two pre-twisted generations, reading each draw's code byte (tg_core.h draw_code: its noisy /
+// jump / flip outcomes) from a per-lane window in LDS.
+//   Window: WIN_CHUNKS 16-B chunks (16 codes each) per lane, slot j of the wave's window at
+//   m0 + j * 1 KB holding the lane's j-th chunk from where the window starts.  prime() fills
+//   it with one LDS-DMA (global_load_lds_dwordx4) per slot: every lane's chunk j goes to slot
+//   j, so M0 (which addresses the DMA's LDS destination and must be wave-uniform) is the same
+//   for all of them and each slot costs ONE instruction.  The first draw waits for the DMAs
+//   (s_waitcnt vmcnt(0), once per launch; k_run primes before the option's setup so the wait
+//   is mostly covered); every later draw is an LDS byte read, issued one draw ahead.  The
+//   window holds 112 draws, more than an option of the default level consumes in one step
+//   (<= ~110); a lane that exhausts it refills it the same way (WAR: lgkmcnt(0) before the
+//   DMAs; RAW: vmcnt(0) after) and pays one memory latency.  The DMAs are issued from inline
+//   asm, invisible to the compiler's waitcnt pass, so no register copy of a loaded value is
+//   waited for early (a register-held prefetch made the compiler wait at the load).
+//   Position bookkeeping is deferred: the window start (pos) plus the draws taken since (n)
+//   are folded into pos at a refill and at finish.
+//   Stale halves: a window overlapping the half the lane is not in, while that half is stale
+//   (crossed), is loaded only after the lane has regenerated that half itself (regen_half:
+//   rare, > 312 draws since the refill; the refilling idle wave, if any, writes the same).
+//   Draws that need the double (handle angles in a flip cascade, an auto-reset's uniform and
+//   gauss) consume the code and read the position's two words (one 8-B load).
 // ------------------------------------------------------------------------------------------
-constexpr int RING_SLOTS = TG_RING_SLOTS;
-constexpr int RING_SLOT_BYTES = 64 * 16;
-constexpr int RING_WAVE_BYTES = RING_SLOTS * RING_SLOT_BYTES;
-constexpr uint32_t MT_CHUNKS = MT_WORDS / 4;  // 312
-static_assert(MT_CHUNKS % RING_SLOTS == 0, "ring slot of a chunk must survive the wrap");
-static_assert(RING_SLOTS >= 3, "prefetch distance");
-static_assert(RING_WAVE_BYTES >= MT_N * 4, "wave_refill reuses the ring as scratch");
+constexpr uint32_t CODE_CHUNKS = MT_CODES / 16;  // 39
+static_assert(MT_CODES % 16 == 0, "whole 16-B code chunks per env");
+constexpr int WIN_CHUNKS = 7;
+constexpr int WIN_SLOT_BYTES = 64 * 16;
+constexpr int WIN_WAVE_BYTES = WIN_CHUNKS * WIN_SLOT_BYTES;  // 7 KB per wave
+constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
+static_assert(WIN_WAVE_BYTES >= WAVE_SCRATCH, "wave_refill reuses the window as scratch");
 
 typedef __attribute__((address_space(1))) uint32_t glb_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) u32x2 lds_u2;
 
 // LDS-DMA of one 16-B chunk per active lane into LDS [m0 + lane * 16]; M0 is saved/restored
-__device__ __forceinline__ void glds16(uint32_t m0, const uint32_t* gptr) {
-#ifdef TG_GLDS_NOSAVE
-  asm volatile(
-      "s_mov_b32 m0, %0\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off"
-      :
-      : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
-      : "memory");
-  return;
-#endif
+__device__ __forceinline__ void glds16(uint32_t m0, const void* gptr) {
   uint32_t save;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -150,134 +137,139 @@ __device__ __forceinline__ void glds16(uint32_t m0, const uint32_t* gptr) {
       : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
       : "memory");
 }
-// chunk -> its slot of the wave's ring; M0 must be wave-uniform, so one DMA per slot value
-template <int J = 0>
-__device__ __forceinline__ void ring_fetch(uint32_t m0_slot0, uint32_t slot, const uint32_t* g) {
-#ifdef TG_DIAG_ONEVAR  // DIAGNOSTIC ONLY: one DMA for every lane, wrong slots (prices the variants)
-  glds16(m0_slot0, g);
-  return;
-#endif
-  if constexpr (J < RING_SLOTS) {
-    if (slot == (uint32_t)J) glds16(m0_slot0 + J * RING_SLOT_BYTES, g);
-    else ring_fetch<J + 1>(m0_slot0, slot, g);
-  }
-}
 
-// the rare second crossing (RngRing::fetch), out of line so that the draw sites stay small
-__device__ __noinline__ void regen_half(uint32_t* mt, double* md, uint32_t h) {
+// the rare second crossing (RngCodes::fill), out of line so that the draw sites stay small
+__device__ __noinline__ void regen_half(uint32_t* mt, uint8_t* mc, uint32_t h) {
   twist_gen(mt + (MT_N - h), mt + h);
-  gen_doubles(mt + h, md + h / 2);
+  gen_codes(mt + h, mc + h / 2);
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
 }
 
-struct RngRing {
-  uint32_t* mt;    // this env's MT_WORDS words (HBM; only to regenerate a stale half)
-  double* md;      // this env's MT_DOUBLES (HBM): what the ring streams
-  lds_u8* cell;    // this lane's 16-B cell in slot 0 of the wave's ring
-  uint32_t m0;     // LDS address of slot 0 of the wave's ring (wave-uniform)
-  uint32_t pos;    // [0, MT_WORDS), even: the next draw is double pos / 2
-  uint32_t rot;    // slot of chunk c = (c - rot) % R (set by prime, see slot_of)
-  uint32_t ph;     // the draws that fetch: o == ph, the first draw's o (0 or 2; prime)
+struct RngCodes {
+  static constexpr uint32_t NONE = 0xFFFFFFFFu;
+  uint32_t* mt;      // this env's MT_WORDS words (HBM)
+  uint8_t* mc;       // this env's MT_CODES code bytes (HBM)
+  lds_u8* cell;      // this lane's 16-B cell in slot 0 of the wave's window
+  uint32_t m0;       // LDS address of slot 0 of the wave's window (wave-uniform)
+  uint32_t pos;      // word position of the window's first draw (even)
+  uint32_t n;        // draws taken since then
+  uint32_t rd;       // LDS offset of the next draw's code from cell: slot * 1 KB + byte
+  uint32_t left;     // draws left in the window
+  uint32_t nxc;      // the next draw's code (read one draw ahead)
+  uint32_t stale;    // word offset (0 / 624) of the half that is two generations behind, or NONE
   uint32_t draws;
-  double nx;       // the next draw, read from the ring one draw ahead
-  bool primed, loaded, crossed, entered;  // crossed / entered: as tg::Rng
+  uint32_t regens;   // halves this lane regenerated itself (regen_half)
+  bool primed, loaded, entered;  // entered: a half was entered in this launch (as tg::Rng)
 
-  __device__ __forceinline__ RngRing(uint32_t* m, double* d, uint32_t state, lds_u8* wave_ring)
-      : mt(m), md(d), cell(wave_ring + (threadIdx.x & 63) * 16),
-        m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_ring)),
-        pos(state & MT_POS_MASK), rot(0u), ph(0u), draws(0u), nx(0.0), primed(false), loaded(false),
-        crossed((state & MT_STALE) != 0u), entered(false) {}
+  __device__ __forceinline__ RngCodes(uint32_t* m, uint8_t* c, uint32_t state, lds_u8* wave_win)
+      : mt(m), mc(c), cell(wave_win + (threadIdx.x & 63) * 16),
+        m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_win)),
+        pos(state & MT_POS_MASK), n(0u), rd(0u), left(0u), nxc(0u),
+        stale((state & MT_STALE) ? (uint32_t)MT_N - mt_half(state & MT_POS_MASK) : NONE),
+        draws(0u), regens(0u), primed(false), loaded(false), entered(false) {}
 
-  __device__ __forceinline__ void fetch(uint32_t c) {
-    if (c >= MT_CHUNKS) c -= MT_CHUNKS;
-    const uint32_t other = (uint32_t)MT_N - mt_half(pos);
-    if (crossed && c * 4u == other) {
-      // the first chunk of the other half while it is stale (left in this launch, or not yet
-      // refilled since an earlier one): regenerate it from the half the lane is in before
-      // any of its chunks is fetched (per lane, rare)
-      regen_half(mt, md, other);
+  // fold the draws taken since the window start into pos (a window is < 312 draws, so at
+  // most one half boundary lies in between).  Entering a half that is stale (possible only
+  // when the window ended exactly at the boundary, so nothing of it was read) regenerates it
+  // first, from the half being left, which then becomes the stale one.
+  __device__ __forceinline__ void sync() {
+    const uint32_t d = pos >> 1, e = d + n;
+    if (e / (MT_N / 2) != d / (MT_N / 2)) {
+      const uint32_t left_half = mt_half(pos), entered_half = (uint32_t)MT_N - left_half;
+      if (stale == entered_half) {
+        regen_half(mt, mc, entered_half);
+        ++regens;
+      }
+      stale = left_half;
+      entered = true;
     }
-    // chunk c = doubles 2c, 2c+1: the same 16 bytes as words 4c..4c+3 of the word array
-    ring_fetch(m0, slot_of(c), reinterpret_cast<const uint32_t*>(md) + c * 4u);
+    pos = 2u * (e >= (uint32_t)MT_N ? e - (uint32_t)MT_N : e);
+    n = 0u;
   }
-  // Slots and fetch draws count from the lane's first draw, not from chunk 0: a lane whose
-  // first draw is at o = 2 fetches at its o = 2 draws (chunk c + R from (c, 2), one draw
-  // before (c + 1, 0) would fetch it: the same ring state), and its slots count from chunk
-  // c + 1.  Lanes that draw in lockstep in a tick loop then fetch on the same iterations
-  // (every other draw, not every draw for half of them) and into the same slot, so ring_fetch
-  // takes one branch (M0 is per slot) instead of up to R.  312 % R == 0 keeps the mapping
-  // across the wrap (chunk c and c + 312 are the same slot).
-  __device__ __forceinline__ uint32_t slot_of(uint32_t c) const {
-    return (c + RING_SLOTS - rot) % RING_SLOTS;
-  }
-  // the double at pos from the ring (its chunk has landed: see the vmcnt argument above)
-  __device__ __forceinline__ double ring_read() const {
-#ifndef TG_DIAG_NOWAIT  // DIAGNOSTIC ONLY when defined: no RAW wait (prices it; results wrong)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING_SLOTS - 2) : "memory");
+  // DMA the window starting at pos (all lanes reaching it start at slot 0: one DMA per slot)
+  __device__ __forceinline__ void fill() {
+    const uint32_t d = pos >> 1, c0 = d >> 4;
+    if (stale != NONE) {
+      // the draws the window serves are words [pos, pos + 2 * left) (mod 1248; the bytes of
+      // its first and last chunks outside that range are never read): regenerate the stale
+      // half first if they overlap it
+      const uint32_t w0 = pos, w1 = pos + 2u * ((uint32_t)WIN_CHUNKS * 16u - (d & 15u));
+      if ((w0 < stale + (uint32_t)MT_N && stale < w1) ||
+          (w1 > (uint32_t)MT_WORDS && stale < w1 - (uint32_t)MT_WORDS)) {
+        regen_half(mt, mc, stale);
+        ++regens;
+        stale = NONE;
+      }
+    }
+#ifndef TG_DIAG_CODEHASH
+#pragma unroll
+    for (int j = 0; j < WIN_CHUNKS; ++j) {
+      const uint32_t c = c0 + j < CODE_CHUNKS ? c0 + j : c0 + j - CODE_CHUNKS;
+      glds16(m0 + j * WIN_SLOT_BYTES, mc + c * 16u);
+    }
 #endif
-    typedef __attribute__((address_space(3))) double lds_f64;
-    return *(const lds_f64*)(cell + slot_of(pos >> 2) * RING_SLOT_BYTES + (pos & 2u) * 4u);
+    rd = d & 15u;
+    left = (uint32_t)WIN_CHUNKS * 16u - rd;
+    loaded = false;
+  }
+  __device__ __forceinline__ uint32_t read() const {
+    const uint32_t r = rd < (uint32_t)WIN_CHUNKS * 16u ? rd : 0u;  // stay inside the window
+    return cell[(r >> 4) * WIN_SLOT_BYTES + (r & 15u)];
   }
   __device__ __forceinline__ void prime() {
-    // chunks c .. c+R-2, and c+R-1 too when the first draw is at o = 2 (its first fetch, at
-    // that draw, is chunk c+R); chunk c-1's slot is free
-    const uint32_t c = pos >> 2;
-#ifdef TG_RING_ABS
-    rot = 0u;
-    ph = 0u;
-#else
-    ph = pos & 2u;
-    rot = (c + (ph >> 1)) % RING_SLOTS;
-#endif
-#pragma unroll
-    for (int j = 0; j < RING_SLOTS - 1; ++j) fetch(c + j);
-    if (pos & 2u) fetch(c + RING_SLOTS - 1);
+    fill();
     primed = true;
   }
-  // random(): returns the value read one draw ago and reads the next one, so the LDS round
-  // trip overlaps the tick in between instead of sitting in the draw's dependency chain
-  __device__ __forceinline__ double random() {
-#ifdef TG_DIAG_NORNG
-    // DIAGNOSTIC BUILD ONLY (scripts/diag_ablation.py): values from a register hash instead
-    // of the MT buffers, to price the RNG's memory path.  Never part of the product library.
-    uint32_t z = (pos * 0x9E3779B9u) ^ (uint32_t)(uintptr_t)mt;
-    pos = (pos + 2 == (uint32_t)MT_WORDS) ? 0u : pos + 2;
-    z ^= z >> 16; z *= 0x85EBCA6Bu; z ^= z >> 13; z *= 0xC2B2AE35u; z ^= z >> 16;
-    ++draws;
-    return (double)(z >> 5) * (1.0 / 134217728.0);
-#endif
+  // at least k draws available in the window (the option loops call it once per tick: a tick
+  // draws at most 6 times; an auto-reset 4); refilling is rare and has one site per loop
+  __device__ __forceinline__ void reserve(uint32_t k) {
     if (!primed) prime();
-    if (!loaded) {  // first draw of the launch: the first chunk's DMA must land first
-      nx = ring_read();
+    if (left < k) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // no read of the old window pending
+      sync();
+      fill();
+    }
+    if (!loaded) {  // the window's DMAs must have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      nxc = read();
       loaded = true;
     }
-    const double v = nx;
-    const uint32_t c = pos >> 2, o = pos & 2u;
-    pos += 2;
-    if (pos == (uint32_t)MT_WORDS) pos = 0u;
-    if (pos == 0u || pos == (uint32_t)MT_N) crossed = entered = true;
+  }
+  // at least k draws staged (no refill: the plain go loop's exit test)
+  __device__ __forceinline__ bool has(uint32_t k) const { return left >= k; }
+  // one draw, consumed for its outcomes (draw_code); reserve() guarantees it is in the window
+  __device__ __forceinline__ uint32_t code() {
+#ifdef TG_DIAG_CODEHASH  // DIAGNOSTIC BUILD ONLY: codes from a register hash (prices the window)
+    uint32_t z = (pos + 2 * n) * 0x9E3779B9u;
+    z ^= z >> 15;
+    ++n; ++draws; --left;
+    return z & 0x3Fu;
+#endif
+    const uint32_t c = nxc;
+    ++n;
     ++draws;
-    // read the next draw BEFORE this draw's fetch: vmcnt counts the wave's VMEM instructions
-    // in issue order, so a wait placed after a fetch would wait for that very fetch
-    nx = ring_read();
-    if (o == ph) {
-      // o = 0: chunk c-1's slot (read draws ago) takes chunk c+R-1; o = 2 (ph = 2): chunk c's
-      // slot (its last value read a draw ago) takes chunk c+R
-      asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");  // all but the read just issued
-      const uint32_t p = pos;
-      pos = c * 4u;  // fetch() tests the half of the chunk being read
-      fetch(c + RING_SLOTS - 1 + (ph >> 1));
-      pos = p;
-    }
-    return v;
+    ++rd;
+    --left;
+    nxc = read();  // the next draw's code, one draw ahead (a byte of the window when left = 0)
+    return c;
+  }
+  // one draw as its double (rare): the code is consumed too, the value built from the words
+  __device__ __forceinline__ double random() {
+    uint32_t p = (pos >> 1) + n;
+    p = 2u * (p >= (uint32_t)MT_N ? p - (uint32_t)MT_N : p);
+    (void)code();
+    const uint2 w = *reinterpret_cast<const uint2*>(mt + p);
+    return mt_double(w.x, w.y);
   }
   __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
-  // drain the DMAs (the ring is reused as scratch); returns the state word to store
+  // drain the DMAs (the window is reused as scratch); returns the state word to store
   __device__ __forceinline__ uint32_t finish() {
     if (primed) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    sync();
     primed = loaded = false;
-    return pos | (crossed ? MT_STALE : 0u);
+    return pos | (stale != NONE ? MT_STALE : 0u);
   }
+  // the same when a refill of the half that was stale on entry is already queued
   __device__ __forceinline__ uint32_t finish_queued() {
     (void)finish();
     return pos | (entered ? MT_STALE : 0u);
@@ -293,8 +285,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
 // coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
 // earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart).  src / dst are
 // wave-uniform; must be reached by all 64 lanes of the wave.
-typedef __attribute__((address_space(1))) double glb_f64;
-__device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, glb_f64* dst_d,
+__device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
                                            lds_u32* scratch) {
   const int lane = threadIdx.x & 63;
   constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
@@ -318,31 +309,33 @@ __device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, glb
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // round r visible to later rounds
   }
-  // the generation's 312 random() values
+  // the generation's 312 draw codes, 4 per lane (one 4-B store each)
 #pragma unroll
-  for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
+  for (int r = 0; r < (MT_N / 8 + 63) / 64; ++r) {
     const int k = r * 64 + lane;
-    if (k < MT_N / 2) {
-      const u32x2 ww = *(const lds_u2*)(scratch + 2 * k);
-      dst_d[k] = mt_double(ww.x, ww.y);
+    if (k < MT_N / 8) {
+      const lds_u32* w = scratch + 8 * k;
+      const uint32_t v = draw_code(mt_double(w[0], w[1])) | draw_code(mt_double(w[2], w[3])) << 8 |
+                         draw_code(mt_double(w[4], w[5])) << 16 | draw_code(mt_double(w[6], w[7])) << 24;
+      reinterpret_cast<uint32_t*>(dst_c)[k] = v;
     }
   }
 }
 // For every lane in `need`: regenerate the stale half of its env (the one not holding the
 // position in its state word), one env at a time.  Must be reached by all 64 lanes.
-__device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* env_mt, double* env_md,
+__device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* env_mt, uint8_t* env_mc,
                                             uint32_t state, lds_u32* scratch) {
   const uint32_t pos = state & MT_POS_MASK;
   const uint32_t dst = MT_N - mt_half(pos);
   const uint64_t src_l = (uint64_t)(uintptr_t)(env_mt + mt_half(pos));
   const uint64_t dst_l = (uint64_t)(uintptr_t)(env_mt + dst);
-  const uint64_t dd_l = (uint64_t)(uintptr_t)(env_md + dst / 2);
+  const uint64_t dc_l = (uint64_t)(uintptr_t)(env_mc + dst / 2);
   while (need) {
     const int L = __ffsll((long long)need) - 1;
     need &= need - 1;
     wave_twist((const glb_u32*)(uintptr_t)readlane64(src_l, L),
                (glb_u32*)(uintptr_t)readlane64(dst_l, L),
-               (glb_f64*)(uintptr_t)readlane64(dd_l, L), scratch);
+               (uint8_t*)(uintptr_t)readlane64(dc_l, L), scratch);
   }
 }
 
@@ -382,23 +375,23 @@ __global__ __launch_bounds__(BLOCK) void k_create(Soa S, int64_t n, uint64_t see
 }
 // one generation for every env: the half at from_pos -> the other half
 __global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t from_pos) {
-  __shared__ uint32_t scratch[BLOCK / 64][MT_N];
+  __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
-  wave_refill(__ballot(live), S.mt + (live ? i : 0) * MT_WORDS, S.mtd + (live ? i : 0) * MT_DOUBLES, from_pos,
+  wave_refill(__ballot(live), S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES, from_pos,
               (lds_u32*)scratch[threadIdx.x >> 6]);
 }
 
-// the random() values of the first half (words [0, 624)) of every env (tg_write_state)
-__global__ __launch_bounds__(BLOCK) void k_gen_doubles(Soa S, int64_t n) {
+// the draw codes of the first half (words [0, 624)) of every env (tg_write_state)
+__global__ __launch_bounds__(BLOCK) void k_gen_codes(Soa S, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  if (i < n) gen_doubles(S.mt + i * MT_WORDS, S.mtd + i * MT_DOUBLES);
+  if (i < n) gen_codes(S.mt + i * MT_WORDS, S.mc + i * MT_CODES);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
                                                   const uint8_t* __restrict__ mask,
                                                   double* __restrict__ obs) {
-  __shared__ uint32_t scratch[BLOCK / 64][MT_N];
+  __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
   const bool reset = live && (!mask || mask[i]);
@@ -407,7 +400,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
     if (reset) {
-      Rng rng(S.mt + i * MT_WORDS, e.mti, S.mtd + i * MT_DOUBLES);
+      Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
       reset_env(L, e, rng);
       e.mti = rng.finish();
     }
@@ -418,7 +411,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
     }
   }
   const bool stale = reset && (e.mti & MT_STALE);
-  wave_refill(__ballot(stale), S.mt + (live ? i : 0) * MT_WORDS, S.mtd + (live ? i : 0) * MT_DOUBLES, e.mti,
+  wave_refill(__ballot(stale), S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES, e.mti,
               (lds_u32*)scratch[threadIdx.x >> 6]);
   if (reset) {
     e.mti &= ~MT_STALE;
@@ -591,20 +584,21 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
                                                  EpQueue q, int64_t g0,
                                                  unsigned long long* __restrict__ stats,
                                                  uint32_t* __restrict__ err_or) {
-  __shared__ __attribute__((aligned(16))) uint8_t ring[(BLOCK / 64) * RING_WAVE_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
   LEVEL_IN_LDS();
-  lds_u8* const wring = (lds_u8*)ring + (threadIdx.x >> 6) * RING_WAVE_BYTES;
+  lds_u8* const wscr = (lds_u8*)win + (threadIdx.x >> 6) * WIN_WAVE_BYTES;
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
   StepResult r{0, 0, 0, 0};
   uint32_t draws = 0;
+  int lregen = 0;  // halves this lane regenerated in its option loop
   Env e;
   e.mti = 0u;
   int2 ep = make_int2(0, 0);
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
-    RngRing rng(S.mt + i * MT_WORDS, S.mtd + i * MT_DOUBLES, e.mti, wring);
+    RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
     int act;
     if constexpr (POL >= 0) {
       act = policy_action(L, m, e, POL, io.a0, g0 + i, io.t);
@@ -616,13 +610,14 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish();
     draws = rng.draws;
+    lregen = (int)rng.regens;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   // one pass, no classify pass after it: regenerate the halves left in this launch now
   const unsigned long long need = __ballot(live && (e.mti & MT_STALE));
   wave_refill(need, S.mt + (live ? i : 0) * MT_WORDS,
-              S.mtd + (live ? i : 0) * MT_DOUBLES, e.mti,
-              (lds_u32*)wring);
+              S.mc + (live ? i : 0) * MT_CODES, e.mti,
+              (lds_u32*)wscr);
   e.mti &= ~MT_STALE;
   if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
   if (live) {
@@ -631,7 +626,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     S.ep[i] = ep;
   }
   wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
-              __popcll(need), true);
+              __popcll(need) + wave_sum(lregen), true);
 }
 
 // ---- two-pass compacted step (TG_MODE_COMPACT) -------------------------------------------
@@ -758,7 +753,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     e.ang0 = a2.x;
     e.ang1 = a2.y;
     dn = is_done(e);
-    Rng rng(S.mt + i * MT_WORDS, e.mti, S.mtd + i * MT_DOUBLES);
+    Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
     StepResult r{0, 0, (int)dn, 0};
 #if TG_CLASSIFY_STAGE_OBS
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io, orow);
@@ -815,7 +810,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
       }
     pre[NSEG] = acc;
   }
-  __shared__ __attribute__((aligned(16))) uint8_t ring[(BLOCK / 64) * RING_WAVE_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
   LEVEL_IN_LDS();  // includes the barrier
   const int total = pre[NSEG];
   const int base = (blockIdx.x * BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
@@ -839,7 +834,8 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   int2 ep = make_int2(0, 0);
   uint32_t draws = 0;
   int regens = 0;  // wave-uniform
-  lds_u8* const wring = (lds_u8*)ring + (threadIdx.x >> 6) * RING_WAVE_BYTES;
+  int lregen = 0;  // halves this lane regenerated in its option loop
+  lds_u8* const wscr = (lds_u8*)win + (threadIdx.x >> 6) * WIN_WAVE_BYTES;
   unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   TG_STAMP(t0);
 #ifdef TG_DIAG_STAMPS
@@ -850,8 +846,8 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     i = w.lists[(int64_t)(k * SHARDS + sh) * w.shard_cap + idx];
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
-    RngRing rng(S.mt + i * MT_WORDS, S.mtd + i * MT_DOUBLES, e.mti, wring);
-    rng.prime();  // issue the ring DMAs now; the first draw comes after the policy setup
+    RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
+    rng.prime();  // issue the code loads now; the first draw comes after the policy setup
     TG_STAMP(t1);
     run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform: one specialised loop
     TG_STAMP(t2);
@@ -859,6 +855,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish_queued();  // MT_STALE if a half was left: the next step refills it
     draws = rng.draws;
+    lregen = (int)rng.regens;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
@@ -867,7 +864,11 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     S.ang[i] = make_double2(e.ang0, e.ang1);
     S.ep[i] = ep;
   }
+#ifdef TG_DIAG_NOIDLE  // DIAGNOSTIC BUILD ONLY: no refills on the idle waves (results wrong)
+  if (false) {
+#else
   if (base >= total) {
+#endif
     // an idle wave: regenerate stale MT halves listed by k_classify, beside the option loops
     // (an env's half may also be regenerated by its own lane if it needs it first; both write
     // the same generation)
@@ -883,11 +884,12 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
         uint32_t* const env_mt = S.mt + env * MT_WORDS;
         const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
         wave_twist((const glb_u32*)(env_mt + src), (glb_u32*)(env_mt + (MT_N - src)),
-                   (glb_f64*)(S.mtd + env * MT_DOUBLES + (MT_N - src) / 2), (lds_u32*)wring);
+                   S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
       }
     }
   }
-  wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0, regens, true);
+  wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
+             regens + wave_sum(lregen), true);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
   {
@@ -1103,7 +1105,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->S.ang, sizeof(double2) * n);
   ALLOC(h->S.ep, sizeof(int2) * n);
   ALLOC(h->S.mt, sizeof(uint32_t) * MT_WORDS * (size_t)n);
-  ALLOC(h->S.mtd, sizeof(double) * MT_DOUBLES * (size_t)n);
+  ALLOC(h->S.mc, sizeof(uint8_t) * MT_CODES * (size_t)n);
   ALLOC(h->eps, sizeof(tg_episode) * (size_t)h->eps_cap);
   ALLOC(h->eps_count, sizeof(int32_t));
   ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n));
@@ -1143,7 +1145,7 @@ void tg_destroy(tg_batch* h) {
   for (auto ev : h->ev) (void)hipEventDestroy(ev);
   render_free(h->rs);
   void* bufs[] = {h->grid,  h->genrand, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
-                  h->S.mtd, h->eps,     h->eps_count, h->stats, h->err,  h->wl,
+                  h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
                   h->wctr,  h->refill,  h->nrefill,   h->obs_scratch};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -1482,7 +1484,7 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
   else HIP_TRY(hipMemset(h->S.ep, 0, sizeof(int2) * n));
   HIP_TRY(hipMemcpy2D(h->S.mt, sizeof(uint32_t) * MT_WORDS, mt, sizeof(uint32_t) * MT_N,
                       sizeof(uint32_t) * MT_N, (size_t)n, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_gen_doubles, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n);
+  hipLaunchKernelGGL(k_gen_codes, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n);
   hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, 0u);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipDeviceSynchronize());

@@ -35,7 +35,7 @@ struct Soa {
   double2* ang;
   int2* ep;
   uint32_t* mt;   // [N][MT_WORDS]
-  double* mtd;    // [N][MT_DOUBLES]: the random() values of both generations
+  uint8_t* mc;    // [N][MT_CODES]: the draw codes of both generations (tg_core.h draw_code)
 };
 
 struct RenderState;  // tg_render.hip

@@ -13,7 +13,9 @@
 //     WALL (IM/:218-225) — here a 2-cell WALL border around the grid plus clamping;
 //   * near_enough (OB/:46-53) is the exact integer test d^2 < r^2 (inputs are integers);
 //   * the trigger cascade (OB/:76-94) is an explicit 8-bit-frame stack in one u64 register;
-//   * MT19937 keeps two pre-twisted generations per env; consumption only reads (Rng);
+//   * MT19937 keeps two pre-twisted generations per env; consumption only reads (Rng); the
+//     option loops read one code byte per draw (its noisy / jump / flip outcomes, draw_code)
+//     instead of the double;
 //   * each option's policy/tick loop is specialised at compile time to the primitive actions
 //     that option can issue (a wave runs one option in the compacted kernel).
 // Prefixes: TG/ treasure_game.py, IM/ _treasure_game_impl.py, OB/ _objects.py,
@@ -31,6 +33,9 @@ constexpr int INCR = S / 10;   // x_incr / y_incr (IM/:46-47)
 constexpr int HALFW = S / 4;   // player_width // 2 (IM/:49)
 constexpr int MT_N = 624, MT_M = 397;
 constexpr int TICK_CAP = 1 << 14;  // the reference has no cap (OP/:28-31); observed max 105
+// random() draws one primitive tick can take: a move or jump 1; INTERACT flips <= 2 handles,
+// each 1 draw + <= 2 angle wiggles of the cascade (every object changes once per cascade)
+constexpr uint32_t TICK_DRAWS = 8;
 constexpr int PAD = 2;         // WALL cells around the grid in LDS (probes reach <= 60 px out)
 
 // Cell bits in the LDS grid.  A door object's cell carries only its one-hot door bit: its type
@@ -143,12 +148,34 @@ TG_HD void twist_gen(const uint32_t* src, uint32_t* dst) {
   dst[MT_N - 1] = mt_twist(src[MT_N - 1], dst[0], dst[MT_M - 1]);
 }
 TG_HD uint32_t mt_half(uint32_t pos) { return pos >= (uint32_t)MT_N ? (uint32_t)MT_N : 0u; }
-// The kernels' option loops read random() values, not words: every generation is stored twice,
-// as 624 words (for the next twist) and as its 312 random() doubles (MT_DOUBLES per env, half h
-// at h / 2), both written by whoever regenerates the half.
-constexpr int MT_DOUBLES = MT_N;  // 2 x 312
-TG_HD void gen_doubles(const uint32_t* words, double* d) {
-  for (int k = 0; k < MT_N / 2; ++k) d[k] = mt_double(words[2 * k], words[2 * k + 1]);
+
+// ---- draw codes ------------------------------------------------------------------------------
+// Every random() value the option loops consume decides one of four things, each a comparison
+// of the double r against constants, computed with the reference's own IEEE expressions:
+//   noisy(+4) (IM/:361-366): int(round(uniform(2.0, 4)))   = rint(2.0 + 2.0 * r) in {2, 3, 4}
+//   noisy(-4):                int(round(uniform(-4, -2.0))) = rint(-4.0 + 2.0 * r) in {-4, -3, -2}
+//   the jump ticker (IM/:317-319): random() > 0.25
+//   handle.flip (OB/:117-122):     uniform(0, 1) <= 0.8  (== r exactly)
+// so each generation is stored twice: its 624 words (for the next twist and for the rare
+// draws that need the double itself: handle angles, the reset's gauss) and one code byte per
+// draw (MT_CODES per env, half h at h / 2) holding those four outcomes.  Whoever regenerates
+// a half writes both.  Tick loops read bytes (16 draws per 16-B load) and do no f64 work.
+constexpr int MT_CODES = MT_N;  // 2 x 312 draws
+constexpr uint32_t CODE_POS = 3u;        // rint(2 + 2r) - 2
+constexpr uint32_t CODE_NEG_SHIFT = 2;   // rint(-4 + 2r) + 4, bits 2-3
+constexpr uint32_t CODE_JUMP = 1u << 4;  // r > 0.25
+constexpr uint32_t CODE_FLIP = 1u << 5;  // r <= 0.8
+TG_HD uint32_t draw_code(double r) {
+  const uint32_t pos = (uint32_t)((int)rint(2.0 + 2.0 * r) - 2);
+  const uint32_t neg = (uint32_t)((int)rint(-4.0 + 2.0 * r) + 4);
+  return pos | (neg << CODE_NEG_SHIFT) | (r > 0.25 ? CODE_JUMP : 0u) | (r <= 0.8 ? CODE_FLIP : 0u);
+}
+// the noisy step of a code: +2..+4 (DIR > 0: RIGHT / DOWN) or -4..-2 (LEFT / UP)
+TG_HD int code_step(uint32_t c, bool neg) {
+  return neg ? (int)((c >> CODE_NEG_SHIFT) & 3u) - 4 : (int)(c & CODE_POS) + 2;
+}
+TG_HD void gen_codes(const uint32_t* words, uint8_t* c) {
+  for (int k = 0; k < MT_N / 2; ++k) c[k] = (uint8_t)draw_code(mt_double(words[2 * k], words[2 * k + 1]));
 }
 
 // Direct-load consumer (few draws per launch: create/reset/classify, and the host checks).
@@ -158,11 +185,11 @@ struct Rng {
   uint32_t draws;  // random() calls (instrumentation for the roofline)
   bool crossed;    // the half not holding pos is stale (MT_STALE on entry, or entered one)
   bool entered;    // entered a half in this launch (the one left is stale)
-  double* md;      // the env's MT_DOUBLES (device), kept in step when a half is regenerated
+  uint8_t* mc;     // the env's MT_CODES (device), kept in step when a half is regenerated
 
-  TG_HD Rng(uint32_t* m, uint32_t state, double* d = nullptr)
+  TG_HD Rng(uint32_t* m, uint32_t state, uint8_t* c = nullptr)
       : mt(m), pos(state & MT_POS_MASK), draws(0u), crossed((state & MT_STALE) != 0u),
-        entered(false), md(d) {}
+        entered(false), mc(c) {}
 
   TG_HD double random() {
     const uint32_t w0 = mt[pos], w1 = mt[pos + 1];
@@ -173,7 +200,7 @@ struct Rng {
       // generations behind): regenerate it from the half just left before reading it
       if (crossed) {
         twist_gen(mt + (MT_N - pos), mt + pos);
-        if (md) gen_doubles(mt + pos, md + pos / 2);
+        if (mc) gen_codes(mt + pos, mc + pos / 2);
       }
       crossed = entered = true;
     }
@@ -182,18 +209,23 @@ struct Rng {
   }
   // Random.uniform = a + (b-a)*random(); built with -ffp-contract=off (no FMA)
   TG_HD double uniform(double a, double b) { return a + (b - a) * random(); }
+  // a draw consumed for its outcome only (see draw_code)
+  TG_HD uint32_t code() { return draw_code(random()); }
+  // draws come straight from the words: nothing to stage (the device's RngCodes stages codes)
+  TG_HD void reserve(uint32_t) {}
+  TG_HD bool has(uint32_t) const { return true; }
   // the state word to store: position, and whether the other half is stale
   TG_HD uint32_t finish() const { return pos | (crossed ? MT_STALE : 0u); }
   // the same when a refill of the half that was stale on entry is already queued
   TG_HD uint32_t finish_queued() const { return pos | (entered ? MT_STALE : 0u); }
 };
 // regenerate the stale half (per-lane form of wave_refill); returns the clean state word
-TG_HD uint32_t refill_after(uint32_t* mt, uint32_t state, double* md = nullptr) {
+TG_HD uint32_t refill_after(uint32_t* mt, uint32_t state, uint8_t* mc = nullptr) {
   const uint32_t pos = state & MT_POS_MASK;
   if (state & MT_STALE) {
     const uint32_t dst = MT_N - mt_half(pos);
     twist_gen(mt + mt_half(pos), mt + dst);
-    if (md) gen_doubles(mt + dst, md + dst / 2);
+    if (mc) gen_codes(mt + dst, mc + dst / 2);
   }
   return pos;
 }
@@ -423,10 +455,10 @@ TG_HD void cascade(const uint32_t* trig, Env& e, int o0, int v0, R& rng) {
     }
   }
 }
-// handle.flip (OB/:117-122): uniform(0, 1) <= 0.8 (== random() exactly)
+// handle.flip (OB/:117-122): uniform(0, 1) <= 0.8 (== random() exactly: CODE_FLIP)
 template <class R>
 TG_HD void flip(const uint32_t* trig, Env& e, int h, R& rng) {
-  if (rng.random() <= 0.8) {
+  if (rng.code() & CODE_FLIP) {
     const int up = (e.f >> (F_OBJ + 3 + h)) & 1u;
     cascade(trig, e, 3 + h, !up, rng);
   } else {
@@ -467,14 +499,14 @@ TG_HD int tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, int p
   else if (may<PM>(prim, P_RIGHT)) ok = m.can_go_side(e, +1);
   else if (may<PM>(prim, P_JUMP)) ok = !m.can_go_down(e) && m.up_clear(e);
   if (ok) {
-    const double r = rng.random();
+    const uint32_t c = rng.code();
     if (may<PM>(prim, P_JUMP)) {  // jump_ticker = 22, or 23 if random() > 0.25 (IM/:317-319)
-      e.f = (e.f & ~F_JT) | ((r > 0.25) ? 23u : 22u);
+      e.f = (e.f & ~F_JT) | ((c & CODE_JUMP) ? 23u : 22u);
     } else {
       // noisy(+-4) (IM/:361-366): int(round(uniform(-4, -2.0))) or int(round(uniform(2.0, 4))),
-      // uniform = a + (b-a)*r with b-a = 2.0 exactly; round() half-to-even == rint
+      // uniform = a + (b-a)*r with b-a = 2.0 exactly; round() half-to-even == rint (draw_code)
       const bool neg = may<PM>(prim, P_UP) | may<PM>(prim, P_LEFT);
-      const int d = (int)rint((neg ? -4.0 : 2.0) + 2.0 * r);
+      const int d = code_step(c, neg);
       if (may<PM>(prim, P_LEFT) | may<PM>(prim, P_RIGHT)) {
         xd = d;
         e.f = may<PM>(prim, P_RIGHT) ? (e.f | F_FACING) : (e.f & ~F_FACING);
@@ -697,6 +729,7 @@ TG_HD bool is_done(const Env& e) {
 // ==========================================================================================
 template <class R>
 TG_HD void reset_env(const Level& L, Env& e, R& rng) {
+  rng.reserve(4);
   e.f = (e.f & E_MASK) | L.init_flags | F_FACING;
   e.ang0 = ((L.init_flags >> (F_OBJ + 3)) & 1u) ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
   e.ang1 = ((L.init_flags >> (F_OBJ + 4)) & 1u) ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
@@ -822,9 +855,13 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
       // a lane leaves when its span ends; the wave when all have (a per-lane loop: a
       // ballot-driven one, with the idle lanes kept inside, made the compiler copy ~26
       // loop-carried registers per iteration and was slower)
-      while (DIR > 0 ? e.px <= lim : e.px >= lim) {  // a plain tick (see go_plain_limit)
-        const double rr = rng.random();
-        e.px += (int)rint((DIR < 0 ? -4.0 : 2.0) + 2.0 * rr);
+      // (the plain phase also ends when the staged draws run low: the full tick restocks them
+      // in rng.reserve, so the plain loop's body holds no refill code)
+      while ((DIR > 0 ? e.px <= lim : e.px >= lim) && rng.has(TICK_DRAWS)) {  // a plain tick
+#if defined(__HIP_DEVICE_COMPILE__) && defined(TG_DIAG_MARK)
+        asm volatile("; PLAIN_TICK_BEGIN");
+#endif
+        e.px += code_step(rng.code(), DIR < 0);
         e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
         r.reward += -1;
         if (DIR > 0 ? e.px > lim : e.px < lim) pickups(L, e);  // left the span: as the full tick
@@ -835,6 +872,7 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
         }
       }
       if (capped) break;
+      rng.reserve(TICK_DRAWS);
       const int prim = policy<K>(L, m, e, o);
       r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
       if (!o.done) lim = go_plain_limit<DIR>(m, e, o.tx);
@@ -847,6 +885,7 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
   }
 #endif
   do {
+    rng.reserve(TICK_DRAWS);
     const int prim = policy<K>(L, m, e, o);
     r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
     if (++r.ticks >= TICK_CAP) {
