@@ -836,6 +836,67 @@ TG_HD int go_plain_limit(const Map& m, const Env& e, int tx) {
   return lim;
 }
 
+// ==========================================================================================
+// Plain ladder ticks.  While up_ladder / down_ladder (MO/:160-189) climbs with its ladder
+// predicate true, can_fall false, no jump ticker and no key / gold in reach, its tick (policy
+// + IM/:290-359) is exactly: one draw, py += noisy(-4) or noisy(+4), reward -1 (x, facing and
+// everything else unchanged; a DOWN tick's can_fall4 finds can_fall false).  The predicates
+// depend on py only through the rows their probes fall in (px is fixed), so they are constant
+// between row breakpoints: ladder_plain_limit() walks those intervals in the direction of
+// motion (at most LADDER_SPAN_INTERVALS of them) and returns the farthest py such that every
+// start position between it and the current py makes a plain tick (INT_MIN / INT_MAX: none).
+// near_cell (OB/:46-53) with px fixed bounds the span before any object's reach.
+// ==========================================================================================
+constexpr int LADDER_SPAN_INTERVALS = 8;
+TG_HD int isqrt_below(int v) {  // largest t >= 0 with t * t < v (v >= 1)
+  int t = (int)sqrtf((float)v);
+  while (t * t >= v) --t;
+  while ((t + 1) * (t + 1) < v) ++t;
+  return t;
+}
+template <int DIR>  // -1: up_ladder (py decreases), +1: down_ladder
+TG_HD int ladder_plain_limit(const Map& m, const Env& e) {
+  constexpr int NONE = DIR > 0 ? -0x40000000 : 0x40000000;
+  if (e.f & F_JT) return NONE;
+  const uint32_t dc = Map::dc_of(e.f);
+  // objects: near(y) <=> (y - oy*48)^2 < R2_OBJ - dx^2; the span stops short of that range
+  int bound = DIR > 0 ? 0x3FFFFFFF : -0x3FFFFFFF;
+  const int ocx[2] = {e.kx, e.gx}, ocy[2] = {e.ky, e.gy};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int dx = e.px - (ocx[j] * S + S / 2);
+    if (dx * dx >= R2_OBJ) continue;
+    const int t = isqrt_below(R2_OBJ - dx * dx), Y = ocy[j] * S;  // near <=> |y - Y| <= t
+    if ((e.py - Y < 0 ? Y - e.py : e.py - Y) <= t) return NONE;
+    if (DIR < 0 && Y < e.py) bound = max(bound, Y + t + 1);
+    if (DIR > 0 && Y > e.py) bound = min(bound, Y - t - 1);
+  }
+  if (DIR < 0) bound = max(bound, 2);  // can_go_up needs py > 1
+  int y = e.py, lim = NONE;
+  for (int it = 0; it < LADDER_SPAN_INTERVALS; ++it) {
+    if (DIR < 0 ? y < bound : y > bound) break;
+    Env p = e;
+    p.py = y;
+    const bool lad = DIR < 0 ? m.can_go_up(p) : m.can_go_down(p);
+    if (!lad || m.can_fall_at(dc, e.px, y)) break;
+    // the interval of start positions whose probes (rows of y + o) all stay in their rows
+    int end;
+    if (DIR < 0) {  // can_go_up: y - 4, y, y + 44; can_fall: y, y + 50
+      end = max(max(floordiv(y - INCR, S) * S + INCR, floordiv(y, S) * S),
+                max(floordiv(y + S - INCR, S) * S - (S - INCR), floordiv(y + S + 2, S) * S - (S + 2)));
+      end = max(end, bound);
+    } else {        // can_go_down: y, y + 24, y + 51; can_fall: y, y + 50
+      end = min(min(floordiv(y, S) * S + S - 1, floordiv(y + S / 2, S) * S + S - 1 - S / 2),
+                min(floordiv(y + S + INCR - 1, S) * S + S - 1 - (S + INCR - 1),
+                    floordiv(y + S + 2, S) * S + S - 1 - (S + 2)));
+      end = min(end, bound);
+    }
+    lim = end;
+    y = end + DIR;
+  }
+  return lim;
+}
+
 // the while-not-done loop of _Option.run (OP/:28-31) for option K, whose can_run held
 template <int K, class R>
 TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env& e, R& rng,
@@ -876,6 +937,34 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
       const int prim = policy<K>(L, m, e, o);
       r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
       if (!o.done) lim = go_plain_limit<DIR>(m, e, o.tx);
+      if (++r.ticks >= TICK_CAP) {
+        e.f |= E_TICKCAP;
+        break;
+      }
+    } while (!o.done);
+    return;
+  }
+  if constexpr (K == O_UP_LADDER || K == O_DOWN_LADDER) {
+    constexpr int DIR = K == O_UP_LADDER ? -1 : 1;
+    int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
+    bool capped = false;
+    do {
+      // plain phase (ladder_plain_limit), then one full tick: as the go loops
+      while ((DIR > 0 ? e.py <= lim : e.py >= lim) && rng.has(TICK_DRAWS)) {
+        e.py += code_step(rng.code(), DIR < 0);
+        r.reward += -1;
+        if (DIR > 0 ? e.py > lim : e.py < lim) pickups(L, e);  // left the span: as the full tick
+        if (++r.ticks >= TICK_CAP) {
+          e.f |= E_TICKCAP;
+          capped = true;
+          lim = DIR > 0 ? -0x40000000 : 0x40000000;
+        }
+      }
+      if (capped) break;
+      rng.reserve(TICK_DRAWS);
+      const int prim = policy<K>(L, m, e, o);
+      r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
+      if (!o.done) lim = ladder_plain_limit<DIR>(m, e);
       if (++r.ticks >= TICK_CAP) {
         e.f |= E_TICKCAP;
         break;

@@ -61,7 +61,7 @@ def time_variant(lib_path, mode, n, steps, warmup):
 
 def main():
     n = int(os.environ.get("N", 1 << 20))
-    steps, warmup = 60, 10
+    steps, warmup = 60, int(os.environ.get("WARMUP", 300))
     prod = _lib.LIB_PATH
     variants = []
     only = os.environ.get("ONLY")
