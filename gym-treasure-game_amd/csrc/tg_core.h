@@ -339,11 +339,23 @@ struct Map {
     return open_at(dc, xa, ya) & open_at(dc, xa, yb) & open_at(dc, xb, ya) & open_at(dc, xb, yb);
   }
   TG_HD bool can_fall(const Env& e) const { return can_fall_at(dc_of(e.f), e.px, e.py); }
-  // can_fall at (px, py + k) for k = 0..3 as bits 0..3, one batch of lookups
+  // can_fall at (px, py + k) for k = 0..3 as bits 0..3: the probes (px -+ 10 at py + k and
+  // py + 50 + k) span at most two rows each, so 8 lookups instead of 16
   TG_HD uint32_t can_fall4(uint32_t dc, int px, int py) const {
+    const int ca = colx(px - HALFW + 2), cb = colx(px + HALFW - 2);
+    const int ya = py, yb = py + S + 2;
+    const int ra0 = rowy(ya), ra1 = rowy(ya + 3), rb0 = rowy(yb), rb1 = rowy(yb + 3);
+    const bool a0 = is_open(cellb(ca, ra0), dc) & is_open(cellb(cb, ra0), dc);
+    const bool a1 = is_open(cellb(ca, ra1), dc) & is_open(cellb(cb, ra1), dc);
+    const bool b0 = is_open(cellb(ca, rb0), dc) & is_open(cellb(cb, rb0), dc);
+    const bool b1 = is_open(cellb(ca, rb1), dc) & is_open(cellb(cb, rb1), dc);
+    // y + k lies in the second row from k = 48 - (y mod 48) on (rows past the border clamp to
+    // the same WALL row, where both lookups agree anyway)
+    const int ka = S - (ya - floordiv48(ya) * S), kb = S - (yb - floordiv48(yb) * S);
     uint32_t r = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r |= (uint32_t)can_fall_at(dc, px, py + k) << k;
+    for (int k = 0; k < 4; ++k)
+      r |= (uint32_t)((k < ka ? a0 : a1) & (k < kb ? b0 : b1)) << k;
     return r;
   }
 };
@@ -897,6 +909,56 @@ TG_HD int ladder_plain_limit(const Map& m, const Env& e) {
   return lim;
 }
 
+// ==========================================================================================
+// Fused air tick: policy<K> (jump_left / jump_right MO/:297-314, 367-384; down_left /
+// down_right MO/:231-244, 426-439) after its first tick, followed by the primitive tick
+// (IM/:290-359), with every predicate the pair may need at the start position evaluated once
+// and up front (their lookups issue as one batch): can_fall (the policy's, and the tick's
+// gravity test at the same position), can_go_side both ways (the policy's back test, the
+// tick's precondition), up_clear (the jump ticker's rise).  Same outcomes and draws as
+// policy<K> + tick<prims_of(K)>.
+// ==========================================================================================
+template <int K, class R>
+TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng) {
+  constexpr int DIR = (K == O_JUMP_LEFT || K == O_DOWN_LEFT) ? -1 : 1;
+  constexpr bool JUMP = K == O_JUMP_LEFT || K == O_JUMP_RIGHT;
+  const bool cf0 = m.can_fall(e);
+  const bool fwd = m.can_go_side(e, DIR);
+  const bool bwd = JUMP ? m.can_go_side(e, -DIR) : false;
+  const bool uc = m.up_clear(e);
+  int mv = 0;  // the primitive: -1 LEFT, +1 RIGHT, 0 NOP
+  if (close_x(e, o.tx)) {
+    if (!cf0) o.done = true;
+  } else {
+    mv = (JUMP && !cf0 && !fwd) ? -DIR : DIR;  // MO/:311-314: back off when blocked on the floor
+  }
+  int xd = 0, yd = 0;
+  if (mv != 0 && (mv == DIR ? fwd : bwd)) {  // can_go_left / can_go_right (IM/:303-311)
+    xd = code_step(rng.code(), mv < 0);
+    e.f = mv > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
+  }
+  const uint32_t jt = e.f & F_JT;  // IM/:331-337, at the pre-move x
+  if (jt > 0) {
+    if (uc) yd = -INCR;
+    e.f = (e.f & ~F_JT) | (jt - 1);
+  } else if (cf0) {
+    yd = INCR;
+  }
+  e.px += xd;
+  if (yd > 0) {  // IM/:341-348
+    const uint32_t cf = m.can_fall4(Map::dc_of(e.f), e.px, e.py);
+    if (cf & 1u) {
+      int dist = yd;
+      for (int k = yd - 1; k >= 1; --k)
+        if (!((cf >> k) & 1u)) dist = k;
+      yd = dist;
+    }
+  }
+  e.py += yd;
+  pickups(L, e);
+  return -1;  // STEP_REWARD (no JUMP after the first tick)
+}
+
 // the while-not-done loop of _Option.run (OP/:28-31) for option K, whose can_run held
 template <int K, class R>
 TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env& e, R& rng,
@@ -965,6 +1027,22 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
       const int prim = policy<K>(L, m, e, o);
       r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
       if (!o.done) lim = ladder_plain_limit<DIR>(m, e);
+      if (++r.ticks >= TICK_CAP) {
+        e.f |= E_TICKCAP;
+        break;
+      }
+    } while (!o.done);
+    return;
+  }
+  if constexpr (K == O_JUMP_LEFT || K == O_JUMP_RIGHT || K == O_DOWN_LEFT || K == O_DOWN_RIGHT) {
+    do {
+      rng.reserve(TICK_DRAWS);
+      if (o.init) {
+        r.reward += air_tick<K>(L, m, e, o, rng);
+      } else {  // the first tick (the jump itself; the drop's target)
+        const int prim = policy<K>(L, m, e, o);
+        r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
+      }
       if (++r.ticks >= TICK_CAP) {
         e.f |= E_TICKCAP;
         break;
