@@ -56,9 +56,9 @@ EP_CAP = 4096          # episode records gathered per rank per step of a drain i
 #   every env: action 4 + state word 16 read (classify)
 #   reward-None env: angles 16 + episode 8 read; episode 8 + obs 72 + reward/valid/done 6 written
 #   valid env: worklist index 4 + 4, state 16 + 16, angles 16 + 16, episode 8 + 8, obs 72, rows 6
-#   random() draw: one 8-B value (the pre-twisted generation's doubles)
-#   MT regeneration: 624 words read, 624 words + 312 values written
-BYTES_ENV, BYTES_INVALID, BYTES_VALID, BYTES_DRAW, BYTES_REGEN = 20, 110, 166, 8, 7488
+#   random() draw: its 1-B code (tg_core.h draw_code; the option loops read codes, not doubles)
+#   MT regeneration: 624 words read, 624 words + 312 codes written
+BYTES_ENV, BYTES_INVALID, BYTES_VALID, BYTES_DRAW, BYTES_REGEN = 20, 110, 166, 1, 5304
 # SURVEY.md §8(d)'s layout-independent count per env-step: action 4 + obs 72 + reward 4 +
 # valid 1 + done 1 + state read/write 2 x 40 = 162, plus 24 per random() draw (8 B of MT words
 # read + 16 B amortised twist read/write)

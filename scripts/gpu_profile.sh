@@ -3,9 +3,9 @@
 # A test failure (rc 1) does not stop the session; any other failure ends it.
 set -u
 OUT=${OUT:-gpurun_out}
-TAG=${TAG:-r01c}
+TAG=${TAG:-r02}
 BENCH_ARGS=${BENCH_ARGS:---steps 100 --warmup 10}
-PMC_ARGS=${PMC_ARGS:---steps 30 --warmup 5 --cpu-seconds 0}
+PROF_ARGS=${PROF_ARGS:---steps 30 --warmup 5 --cpu-seconds 0 --secondary-steps 0}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 step() {
@@ -14,25 +14,24 @@ step() {
   timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"
-  tail -n 3 "$OUT/$name.log"
+  tail -n 2 "$OUT/$name.log" | cut -c1-300
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -q
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 fi
 step bench 600 python bench.py $BENCH_ARGS
-step trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$TAG" -o run --output-format csv -- python3 bench.py $BENCH_ARGS
-step counters_list 120 rocprofv3 -L
-step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$TAG" -o run --output-format csv -- python3 bench.py $PMC_ARGS
-step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$TAG" -o run --output-format csv -- python3 bench.py $PMC_ARGS
-step pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d "$OUT/pmc_sq1_$TAG" -o run --output-format csv -- python3 bench.py $PMC_ARGS
-step pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2_$TAG" -o run --output-format csv -- python3 bench.py $PMC_ARGS
+step trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$TAG" -o run --output-format csv -- python3 bench.py $PROF_ARGS
+step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$TAG" -o run --output-format csv -- python3 bench.py $PROF_ARGS
+step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$TAG" -o run --output-format csv -- python3 bench.py $PROF_ARGS
+step pmc_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d "$OUT/pmc_sq1_$TAG" -o run --output-format csv -- python3 bench.py $PROF_ARGS
+step pmc_sq2 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2_$TAG" -o run --output-format csv -- python3 bench.py $PROF_ARGS
 if [ "${C5:-0}" = 1 ]; then  # config C5: the same passes over the render workload
   C5_ARGS="--workload c5 --steps 10 --warmup 2 --cpu-seconds 0"
   step bench_c5 600 python bench.py --workload c5 --steps 30 --warmup 3
   step trace_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_${TAG}c5" -o run --output-format csv -- python3 bench.py $C5_ARGS
-  step pmc_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_${TAG}c5" -o run --output-format csv -- python3 bench.py $C5_ARGS
-  step pmc_write_c5 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_${TAG}c5" -o run --output-format csv -- python3 bench.py $C5_ARGS
+  step pmc_fetch_c5 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_${TAG}c5" -o run --output-format csv -- python3 bench.py $C5_ARGS
+  step pmc_write_c5 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_${TAG}c5" -o run --output-format csv -- python3 bench.py $C5_ARGS
 fi
 echo "== all done"

@@ -35,7 +35,15 @@ def kernel_stats(path):
     return out
 
 
-def counters(path):
+def bench_line(path):
+    """the JSON line bench.py printed in a profiled run's log (its steps / regeneration rate)"""
+    if not os.path.exists(path):
+        return None
+    lines = [ln for ln in open(path) if ln.startswith("{")]
+    return json.loads(lines[-1]) if lines else None
+
+
+def counters(path, last=None):
     per = defaultdict(lambda: defaultdict(list))
     meta = {}
     with open(path) as f:
@@ -44,7 +52,9 @@ def counters(path):
             per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta[k] = {"grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),
                        "sgpr": int(r["SGPR_Count"]), "lds": int(r["LDS_Block_Size"])}
-    avg = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in per.items()}
+    # the timed steps are the last dispatches of each step kernel
+    avg = {k: {c: sum(v[-last:] if last else v) / len(v[-last:] if last else v)
+               for c, v in d.items()} for k, d in per.items()}
     return avg, meta
 
 
@@ -65,10 +75,12 @@ def main():
     res["kernel_trace"] = ks
     pm = {}
     meta = {}
+    prof_line = bench_line(os.path.join(a.out, "pmc_fetch.log"))
+    last = prof_line["steps"] if prof_line else None
     for p in ("fetch", "write", "sq1", "sq2"):
         path = os.path.join(a.out, "pmc_%s_%s" % (p, a.tag), "run_counter_collection.csv")
         if os.path.exists(path):
-            avg, m = counters(path)
+            avg, m = counters(path, last)
             meta.update(m)
             for k, d in avg.items():
                 pm.setdefault(k, {}).update(d)
@@ -94,9 +106,17 @@ def main():
                                           (known, raw_err)}
         ns = sum(ks[k]["avg_ns"] for k in ks if k.split("<")[0] in names)
         res["step_kernels_avg_ns"] = ns
+        # VALU issue utilisation of the step kernels: wave64 VALU instructions x 2 cycles
+        # (SIMD-32) over the SIMD-cycles of their duration at the 2.4 GHz nominal clock
+        valu = sum(pm[k].get("SQ_INSTS_VALU", 0.0) for k in step_k)
+        valu_util = valu * 2.0 / (1024 * ns * 2.4) if valu and ns else None
+        res["valu_util"] = valu_util
         tj = {"envs": a.envs, "policy": a.policy, "mode": a.mode, "kernels": sorted(step_k),
-              "hbm_bytes_per_launch": tot, "step_kernels_avg_ns": ns,
-              "source": "profiles/%s_summary.json" % a.tag}
+              "hbm_bytes_per_launch": tot, "step_kernels_avg_ns": ns, "valu_util": valu_util,
+              "regens_per_step": prof_line.get("regens_per_step") if prof_line else None,
+              "burn_in": prof_line.get("burn_in") if prof_line else None,
+              "source": "profiles/%s_summary.json (rocprofv3 --pmc passes of bench.py %s)"
+                        % (a.tag, "steps=%s" % last)}
         with open(os.path.join(ROOT, "profiles", "traffic_step.json"), "w") as f:
             json.dump(tj, f, indent=1)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
