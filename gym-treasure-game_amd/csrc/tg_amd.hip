@@ -647,6 +647,12 @@ constexpr int NSEG = O_COUNT * SHARDS;
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
 struct Work {
   int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = option * SHARDS + shard
+  // the listed envs' state, in worklist order (written by k_classify, which has loaded it
+  // anyway): k_run reads its chunk's 64 records coalesced, in one round trip with the list
+  // entries, instead of a dependent gather of 16 + 16 + 8 scattered bytes per lane
+  uint4* __restrict__ wst4;      // [NSEG][shard_cap]
+  double2* __restrict__ wang;
+  int2* __restrict__ wep;
   int32_t* __restrict__ ctr;     // [NSEG * CTR_STRIDE], this step's counters
   int32_t* __restrict__ ctr_next;  // the other parity's, zeroed here for the next step
   uint32_t* __restrict__ refill;  // [n]: per classify wave w, slots 64w..: env | source half
@@ -782,7 +788,13 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   }
   if (threadIdx.x < O_COUNT) bbase[threadIdx.x] = my_base;
   __syncthreads();
-  if (runs) w.lists[(int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot] = (int32_t)i;
+  if (runs) {
+    const int64_t at = (int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot;
+    w.lists[at] = (int32_t)i;
+    w.wst4[at] = s4;
+    w.wang[at] = a2;
+    w.wep[at] = ep;
+  }
   wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
               AUTORESET ? (live && !runs && dn) : 0);
 }
@@ -846,9 +858,10 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
 #endif
   (void)t0; (void)t1; (void)t2; (void)t3;
   if (live) {
-    i = w.lists[(int64_t)(k * SHARDS + sh) * w.shard_cap + idx];
-    unpack(S.st4[i], S.ang[i], e);
-    ep = S.ep[i];
+    const int64_t at = (int64_t)(k * SHARDS + sh) * w.shard_cap + idx;
+    i = w.lists[at];
+    unpack(w.wst4[at], w.wang[at], e);
+    ep = w.wep[at];
     RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
     rng.prime();  // issue the code loads now; the first draw comes after the policy setup
     TG_STAMP(t1);
@@ -1121,6 +1134,9 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   // a shard holds the envs of every SHARDS-th workgroup
   h->shard_cap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK;
   ALLOC(h->wl, sizeof(int32_t) * NSEG * (size_t)h->shard_cap);
+  ALLOC(h->wst4, sizeof(uint4) * NSEG * (size_t)h->shard_cap);
+  ALLOC(h->wang, sizeof(double2) * NSEG * (size_t)h->shard_cap);
+  ALLOC(h->wep, sizeof(int2) * NSEG * (size_t)h->shard_cap);
   ALLOC(h->wctr, sizeof(int32_t) * 2 * NSEG * CTR_STRIDE);
   ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63));
   ALLOC(h->nrefill, (size_t)((n + 63) >> 6));
@@ -1154,6 +1170,7 @@ void tg_destroy(tg_batch* h) {
   render_free(h->rs);
   void* bufs[] = {h->grid,  h->genrand, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
                   h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
+                  h->wst4,  h->wang,    h->wep,
                   h->wctr,  h->refill,  h->nrefill,   h->obs_scratch};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -1203,7 +1220,7 @@ int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
     int32_t* const cur = h->wctr + (h->parity ? NSEG * CTR_STRIDE : 0);
     int32_t* const nxt = h->wctr + (h->parity ? 0 : NSEG * CTR_STRIDE);
     h->parity ^= 1;
-    const Work w{h->wl, cur, nxt, h->refill, h->nrefill, h->shard_cap};
+    const Work w{h->wl, h->wst4, h->wang, h->wep, cur, nxt, h->refill, h->nrefill, h->shard_cap};
     decltype(&k_classify<true, true>) kc;
     if (io.policy == TG_POLICY_UNIFORM)
       kc = ar ? (fo ? k_classify<true, true, 0> : k_classify<true, false, 0>)

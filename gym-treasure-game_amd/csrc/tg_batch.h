@@ -60,6 +60,9 @@ struct tg_batch {
   uint32_t* err = nullptr;
   int mode = TG_MODE_COMPACT;
   int32_t* wl = nullptr;   // per-(option, shard) worklists (compact mode)
+  uint4* wst4 = nullptr;   // the listed envs' state in worklist order (k_classify -> k_run)
+  double2* wang = nullptr;
+  int2* wep = nullptr;
   int32_t* wctr = nullptr; // sharded counters
   uint32_t* refill = nullptr;  // stale MT halves to regenerate in k_run (compact mode)
   uint8_t* nrefill = nullptr;
