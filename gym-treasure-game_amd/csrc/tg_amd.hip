@@ -717,7 +717,11 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
       if (io.actions) io.actions[i] = act;
     }
     k = option_index(act);
+#ifdef TG_DIAG_CLS_NOCANRUN  // DIAGNOSTIC BUILD ONLY: prices can_run (results wrong)
+    runs = k >= 0 && ((sm64((uint64_t)i ^ (uint64_t)io.t) & 7u) < 2u) && k != O_INTERACT;
+#else
     runs = k >= 0 && can_run(L, m, e, k);
+#endif
   }
   // halves left in the previous step (MT_STALE) go on the refill list; k_run's idle waves
   // regenerate them beside the option loops (a lane that needs one first does it itself)
@@ -765,7 +769,11 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
     StepResult r{0, 0, (int)dn, 0};
 #if TG_CLASSIFY_STAGE_OBS
+#ifdef TG_DIAG_CLS_NOFINISH  // DIAGNOSTIC BUILD ONLY: prices the invalid envs' finish
+    io.reward[i] = 0; io.valid[i] = 0; io.done[i] = (uint8_t)dn;
+#else
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io, orow);
+#endif
 #else
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
 #endif
@@ -1104,7 +1112,6 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   h->n = n;
   h->g0 = global_offset;
   h->seed0 = seed_base;
-  h->L = L;
   h->domain = dom;
   // completed-episode queue: drained by tg_episodes; records beyond it are counted as dropped
   const int64_t cap = 4 * n > (1 << 16) ? 4 * n : (1 << 16);
@@ -1122,6 +1129,10 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   grid.resize((grid.size() + 3) & ~(size_t)3, 0);
   ALLOC(h->grid, grid.size());
   ALLOC(h->genrand, sizeof gen);
+  const std::vector<uint32_t> gotab = build_gotab(L, grid);
+  ALLOC(h->gotab, sizeof(uint32_t) * gotab.size());
+  L.gotab = h->gotab;
+  h->L = L;
   ALLOC(h->S.st4, sizeof(uint4) * n);
   ALLOC(h->S.ang, sizeof(double2) * n);
   ALLOC(h->S.ep, sizeof(int2) * n);
@@ -1143,6 +1154,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
 #undef ALLOC
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->gotab, gotab.data(), sizeof(uint32_t) * gotab.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
       hipMemset(h->wctr, 0, sizeof(int32_t) * 2 * NSEG * CTR_STRIDE) != hipSuccess ||
       hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)) != hipSuccess ||
@@ -1168,7 +1180,7 @@ void tg_destroy(tg_batch* h) {
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   for (auto ev : h->ev) (void)hipEventDestroy(ev);
   render_free(h->rs);
-  void* bufs[] = {h->grid,  h->genrand, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
+  void* bufs[] = {h->grid,  h->genrand, h->gotab, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
                   h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
                   h->wst4,  h->wang,    h->wep,
                   h->wctr,  h->refill,  h->nrefill,   h->obs_scratch};

@@ -52,6 +52,7 @@ struct tg_batch {
   tg::Level L{};
   uint32_t* grid = nullptr;  // bordered cell grid, padded to whole words
   uint32_t* genrand = nullptr;
+  uint32_t* gotab = nullptr;  // GoTable (tg_core.h go_lookup), W * H * 32 entries
   tg::Soa S{};
   tg_episode* eps = nullptr;
   int32_t* eps_count = nullptr;

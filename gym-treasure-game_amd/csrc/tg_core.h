@@ -71,6 +71,9 @@ struct Level {
   int8_t key_cx, key_cy, bolt_cx, bolt_cy, gold_cx, gold_cy;
   uint32_t init_flags;       // door/handle/bolt initial booleans at their F_OBJ bits
   uint32_t trig[6][2];       // trigger lists [object][polarity]: count(4b) + 7 x (target 3b, val 1b)
+  // go_left / go_right can_run and target per (cell, door state, key home?, gold home?)
+  // (GoTable; device global memory, built at tg_create; null: computed directly)
+  const uint32_t* gotab;
 };
 
 // ---- per-env state (registers) -------------------------------------------------------------
@@ -596,6 +599,22 @@ TG_HD bool landing(const Map& m, const Env& e, int xc, int yc) {
   return m.open_cell(Map::dc_of(e.f), xc, yc) & Map::is_wall(m.cellb(xc, yc + 1));
 }
 
+// ---- GoTable: the go options' can_run and target, precomputed --------------------------------
+// go_left / go_right's can_run (MO/:23-41, 95-113) and target (MO/:43-67, 115-139) read only
+// the player's cell (xc, yc), cell types of rows yc - 1 .. yc + 1, the door states and, through
+// is_object_at (IM/:402-409), the key's and the gold's cells on row yc.  The key is at home, in
+// the bag (row H - 1) or at (-1, -1); the gold at home or in the bag.  So for a player cell
+// inside the grid whose row holds neither a moved key nor a bagged gold (row H - 1 is a wall
+// in every playable level), the answer depends on (cell, door state, key at home, gold at
+// home) only: entry ((yc * W + xc) * 8 + doors) * 4 + key_home * 2 + gold_home holds
+// bit 0 / 1 = can_run left / right, bits 8-15 / 16-23 = target column + 1.
+TG_HD bool go_lookup(const Level& L, const Env& e, int xc, int yc, uint32_t& out) {
+  if (!L.gotab || xc < 0 || xc >= L.W || yc < 0 || yc >= L.H) return false;
+  const bool kh = e.kx == L.key_cx && e.ky == L.key_cy, gh = e.gx == L.gold_cx && e.gy == L.gold_cy;
+  if ((!kh && e.ky == yc) || (!gh && e.gy == yc)) return false;
+  out = L.gotab[((yc * L.W + xc) * 8 + (int)Map::dc_of(e.f)) * 4 + (kh ? 2 : 0) + (gh ? 1 : 0)];
+  return true;
+}
 TG_HD bool can_run(const Level& L, const Map& m, const Env& e, int k) {
   int xc, yc;
   player_cell(e, xc, yc);
@@ -604,6 +623,8 @@ TG_HD bool can_run(const Level& L, const Map& m, const Env& e, int k) {
     case O_GO_LEFT:
     case O_GO_RIGHT: {  // MO/:23-41, 95-113
       const int dir = k == O_GO_LEFT ? -1 : 1;
+      uint32_t gt;
+      if (go_lookup(L, e, xc, yc, gt)) return (gt >> (k == O_GO_LEFT ? 0 : 1)) & 1u;
       int tc;
       if (!go_target(L, m, e, dir, xc, yc, tc)) return false;
       for (int x = xc; dir < 0 ? x >= tc : x <= tc; x += dir) {
@@ -667,7 +688,9 @@ TG_HD int policy(const Level& L, const Map& m, const Env& e, Opt& o) {
     constexpr int dir = K == O_GO_LEFT ? -1 : 1;
     if (!o.init) {
       player_cell(e, xc, yc);
-      go_target(L, m, e, dir, xc, yc, o.tx);  // exists: can_run checked it
+      uint32_t gt;
+      if (go_lookup(L, e, xc, yc, gt)) o.tx = (int)((gt >> (dir < 0 ? 8 : 16)) & 0xFFu) - 1;
+      else go_target(L, m, e, dir, xc, yc, o.tx);  // exists: can_run checked it
       o.init = true;
     }
     if (close_x(e, o.tx)) o.done = true;

@@ -173,4 +173,37 @@ inline int parse_level(const char* dom, const char* objs, const char* inter, Lev
   return 0;
 }
 
+// The GoTable (tg_core.h go_lookup) of a parsed level, W * H * 32 entries, evaluated with the
+// direct go_target / can_run code at a player standing in the middle of each cell: the key and
+// the gold at home, or off the row (a position go_lookup never answers from the table).
+inline std::vector<uint32_t> build_gotab(const Level& Lin, const std::vector<uint8_t>& grid) {
+  Level L = Lin;
+  L.gotab = nullptr;  // evaluate directly
+  const Map m{grid.data(), L.W, L.H};
+  std::vector<uint32_t> tab((size_t)L.W * L.H * 32);
+  for (int yc = 0; yc < L.H; ++yc)
+    for (int xc = 0; xc < L.W; ++xc)
+      for (int dc = 0; dc < 8; ++dc)
+        for (int kg = 0; kg < 4; ++kg) {
+          Env e{};
+          e.px = xc * S + S / 2;
+          e.py = yc * S;
+          e.f = (uint32_t)dc << F_OBJ;
+          e.kx = (kg & 2) ? L.key_cx : -1;
+          e.ky = (kg & 2) ? L.key_cy : -1;
+          e.gx = (kg & 1) ? L.gold_cx : -1;
+          e.gy = (kg & 1) ? L.gold_cy : -1;
+          uint32_t v = 0;
+          for (int d = 0; d < 2; ++d) {
+            const int dir = d ? 1 : -1;
+            int tc = -1;
+            go_target(L, m, e, dir, xc, yc, tc);
+            v |= (uint32_t)can_run(L, m, e, d ? O_GO_RIGHT : O_GO_LEFT) << d;
+            v |= (uint32_t)((tc + 1) & 0xFF) << (8 + 8 * d);
+          }
+          tab[(((size_t)yc * L.W + xc) * 8 + dc) * 4 + kg] = v;
+        }
+  return tab;
+}
+
 }  // namespace tg

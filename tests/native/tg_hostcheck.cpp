@@ -35,15 +35,24 @@ uint64_t rec_hash(uint64_t h, const double o[9], int32_t r, int v, int d) {
 
 extern "C" {
 
+// go_left / go_right answered from the GoTable as on the device (1, default) or directly (0)
+static int g_gotab = 1;
+void hc_set_gotab(int on) { g_gotab = on; }
+
 static bool load_level(const char* dom, const char* objs, const char* inter, Level& L,
-                       std::vector<uint8_t>& grid) {
+                       std::vector<uint8_t>& grid, std::vector<uint32_t>& tab) {
   std::string err;
   if (!dom) {
     dom = kDefaultDomain;
     objs = kDefaultObjects;
     inter = kDefaultInteractions;
   }
-  return parse_level(dom, objs, inter, L, grid, err) == 0;
+  if (parse_level(dom, objs, inter, L, grid, err) != 0) return false;
+  if (g_gotab) {
+    tab = build_gotab(L, grid);
+    L.gotab = tab.data();
+  }
+  return true;
 }
 
 // Level texts as tg_create takes them (NULL = built-in default).
@@ -54,7 +63,8 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
            int64_t* draws, int64_t* ticks) {
   Level Lv;
   std::vector<uint8_t> grid;
-  if (!load_level(dom, objs, inter, Lv, grid)) return -1;
+  std::vector<uint32_t> tab;
+  if (!load_level(dom, objs, inter, Lv, grid, tab)) return -1;
   const Level* L = &Lv;
   uint32_t gen[MT_N];
   gen[0] = 19650218u;
@@ -155,7 +165,8 @@ int hc_rng_stream(uint64_t seed, const int32_t* launches, int nl, int defer, dou
 unsigned hc_predicates(int px, int py, unsigned door_bits) {
   static Level L;
   static std::vector<uint8_t> grid;
-  if (grid.empty() && !load_level(nullptr, nullptr, nullptr, L, grid)) return ~0u;
+  static std::vector<uint32_t> tab;
+  if (grid.empty() && !load_level(nullptr, nullptr, nullptr, L, grid, tab)) return ~0u;
   const Map m{grid.data(), L.W, L.H};
   Env e{};
   e.px = px;
@@ -182,7 +193,8 @@ int hc_render_run(const char* dom, const char* objs, const char* inter, uint64_t
                   int autoreset, const uint8_t* sprites, int sw, int sh, uint8_t* frames) {
   Level Lv;
   std::vector<uint8_t> grid;
-  if (!load_level(dom, objs, inter, Lv, grid)) return -1;
+  std::vector<uint32_t> tab;
+  if (!load_level(dom, objs, inter, Lv, grid, tab)) return -1;
   const Level* L = &Lv;
   std::vector<std::string> desc;
   for (auto& l : lines_of(dom ? dom : kDefaultDomain)) desc.push_back(strip(l));

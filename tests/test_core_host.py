@@ -148,3 +148,20 @@ def test_core_vs_reference_levels(hostcheck, level, policy):
     g = {k: d[k] for k in ("obs", "final_obs", "reward", "valid", "done")}
     assert_same(o, g, keys=list(g))
     np.testing.assert_array_equal(o["draws"], d["draws"][:, -1])
+
+
+@pytest.mark.parametrize("level", [None, "corridor", "gen1", "gen2", "gen3", "exit"])
+@pytest.mark.parametrize("policy", [0, 1])
+def test_core_gotable_matches_direct(hostcheck, level, policy):
+    """The go options' GoTable (tg_core.h go_lookup, the device's path) against the direct
+    scan it replaces, over whole auto-reset trajectories (keys and gold picked up and dropped
+    into the bag, every door state the levels reach)."""
+    ld = None if level is None else os.path.join(LEVELS, level)
+    try:
+        hostcheck.hc_set_gotab(0)
+        direct = hc_run(hostcheck, 11, 0, 256, 60, 0xBEEF, policy, True, level_dir=ld)
+    finally:
+        hostcheck.hc_set_gotab(1)
+    table = hc_run(hostcheck, 11, 0, 256, 60, 0xBEEF, policy, True, level_dir=ld)
+    assert_same(direct, table)
+    np.testing.assert_array_equal(direct["ticks"], table["ticks"])
