@@ -944,6 +944,483 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
 #endif
 }
 
+// ------------------------------------------------------------------------------------------
+// tg_rollout, TG_MODE_ASYNC: K steps of every env in ONE launch, no step barrier.
+//   Workgroup b owns envs [b*E, b*E + E) for the whole launch (E <= RO_EMAX; nothing is
+//   shared between workgroups, so there is no cross-CU hand-off and no grid-wide wait).  Inside
+//   a workgroup the envs sit in per-option queues (LDS bitmaps over the E local indices, one
+//   bit per env, plus a count); each wave repeatedly pops up to 64 envs of ONE option, runs
+//   their option loops (the same run_option as k_run: wave-uniform k), finishes the step (the
+//   step's outputs at row t of [K][N]), and then, per lane, evaluates the env's NEXT step: the
+//   policy's action, can_run (a reward-None step is finished right there, as k_classify does,
+//   and the next one evaluated), and pushes the env onto that option's queue.  Envs therefore
+//   advance at their own pace — env i's step t still depends only on env i's state, so every
+//   output row, state word and episode record is the one K x tg_step produces (the episode
+//   queue's ORDER differs) — and a wave never waits for the slowest option of a step.
+//   Stale MT halves: an env that leaves a half goes onto queue RO_REFILL first; a wave that
+//   pops it regenerates the half with the coalesced whole-wave twist (wave_refill), then moves
+//   the env on to the option recorded for it (nextk).  So no env enters a stale half here.
+//   Same-CU hand-offs only: a lane's global stores of an env (state, MT) are complete
+//   (s_waitcnt vmcnt(0)) before the env's bit is set; pops and pushes are LDS atomics; pops
+//   hold a workgroup LDS lock while they scan the bitmap.
+// ------------------------------------------------------------------------------------------
+constexpr int RO_WAVES = 4;
+#ifndef TG_RO_MINW
+#define TG_RO_MINW 2  // waves per SIMD the register budget is sized for (launch bounds)
+#endif
+constexpr int RO_THREADS = RO_WAVES * 64;
+constexpr int RO_EMAX = 2048;            // envs per workgroup: 64 bitmap words (one per lane)
+constexpr int RO_WORDS = RO_EMAX / 32;
+constexpr int RO_REFILL = O_COUNT;       // queue of envs whose stale MT half comes first
+constexpr int RO_NQ = O_COUNT + 1;
+constexpr uint8_t RO_RETIRE = 0xFF;      // nextk: the env has done its K steps
+constexpr uint32_t RO_E_STALL = 1u << 31;  // err bit: a workgroup's waves found no work (bug)
+constexpr unsigned long long RO_STALL_TICKS = 200000000ull;  // 2 s of the 100 MHz clock without progress
+static_assert(RO_WORDS == 64, "one bitmap word per lane");
+
+struct RollIO {
+  StepIO io;         // row-0 pointers ([K][N] arrays), policy, action seed, t = the first step
+  int32_t steps;     // K
+  bool obs_rows;     // obs is [K][N][9] (else [N][9] scratch, overwritten every step)
+};
+__device__ __forceinline__ StepIO step_io(const RollIO& R, int t, int64_t n) {
+  StepIO s = R.io;
+  const size_t off = (size_t)t * (size_t)n;
+  if (s.actions) s.actions += off;
+  if (R.obs_rows) s.obs += off * 9;
+  s.reward += off;
+  s.valid += off;
+  s.done += off;
+  s.t = R.io.t + t;
+  return s;
+}
+
+struct RoLds {
+  uint32_t bits[RO_NQ][RO_WORDS];
+  int cnt[RO_NQ];
+  int cursor[RO_NQ];
+  int lock, running, retired;
+  uint16_t tstep[RO_EMAX];  // steps done in this launch
+  uint8_t nextk[RO_EMAX];   // the option an env on RO_REFILL moves on to (or RO_RETIRE)
+  uint16_t stage[RO_WAVES][64];
+  unsigned long long count[6];  // steps, valid, ticks, draws, episodes, regens (the launch's)
+  unsigned long long wticks;
+};
+
+struct LaneCount {
+  int steps, valid, ticks, draws, episodes, regens;
+};
+// a batch's counts into the workgroup's (LDS) totals; all 64 lanes
+__device__ __forceinline__ void ro_count(RoLds& Q, const LaneCount& c) {
+  const int v[6] = {wave_sum(c.steps), wave_sum(c.valid), wave_sum(c.ticks), wave_sum(c.draws),
+                    wave_sum(c.episodes), wave_sum(c.regens)};
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if (v[k]) atomicAdd(&Q.count[k], (unsigned long long)v[k]);
+  }
+}
+
+// one completed episode, from a lane on its own (the rare reward-None step that ends one)
+__device__ __forceinline__ void record_episode_lane(int64_t g, int2& ep, const EpQueue& q,
+                                                    unsigned long long* stats) {
+  const int slot = atomicAdd(q.count, 1);
+  if ((uint32_t)slot >= (uint32_t)q.cap) {
+    atomicMin(q.count, q.cap);
+    atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + ST_EP_OVERFLOW], 1ull);
+  } else {
+    tg_episode r;
+    r.env = g;
+    r.ret = ep.x;
+    r.len = ep.y;
+    q.eps[slot] = r;
+  }
+  ep = make_int2(0, 0);
+}
+
+// The env's next step(s) after `t` steps: reward-None steps are finished here (k_classify's
+// path) until one whose option can run, or the K-th step.  Returns the queue to push the env
+// onto: its option, RO_REFILL (a stale half; nk = the option or RO_RETIRE), or -1 (retired).
+template <bool AUTORESET, int POL>
+__device__ __forceinline__ int ro_advance(const Level& L, const Map& m, Env& e, int2& ep,
+                                          int64_t i, int64_t g, int& t, const RollIO& R,
+                                          int64_t n, const Soa& S, const EpQueue& q,
+                                          unsigned long long* stats, uint8_t& nk, LaneCount& c) {
+  nk = RO_RETIRE;
+  while (t < R.steps) {
+    const int act = policy_action(L, m, e, POL, R.io.a0, g, R.io.t + t);
+    const StepIO io = step_io(R, t, n);
+    if (io.actions) io.actions[i] = act;
+    const int k = option_index(act);
+    if (k >= 0 && can_run(L, m, e, k)) {
+      nk = (uint8_t)k;
+      break;
+    }
+    // reward None, state unchanged (TG/:91-96, OP/:22-23)
+    if (k < 0) e.f |= E_ACTION;
+    const bool dn = is_done(e);
+    Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
+    const StepResult r{0, 0, (int)dn, 0};
+    finish_step<AUTORESET, false>(L, e, rng, i, r, ep, io);
+    e.mti = rng.finish();
+    c.draws += (int)rng.draws;
+    c.steps += 1;
+    if (AUTORESET && dn) {
+      record_episode_lane(g, ep, q, stats);
+      c.episodes += 1;
+    }
+    ++t;
+  }
+  if (e.mti & MT_STALE) return RO_REFILL;
+  return nk == RO_RETIRE ? -1 : (int)nk;
+}
+
+// push every lane's env (local index j) onto queue `dest` (-1: retired, -2: nothing); all 64
+// lanes.  The lanes' global stores must be complete (the caller's vmcnt(0)).
+__device__ __forceinline__ void ro_push(RoLds& Q, int dest, int j) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int qq = 0; qq < RO_NQ; ++qq) {
+    const unsigned long long b = __ballot(dest == qq);
+    if (b) {
+      if (dest == qq) atomicOr(&Q.bits[qq][j >> 5], 1u << (j & 31));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the bits before the count
+      if (lane == __ffsll((long long)b) - 1) atomicAdd(&Q.cnt[qq], __popcll(b));
+    }
+  }
+  const unsigned long long r = __ballot(dest == -1);
+  if (r && lane == __ffsll((long long)r) - 1) atomicAdd(&Q.retired, __popcll(r));
+}
+
+// the workgroup's queue lock (lane 0 spins; bounded by RO_STALL_TICKS of real time): false =
+// give up (flagged).  Waves with nothing to do poll the counts WITHOUT the lock, so a holder
+// never competes with idle pollers.
+__device__ __forceinline__ bool ro_lock(RoLds& Q, uint32_t* err_or) {
+  int got = 1;
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long t0 = 0;
+    while (atomicCAS(&Q.lock, 0, 1) != 0) {
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      if (!t0) t0 = now;
+      if (now - t0 > RO_STALL_TICKS) {  // cannot happen unless the bookkeeping is broken
+        got = 0;
+        atomicOr(err_or, RO_E_STALL);
+        printf("k_rollout: block %d wave %d: queue lock not released\n", (int)blockIdx.x,
+               (int)(threadIdx.x >> 6));
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  got = __shfl(got, 0, 64);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return got != 0;
+}
+__device__ __forceinline__ void ro_unlock(RoLds& Q) {
+  if ((threadIdx.x & 63) == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    atomicExch(&Q.lock, 0);
+  }
+}
+// With the lock held: take up to `want` envs off queue qsel into Q.stage[wave][0, take), scanning
+// its bitmap from the queue's cursor (lane l reads word cursor + l), so every queued env is
+// reached within one sweep.  Returns take (wave-uniform).  All 64 lanes.
+__device__ __forceinline__ int ro_pop(RoLds& Q, int qsel, int want) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int take = __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(&Q.cnt[qsel], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+  if (take > want) take = want;
+  if (take <= 0) return 0;
+  const int cur = __builtin_amdgcn_readfirstlane(Q.cursor[qsel]);
+  const int wd = (cur + lane) & (RO_WORDS - 1);
+  uint32_t v = __hip_atomic_load(&Q.bits[qsel][wd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int pc = __popc(v);
+  int incl = pc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  const int avail = __shfl(incl, 63, 64);
+  if (avail < take) take = avail;  // never (a counted env's bit is set before its count)
+  const int excl = incl - pc;
+  const int mine = excl >= take ? 0 : (take - excl < pc ? take - excl : pc);
+  uint32_t picked = 0;
+  for (int r = 0; r < mine; ++r) {
+    const uint32_t bit = v & (0u - v);
+    picked |= bit;
+    v ^= bit;
+    Q.stage[wave][excl + r] = (uint16_t)(wd * 32 + __builtin_ctz(bit));
+  }
+  if (picked) atomicAnd(&Q.bits[qsel][wd], ~picked);
+  const unsigned long long tk = __ballot(mine > 0);
+  const int last = tk ? 63 - __clzll((long long)tk) : 0;
+  const int lastw = __shfl(wd, last, 64), lastleft = __shfl(pc - mine, last, 64);
+  if (lane == 0 && take > 0) {
+    Q.cursor[qsel] = lastleft ? lastw : ((lastw + 1) & (RO_WORDS - 1));
+    atomicSub(&Q.cnt[qsel], take);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the stage entries, for every lane
+  return take;
+}
+
+constexpr int RO_REFILL_T = 16;  // a stint refills its idle lanes once this many are idle
+constexpr int RO_BACKOFF = 8;    // rounds before popping again after the queue ran dry
+#ifndef TG_RO_WTICKS
+#define TG_RO_WTICKS 1           // count wave-ticks (lane efficiency) in the stints
+#endif
+
+// One stint of a wave on option K: its lanes run option K for envs popped from queue K; a lane
+// whose option ends waits (pend) until RO_REFILL_T lanes are idle, then those are finished
+// together (finish_step, the next step's action, push) and refilled from the queue.  Returns
+// when no lane is in flight and the queue is empty.  All 64 lanes.
+template <int K, bool AUTORESET, int POL>
+__device__ __forceinline__ void ro_stint(const Soa& S, int64_t n, const Level& L,
+                                         const uint32_t* trig, const Map& m, const RollIO& R,
+                                         const EpQueue& q, int64_t g0, int64_t base, int ne,
+                                         RoLds& Q, lds_u8* wscr, unsigned long long* stats,
+                                         uint32_t* err_or) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  bool act = false, pend = false;
+  int j = 0, lim = 0;
+  Env e;
+  e.px = e.py = e.kx = e.ky = e.gx = e.gy = 0;
+  e.f = e.mti = 0u;
+  e.ang0 = e.ang1 = 0.0;
+  Opt o{0, false, false};
+  StepResult r{0, 0, 0, 0};
+  RngCodes rng(S.mt, S.mc, 0u, wscr);
+  int backoff = 0;  // wave-uniform
+  unsigned long long wticks = 0;
+  (void)wticks;
+  (void)ne;
+  while (true) {
+    const unsigned long long am = __ballot(act);
+    const int nact = __popcll(am);
+    if (nact == 0 || (64 - nact >= RO_REFILL_T && backoff == 0)) {
+      // ---- finish the lanes whose option has ended
+      LaneCount c{0, 0, 0, 0, 0, 0};
+      int dest = -2;
+      if (pend) {
+        const int64_t i = base + j;
+        int2 ep = S.ep[i];
+        int t = Q.tstep[j];
+        r.done = is_done(e);
+        finish_step<AUTORESET, false>(L, e, rng, i, r, ep, step_io(R, t, n));
+        e.mti = rng.finish();
+        c.steps = c.valid = 1;
+        c.ticks = r.ticks;
+        c.draws = (int)rng.draws;
+        c.regens = (int)rng.regens;
+        ++t;
+        if (AUTORESET && r.done) {
+          record_episode_lane(g0 + i, ep, q, stats);
+          c.episodes = 1;
+        }
+        uint8_t nk;
+        dest = ro_advance<AUTORESET, POL>(L, m, e, ep, i, g0 + i, t, R, n, S, q, stats, nk, c);
+        if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+        S.st4[i] = pack(e);
+        S.ang[i] = make_double2(e.ang0, e.ang1);
+        S.ep[i] = ep;
+        Q.tstep[j] = (uint16_t)t;
+        Q.nextk[j] = nk;
+        pend = false;
+      }
+      if (__ballot(dest != -2)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the envs' stores before their bits
+        ro_push(Q, dest, j);
+        ro_count(Q, c);
+      }
+      // ---- new envs for the idle lanes
+      int take = 0;
+      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&Q.cnt[K], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP)) > 0) {
+        if (!ro_lock(Q, err_or)) return;
+        take = ro_pop(Q, K, 64 - nact);
+        ro_unlock(Q);
+      }
+      if (take) {
+        const unsigned long long below = (1ull << lane) - 1ull;
+        const int rank = __popcll(~am & below);
+        if (!act && rank < take) {
+          j = Q.stage[wave][rank];
+          const int64_t i = base + j;
+          unpack(S.st4[i], S.ang[i], e);
+          o = Opt{0, false, false};
+          r = StepResult{0, 1, 0, 0};
+          lim = round_no_span(K);
+          rng = RngCodes(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
+          rng.prime();
+          act = true;
+        }
+        backoff = 0;
+      } else {
+        backoff = RO_BACKOFF;
+      }
+      if (!__ballot(act)) break;
+    } else if (backoff) {
+      --backoff;
+    }
+#if TG_RO_WTICKS
+    const int tb = r.ticks;
+#endif
+    if (act && run_round_k<K>(L, trig, m, e, rng, r, o, lim)) {
+      act = false;
+      pend = true;
+    }
+#if TG_RO_WTICKS
+    wticks += (unsigned long long)wave_max(act || pend ? r.ticks - tb : 0);
+#endif
+  }
+#if TG_RO_WTICKS
+  if (lane == 0 && wticks) atomicAdd(&Q.wticks, wticks);
+#endif
+}
+
+// the queued envs' stale MT halves, regenerated with the whole wave (wave_refill), then on to
+// the option recorded for each (nextk).  All 64 lanes; `take` envs staged by ro_pop.
+__device__ __forceinline__ void ro_refill_batch(const Soa& S, int64_t base, int take, RoLds& Q,
+                                                lds_u8* wscr) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool live = lane < take;
+  const int j = live ? (int)Q.stage[wave][lane] : 0;
+  const int64_t i = base + j;
+  Env e;
+  e.mti = 0u;
+  uint4 s4 = make_uint4(0, 0, 0, 0);
+  if (live) {
+    s4 = S.st4[i];
+    unpack_st4(s4, e);
+  }
+  wave_refill(__ballot(live), S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES,
+              e.mti, (lds_u32*)wscr);
+  int dest = -2;
+  LaneCount c{0, 0, 0, 0, 0, 0};
+  if (live) {
+    s4.w = e.mti & ~MT_STALE;
+    S.st4[i] = s4;
+    c.regens = 1;
+    const uint8_t nk = Q.nextk[j];
+    dest = nk == RO_RETIRE ? -1 : (int)nk;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new half and state before the bits
+  ro_push(Q, dest, j);
+  ro_count(Q, c);
+}
+
+template <bool AUTORESET, int POL>
+__global__ __launch_bounds__(RO_THREADS, TG_RO_MINW) void k_rollout(Soa S, int64_t n, Level L,
+                                                          const uint32_t* __restrict__ grid,
+                                                          RollIO R, EpQueue q, int64_t g0,
+                                                          int32_t E,
+                                                          unsigned long long* __restrict__ stats,
+                                                          uint32_t* __restrict__ err_or) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[RO_WAVES * WIN_WAVE_BYTES];
+  __shared__ RoLds Q;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * E;
+  const int ne = (int)(n - base < (int64_t)E ? n - base : (int64_t)E);
+  for (int w = threadIdx.x; w < RO_NQ * RO_WORDS; w += RO_THREADS) (&Q.bits[0][0])[w] = 0u;
+  if (threadIdx.x < RO_NQ) Q.cnt[threadIdx.x] = Q.cursor[threadIdx.x] = 0;
+  if (threadIdx.x == 0) Q.lock = Q.running = Q.retired = 0;
+  if (threadIdx.x < 6) Q.count[threadIdx.x] = 0ull;
+  if (threadIdx.x == 6) Q.wticks = 0ull;
+  LEVEL_IN_LDS();  // includes the barrier
+  lds_u8* const wscr = (lds_u8*)win + wave * WIN_WAVE_BYTES;
+
+  // every env's first step: its action, and the reward-None steps before one that runs
+  for (int j0 = 0; j0 < ne; j0 += RO_THREADS) {
+    const int j = j0 + (int)threadIdx.x;
+    int dest = -2;
+    LaneCount c{0, 0, 0, 0, 0, 0};
+    if (j < ne) {
+      const int64_t i = base + j;
+      Env e;
+      unpack(S.st4[i], S.ang[i], e);
+      int2 ep = S.ep[i];
+      int t = 0;
+      uint8_t nk;
+      dest = ro_advance<AUTORESET, POL>(L, m, e, ep, i, g0 + i, t, R, n, S, q, stats, nk, c);
+      if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+      if (t) {
+        S.st4[i] = pack(e);
+        S.ang[i] = make_double2(e.ang0, e.ang1);
+        S.ep[i] = ep;
+      }
+      Q.tstep[j] = (uint16_t)t;
+      Q.nextk[j] = nk;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ro_push(Q, dest, j);
+    ro_count(Q, c);
+  }
+  __syncthreads();
+
+  unsigned long long idle0 = 0;  // when this wave last found no work (0: it did find some)
+  while (true) {
+    // ---- the next work of this wave: the refill queue first, else the fullest option queue
+    // (counts read without the lock; a pop takes the lock and re-checks)
+    const int cl = lane < RO_NQ ? __hip_atomic_load(&Q.cnt[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+    const int retired = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&Q.retired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    int qsel = -1;
+    if (__builtin_amdgcn_readlane(cl, RO_REFILL) > 0) {
+      qsel = RO_REFILL;
+    } else {
+      int best = 0;
+#pragma unroll
+      for (int qq = 0; qq < O_COUNT; ++qq) {
+        const int v = __builtin_amdgcn_readlane(cl, qq);
+        if (v > best) best = v, qsel = qq;
+      }
+    }
+    if (qsel < 0) {
+      if (retired >= ne) break;
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      if (!idle0) idle0 = now;
+      if (now - idle0 > RO_STALL_TICKS) {  // cannot happen unless the bookkeeping is broken
+        if (lane == 0) {
+          atomicOr(err_or, RO_E_STALL);
+          printf("k_rollout: block %d wave %d: no work, retired %d of %d\n", (int)blockIdx.x,
+                 (int)(threadIdx.x >> 6), retired, ne);
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+      continue;
+    }
+    idle0 = 0;
+    if (qsel == RO_REFILL) {
+      if (!ro_lock(Q, err_or)) break;
+      const int take = ro_pop(Q, RO_REFILL, 64);
+      ro_unlock(Q);
+      if (take) ro_refill_batch(S, base, take, Q, wscr);
+      continue;
+    }
+#define RO_STINT(KK) ro_stint<KK, AUTORESET, POL>(S, n, L, trig, m, R, q, g0, base, ne, Q, wscr, stats, err_or)
+    switch (qsel) {
+      case O_GO_LEFT: RO_STINT(O_GO_LEFT); break;
+      case O_GO_RIGHT: RO_STINT(O_GO_RIGHT); break;
+      case O_UP_LADDER: RO_STINT(O_UP_LADDER); break;
+      case O_DOWN_LADDER: RO_STINT(O_DOWN_LADDER); break;
+      case O_INTERACT: RO_STINT(O_INTERACT); break;
+      case O_DOWN_LEFT: RO_STINT(O_DOWN_LEFT); break;
+      case O_DOWN_RIGHT: RO_STINT(O_DOWN_RIGHT); break;
+      case O_JUMP_LEFT: RO_STINT(O_JUMP_LEFT); break;
+      default: RO_STINT(O_JUMP_RIGHT); break;
+    }
+#undef RO_STINT
+  }
+  __syncthreads();  // every wave has left the loop: the workgroup's counts are final
+  if (threadIdx.x < 7) {
+    const unsigned long long v = threadIdx.x < 6 ? Q.count[threadIdx.x] : Q.wticks;
+    const int slot = threadIdx.x < 5 ? ST_STEPS + (int)threadIdx.x
+                     : threadIdx.x == 5 ? ST_REGENS : ST_WTICKS;
+    if (v) atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + slot], v);
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
                                                  const uint32_t* __restrict__ grid,
                                                  uint16_t* __restrict__ out) {
@@ -1059,7 +1536,12 @@ int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 // k_run needs one wave per 64-lane chunk of the padded worklists: at most n/64 + NSEG chunks
 int run_grid_for(int64_t n) { return grid_for(n) + (NSEG * 64 + BLOCK - 1) / BLOCK + REFILL_BLOCKS; }
 // per-block launch-counter slots cover the largest step grid
-int stat_slots(int64_t n) { return run_grid_for(n); }
+// one counter slot per workgroup of the widest step launch: k_run, or k_rollout (>= 64 envs
+// per workgroup)
+int stat_slots(int64_t n) {
+  const int64_t ro = (n + 63) / 64;
+  return ro > run_grid_for(n) ? (int)ro : run_grid_for(n);
+}
 
 int flush_timing(tg_batch* h) {
   for (size_t k = 0; k + 1 < h->ev_used; k += 2) {
@@ -1109,6 +1591,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
 
   tg_batch* h = new tg_batch();
   h->device = device;
+  h->cus = prop.multiProcessorCount;
   h->n = n;
   h->g0 = global_offset;
   h->seed0 = seed_base;
@@ -1259,6 +1742,50 @@ int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
   }
   return TG_OK;
 }
+
+// envs per k_rollout workgroup: one round of workgroups fills every CU's resident slots
+// (a second, partial round would run on a few CUs after the rest had finished); at least 64
+int32_t ro_envs_per_block(int64_t n, int slots) {
+  const int64_t e = (n + slots - 1) / slots;
+  return (int32_t)(e < 64 ? 64 : (e > RO_EMAX ? RO_EMAX : e));
+}
+
+int launch_rollout(tg_batch* h, const RollIO& R, bool ar, hipStream_t st) {
+  if (h->timing) {
+    while (h->ev.size() < h->ev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      h->ev.push_back(ev);
+    }
+    HIP_TRY(hipEventRecord(h->ev[h->ev_used], st));
+  }
+  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
+  decltype(&k_rollout<true, 0>) kern;
+  if (R.io.policy == TG_POLICY_UNIFORM)
+    kern = ar ? k_rollout<true, 0> : k_rollout<false, 0>;
+  else
+    kern = ar ? k_rollout<true, 1> : k_rollout<false, 1>;
+  if (!h->ro_per_cu) {
+    int nb = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kern),
+                                                         RO_THREADS, 0));
+    h->ro_per_cu = nb > 0 ? nb : 1;
+  }
+  const int32_t E = ro_envs_per_block(h->n, h->cus * h->ro_per_cu);
+  const dim3 grid((unsigned)((h->n + E - 1) / E)), block(RO_THREADS);
+  if ((int64_t)grid.x > (int64_t)stat_slots(h->n))
+    return fail(TG_E_INVAL, "k_rollout: %u workgroups exceed the %d counter slots", grid.x,
+                stat_slots(h->n));
+  hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, R, q, h->g0, E,
+                     h->stats, h->err);
+  HIP_TRY(hipGetLastError());
+  if (h->timing) {
+    HIP_TRY(hipEventRecord(h->ev[h->ev_used + 1], st));
+    h->ev_used += 2;
+    if (h->ev_used >= 4096) return flush_timing(h);
+  }
+  return TG_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1285,6 +1812,20 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
     if (hipMalloc((void**)&h->obs_scratch, sizeof(double) * 9 * (size_t)n) != hipSuccess)
       return fail(TG_E_NOMEM, "tg_rollout: obs scratch");
   const bool ar = (flags & TG_STEP_AUTORESET) != 0;
+  if (h->mode == TG_MODE_ASYNC) {
+    constexpr int32_t KMAX = 0xFFFF;  // k_rollout counts an env's steps in 16 bits
+    for (int32_t s0 = 0; s0 < steps; s0 += KMAX) {
+      const int32_t k = steps - s0 < KMAX ? steps - s0 : KMAX;
+      const size_t off = (size_t)s0 * (size_t)n;
+      const RollIO R{StepIO{actions ? actions + off : nullptr, obs ? obs + off * 9 : h->obs_scratch,
+                            reward + off, valid + off, done + off, nullptr, policy, action_seed,
+                            t0 + s0},
+                     k, obs != nullptr};
+      const int rc = launch_rollout(h, R, ar, (hipStream_t)stream);
+      if (rc) return rc;
+    }
+    return TG_OK;
+  }
   for (int32_t s = 0; s < steps; ++s) {
     const StepIO io{actions ? actions + (size_t)s * n : nullptr,
                     obs ? obs + (size_t)s * n * 9 : h->obs_scratch,
@@ -1349,7 +1890,7 @@ int tg_errors(tg_batch* h, uint32_t* out, void* stream) {
 
 int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
   BIND(h);
-  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT)
+  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT && mode != TG_MODE_ASYNC)
     return fail(TG_E_INVAL, "tg_set_mode: unknown mode %d", mode);
   h->mode = mode;
   (void)run_blocks;  // reserved

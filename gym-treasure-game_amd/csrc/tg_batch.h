@@ -52,7 +52,9 @@ struct tg_batch {
   tg::Level L{};
   uint32_t* grid = nullptr;  // bordered cell grid, padded to whole words
   uint32_t* genrand = nullptr;
-  uint32_t* gotab = nullptr;  // GoTable (tg_core.h go_lookup), W * H * 32 entries
+  uint32_t* gotab = nullptr;
+  int cus = 0;               // compute units (k_rollout sizes its workgroups to fill them once)
+  int ro_per_cu = 0;         // k_rollout workgroups resident per CU (occupancy API, first use)  // GoTable (tg_core.h go_lookup), W * H * 32 entries
   tg::Soa S{};
   tg_episode* eps = nullptr;
   int32_t* eps_count = nullptr;

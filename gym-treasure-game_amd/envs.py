@@ -294,7 +294,8 @@ class TreasureGameVec:
     def set_mode(self, mode="compact", run_blocks=0):
         """Step implementation: "compact" (two-pass, default) or "direct" (one lane per env
         runs in place); both are bit-identical."""
-        m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT}[mode]
+        m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT,
+             "async": _lib.TG_MODE_ASYNC}[mode]
         check(self._L.tg_set_mode(self.handle, m, int(run_blocks)), "tg_set_mode")
 
     def set_episode_capacity(self, cap):

@@ -1,0 +1,115 @@
+"""TG_MODE_ASYNC's tg_rollout (k_rollout: every env's K steps in one launch, per-workgroup
+option queues, no step barrier) against the per-step kernels, bit for bit: every output row,
+the final env states and MT streams, and the SET of completed episodes (their queue order is
+the one thing that differs).  Sizes up to the bench's 1M envs (2,048 envs per workgroup, the
+largest the LDS bitmaps hold), levels whose options cross MT generations inside one step, and
+batches that enter the rollout with stale MT halves left by tg_step."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LEVELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels")
+
+
+def episodes_sorted(vec):
+    e = vec.episodes(cap=vec.num_envs * 64).cpu().numpy()
+    return e[np.lexsort((e[:, 2], e[:, 1], e[:, 0]))] if len(e) else e
+
+
+def run_pair(tg, n, k, policy, pre_steps=0, level=None, seed=5, a0=0xA5A5, chunks=(None,)):
+    """the same batch through K x (tg_policy_actions + tg_step) and through async tg_rollout
+    (in `chunks` calls); returns both sides' outputs, final states and sorted episodes"""
+    ld = None if level is None else os.path.join(LEVELS, level)
+    sides = []
+    for mode in ("compact", "async"):
+        v = tg.TreasureGameVec(n, seed=seed, autoreset=True, mode=mode, level_dir=ld)
+        v.reset()
+        for t in range(pre_steps):  # leaves stale MT halves for the rollout to start from
+            v.step(v.policy_actions(t, a0, policy))
+        outs = []
+        if mode == "compact":
+            for t in range(pre_steps, pre_steps + k):
+                act = v.policy_actions(t, a0, policy).clone()
+                o, r, va, d, _ = v.step(act)
+                outs.append({"obs": o.clone(), "reward": r.clone(), "valid": va.clone(),
+                             "done": d.clone(), "actions": act})
+            out = {key: torch.stack([x[key] for x in outs]) for key in outs[0]}
+        else:
+            t0, parts = pre_steps, []
+            sizes = [k] if chunks == (None,) else list(chunks)
+            assert sum(sizes) == k
+            for c in sizes:
+                parts.append(v.rollout(c, t0=t0, action_seed=a0, policy=policy))
+                t0 += c
+            out = {key: torch.cat([p[key] for p in parts]) for key in parts[0]}
+        torch.cuda.synchronize()
+        sides.append((out, v.read_state(mt=True), episodes_sorted(v), v.stats(), v.errors()))
+        v.close()
+    return sides
+
+
+def check_pair(sides, n, k, errors=0):
+    (oa, sa, ea, sta, era), (ob, sb, eb, stb, erb) = sides
+    assert era == errors and erb == errors
+    for key in ("reward", "valid", "done", "actions"):
+        assert torch.equal(oa[key], ob[key]), key
+    assert torch.equal(oa["obs"].view(torch.int64), ob["obs"].view(torch.int64)), "obs"
+    for key in sa:
+        assert np.array_equal(sa[key], sb[key]), key
+    assert np.array_equal(ea, eb)
+    assert stb["steps"] >= n * k
+    for key in ("valid_steps", "ticks", "draws", "episodes"):
+        assert sta[key] == stb[key], key
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 1000, 70001])
+def test_async_rollout_ragged_batches(tg, n):
+    """batches that leave a partial workgroup / partial bitmap word; rollouts in 3 calls"""
+    k = 21
+    check_pair(run_pair(tg, n, k, "uniform", chunks=(7, 1, 13)), n, k)
+
+
+def test_async_rollout_after_steps(tg):
+    """envs enter the rollout with MT_STALE halves left by tg_step (the refill queue first)"""
+    n, k = 50000, 30
+    check_pair(run_pair(tg, n, k, "masked", pre_steps=9), n, k)
+
+
+@pytest.mark.parametrize("level", ["corridor", "gen2", "exit"])
+def test_async_rollout_levels(tg, level):
+    """corridor: go options of ~650 draws (two MT generation crossings inside one step).  Some
+    of its envs get stuck against an end wall in an option that never ends (the reference
+    would loop forever; the kernels stop at TICK_CAP and flag E_TICKCAP): both sides must
+    flag exactly that, with identical outputs"""
+    n, k = 4096, 25
+    check_pair(run_pair(tg, n, k, "uniform", level=level), n, k,
+               errors=(1 << 24) if level == "corridor" else 0)
+
+
+def test_async_rollout_no_obs_and_no_autoreset(tg):
+    """obs=None (the scratch row) and auto-reset off: the other k_rollout instantiation"""
+    n, k, a0 = 20000, 20, 77
+    res = []
+    for mode in ("compact", "async"):
+        v = tg.TreasureGameVec(n, seed=9, autoreset=False, mode=mode)
+        v.reset()
+        r = v.rollout(k, t0=0, action_seed=a0, policy="uniform", obs=False)
+        res.append((r, v.read_state(mt=True), v.observe().clone()))
+        v.close()
+    (ra, sa, oa), (rb, sb, ob) = res
+    for key in ("reward", "valid", "done", "actions"):
+        assert torch.equal(ra[key], rb[key]), key
+    for key in sa:
+        assert np.array_equal(sa[key], sb[key]), key
+    assert torch.equal(oa.view(torch.int64), ob.view(torch.int64))
+
+
+@pytest.mark.parametrize("policy", ["uniform", "masked"])
+def test_async_rollout_1m_envs(tg, policy):
+    """the bench's size: 1M envs, 2,048 per workgroup"""
+    n, k = 1 << 20, 24
+    check_pair(run_pair(tg, n, k, policy), n, k)
