@@ -966,14 +966,16 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
 // ------------------------------------------------------------------------------------------
 constexpr int RO_WAVES = 4;
 #ifndef TG_RO_MINW
-#define TG_RO_MINW 2  // waves per SIMD the register budget is sized for (launch bounds)
+#define TG_RO_MINW 3  // waves per SIMD the register budget is sized for (launch bounds)
 #endif
 constexpr int RO_THREADS = RO_WAVES * 64;
 constexpr int RO_EMAX = 2048;            // envs per workgroup: 64 bitmap words (one per lane)
 constexpr int RO_WORDS = RO_EMAX / 32;
 constexpr int RO_REFILL = O_COUNT;       // queue of envs whose stale MT half comes first
-constexpr int RO_NQ = O_COUNT + 1;
+constexpr int RO_NEXT = O_COUNT + 1;     // queue of envs whose next step is to be evaluated
+constexpr int RO_NQ = O_COUNT + 2;
 constexpr uint8_t RO_RETIRE = 0xFF;      // nextk: the env has done its K steps
+constexpr uint8_t RO_TONEXT = 0xFE;      // nextk: after the refill, on to RO_NEXT
 constexpr uint32_t RO_E_STALL = 1u << 31;  // err bit: a workgroup's waves found no work (bug)
 constexpr unsigned long long RO_STALL_TICKS = 200000000ull;  // 2 s of the 100 MHz clock without progress
 static_assert(RO_WORDS == 64, "one bitmap word per lane");
@@ -1164,118 +1166,39 @@ __device__ __forceinline__ int ro_pop(RoLds& Q, int qsel, int want) {
   return take;
 }
 
-constexpr int RO_REFILL_T = 16;  // a stint refills its idle lanes once this many are idle
-constexpr int RO_BACKOFF = 8;    // rounds before popping again after the queue ran dry
-#ifndef TG_RO_WTICKS
-#define TG_RO_WTICKS 1           // count wave-ticks (lane efficiency) in the stints
-#endif
-
-// One stint of a wave on option K: its lanes run option K for envs popped from queue K; a lane
-// whose option ends waits (pend) until RO_REFILL_T lanes are idle, then those are finished
-// together (finish_step, the next step's action, push) and refilled from the queue.  Returns
-// when no lane is in flight and the queue is empty.  All 64 lanes.
-template <int K, bool AUTORESET, int POL>
-__device__ __forceinline__ void ro_stint(const Soa& S, int64_t n, const Level& L,
-                                         const uint32_t* trig, const Map& m, const RollIO& R,
-                                         const EpQueue& q, int64_t g0, int64_t base, int ne,
-                                         RoLds& Q, lds_u8* wscr, unsigned long long* stats,
-                                         uint32_t* err_or) {
+// the queued envs' next steps (ro_advance: the policy's action, can_run, reward-None steps
+// finished on the spot), then on to their option's queue.  All 64 lanes; `take` envs staged.
+template <bool AUTORESET, int POL>
+__device__ __forceinline__ void ro_next_batch(const Soa& S, int64_t n, const Level& L,
+                                              const Map& m, const RollIO& R, const EpQueue& q,
+                                              int64_t g0, int64_t base, int take, RoLds& Q,
+                                              unsigned long long* stats, uint32_t* err_or) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  bool act = false, pend = false;
-  int j = 0, lim = 0;
-  Env e;
-  e.px = e.py = e.kx = e.ky = e.gx = e.gy = 0;
-  e.f = e.mti = 0u;
-  e.ang0 = e.ang1 = 0.0;
-  Opt o{0, false, false};
-  StepResult r{0, 0, 0, 0};
-  RngCodes rng(S.mt, S.mc, 0u, wscr);
-  int backoff = 0;  // wave-uniform
-  unsigned long long wticks = 0;
-  (void)wticks;
-  (void)ne;
-  while (true) {
-    const unsigned long long am = __ballot(act);
-    const int nact = __popcll(am);
-    if (nact == 0 || (64 - nact >= RO_REFILL_T && backoff == 0)) {
-      // ---- finish the lanes whose option has ended
-      LaneCount c{0, 0, 0, 0, 0, 0};
-      int dest = -2;
-      if (pend) {
-        const int64_t i = base + j;
-        int2 ep = S.ep[i];
-        int t = Q.tstep[j];
-        r.done = is_done(e);
-        finish_step<AUTORESET, false>(L, e, rng, i, r, ep, step_io(R, t, n));
-        e.mti = rng.finish();
-        c.steps = c.valid = 1;
-        c.ticks = r.ticks;
-        c.draws = (int)rng.draws;
-        c.regens = (int)rng.regens;
-        ++t;
-        if (AUTORESET && r.done) {
-          record_episode_lane(g0 + i, ep, q, stats);
-          c.episodes = 1;
-        }
-        uint8_t nk;
-        dest = ro_advance<AUTORESET, POL>(L, m, e, ep, i, g0 + i, t, R, n, S, q, stats, nk, c);
-        if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
-        S.st4[i] = pack(e);
-        S.ang[i] = make_double2(e.ang0, e.ang1);
-        S.ep[i] = ep;
-        Q.tstep[j] = (uint16_t)t;
-        Q.nextk[j] = nk;
-        pend = false;
-      }
-      if (__ballot(dest != -2)) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the envs' stores before their bits
-        ro_push(Q, dest, j);
-        ro_count(Q, c);
-      }
-      // ---- new envs for the idle lanes
-      int take = 0;
-      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&Q.cnt[K], __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP)) > 0) {
-        if (!ro_lock(Q, err_or)) return;
-        take = ro_pop(Q, K, 64 - nact);
-        ro_unlock(Q);
-      }
-      if (take) {
-        const unsigned long long below = (1ull << lane) - 1ull;
-        const int rank = __popcll(~am & below);
-        if (!act && rank < take) {
-          j = Q.stage[wave][rank];
-          const int64_t i = base + j;
-          unpack(S.st4[i], S.ang[i], e);
-          o = Opt{0, false, false};
-          r = StepResult{0, 1, 0, 0};
-          lim = round_no_span(K);
-          rng = RngCodes(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
-          rng.prime();
-          act = true;
-        }
-        backoff = 0;
-      } else {
-        backoff = RO_BACKOFF;
-      }
-      if (!__ballot(act)) break;
-    } else if (backoff) {
-      --backoff;
+  const bool live = lane < take;
+  const int j = live ? (int)Q.stage[wave][lane] : 0;
+  int dest = -2;
+  LaneCount c{0, 0, 0, 0, 0, 0};
+  if (live) {
+    const int64_t i = base + j;
+    Env e;
+    unpack(S.st4[i], S.ang[i], e);
+    int2 ep = S.ep[i];
+    int t = Q.tstep[j];
+    const int t0 = t;
+    uint8_t nk;
+    dest = ro_advance<AUTORESET, POL>(L, m, e, ep, i, g0 + i, t, R, n, S, q, stats, nk, c);
+    if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+    if (t != t0) {
+      S.st4[i] = pack(e);
+      S.ang[i] = make_double2(e.ang0, e.ang1);
+      S.ep[i] = ep;
+      Q.tstep[j] = (uint16_t)t;
     }
-#if TG_RO_WTICKS
-    const int tb = r.ticks;
-#endif
-    if (act && run_round_k<K>(L, trig, m, e, rng, r, o, lim)) {
-      act = false;
-      pend = true;
-    }
-#if TG_RO_WTICKS
-    wticks += (unsigned long long)wave_max(act || pend ? r.ticks - tb : 0);
-#endif
+    Q.nextk[j] = nk;
   }
-#if TG_RO_WTICKS
-  if (lane == 0 && wticks) atomicAdd(&Q.wticks, wticks);
-#endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the envs' stores before their bits
+  ro_push(Q, dest, j);
+  ro_count(Q, c);
 }
 
 // the queued envs' stale MT halves, regenerated with the whole wave (wave_refill), then on to
@@ -1302,7 +1225,7 @@ __device__ __forceinline__ void ro_refill_batch(const Soa& S, int64_t base, int 
     S.st4[i] = s4;
     c.regens = 1;
     const uint8_t nk = Q.nextk[j];
-    dest = nk == RO_RETIRE ? -1 : (int)nk;
+    dest = nk == RO_RETIRE ? -1 : nk == RO_TONEXT ? RO_NEXT : (int)nk;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new half and state before the bits
   ro_push(Q, dest, j);
@@ -1359,23 +1282,42 @@ __global__ __launch_bounds__(RO_THREADS, TG_RO_MINW) void k_rollout(Soa S, int64
 
   unsigned long long idle0 = 0;  // when this wave last found no work (0: it did find some)
   while (true) {
-    // ---- the next work of this wave: the refill queue first, else the fullest option queue
-    // (counts read without the lock; a pop takes the lock and re-checks)
+    // ---- the next batch of this wave (counts polled without the lock; the pop re-reads them
+    // under it).  Full 64-env batches of one option while the queues hold them, so a wave's
+    // lanes start together (their plain-tick spans stay in step); partial ones when the
+    // workgroup runs low.
     const int cl = lane < RO_NQ ? __hip_atomic_load(&Q.cnt[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
     const int retired = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(&Q.retired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    const int running = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&Q.running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     int qsel = -1;
-    if (__builtin_amdgcn_readlane(cl, RO_REFILL) > 0) {
-      qsel = RO_REFILL;
-    } else {
-      int best = 0;
+    {
+      int total = 0, best = 0, bk = -1;
 #pragma unroll
       for (int qq = 0; qq < O_COUNT; ++qq) {
         const int v = __builtin_amdgcn_readlane(cl, qq);
-        if (v > best) best = v, qsel = qq;
+        total += v;
+        if (v > best) best = v, bk = qq;
       }
+      const int rf = __builtin_amdgcn_readlane(cl, RO_REFILL);
+      const int nx = __builtin_amdgcn_readlane(cl, RO_NEXT);
+      const bool few_running = running < RO_WAVES / 2;
+      if (rf > 0 && (rf >= 8 || few_running || best < 64))
+        qsel = RO_REFILL;
+      else if (nx > 0 && (nx >= 64 || few_running || best < 64))
+        qsel = RO_NEXT;
+      else if (bk >= 0 && (best >= 64 || 4 * best >= total || few_running))
+        qsel = bk;
     }
-    if (qsel < 0) {
+    int take = 0;
+    if (qsel >= 0) {
+      if (!ro_lock(Q, err_or)) break;
+      take = ro_pop(Q, qsel, 64);
+      if (take && lane == 0) atomicAdd(&Q.running, 1);
+      ro_unlock(Q);
+    }
+    if (take == 0) {
       if (retired >= ne) break;
       const unsigned long long now = __builtin_amdgcn_s_memrealtime();
       if (!idle0) idle0 = now;
@@ -1387,30 +1329,73 @@ __global__ __launch_bounds__(RO_THREADS, TG_RO_MINW) void k_rollout(Soa S, int64
         }
         break;
       }
-      __builtin_amdgcn_s_sleep(8);
+      __builtin_amdgcn_s_sleep(2);
       continue;
     }
     idle0 = 0;
     if (qsel == RO_REFILL) {
-      if (!ro_lock(Q, err_or)) break;
-      const int take = ro_pop(Q, RO_REFILL, 64);
-      ro_unlock(Q);
-      if (take) ro_refill_batch(S, base, take, Q, wscr);
+      ro_refill_batch(S, base, take, Q, wscr);
+      if (lane == 0) atomicSub(&Q.running, 1);
       continue;
     }
-#define RO_STINT(KK) ro_stint<KK, AUTORESET, POL>(S, n, L, trig, m, R, q, g0, base, ne, Q, wscr, stats, err_or)
-    switch (qsel) {
-      case O_GO_LEFT: RO_STINT(O_GO_LEFT); break;
-      case O_GO_RIGHT: RO_STINT(O_GO_RIGHT); break;
-      case O_UP_LADDER: RO_STINT(O_UP_LADDER); break;
-      case O_DOWN_LADDER: RO_STINT(O_DOWN_LADDER); break;
-      case O_INTERACT: RO_STINT(O_INTERACT); break;
-      case O_DOWN_LEFT: RO_STINT(O_DOWN_LEFT); break;
-      case O_DOWN_RIGHT: RO_STINT(O_DOWN_RIGHT); break;
-      case O_JUMP_LEFT: RO_STINT(O_JUMP_LEFT); break;
-      default: RO_STINT(O_JUMP_RIGHT); break;
+    if (qsel == RO_NEXT) {
+      ro_next_batch<AUTORESET, POL>(S, n, L, m, R, q, g0, base, take, Q, stats, err_or);
+      if (lane == 0) atomicSub(&Q.running, 1);
+      continue;
     }
-#undef RO_STINT
+    // ---- one step of option qsel for every popped env
+    const int k = qsel;
+    const bool live = lane < take;
+    const int j = live ? (int)Q.stage[wave][lane] : 0;
+    const int64_t i = base + j;
+    int dest = -2;
+    LaneCount c{0, 0, 0, 0, 0, 0};
+    StepResult r{0, 0, 0, 0};
+    if (live) {
+      Env e;
+      unpack(S.st4[i], S.ang[i], e);
+      int2 ep = S.ep[i];
+      int t = Q.tstep[j];
+      RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
+      rng.prime();
+#if TG_PRIO_SLOW
+      if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(TG_PRIO_SLOW);
+#endif
+      run_option(L, trig, m, e, k, rng, r);
+#if TG_PRIO_SLOW
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      r.done = is_done(e);
+      finish_step<AUTORESET, false>(L, e, rng, i, r, ep, step_io(R, t, n));
+      e.mti = rng.finish();
+      c.steps = c.valid = 1;
+      c.ticks = r.ticks;
+      c.draws = (int)rng.draws;
+      c.regens = (int)rng.regens;
+      ++t;
+      if (AUTORESET && r.done) {
+        record_episode_lane(g0 + i, ep, q, stats);
+        c.episodes = 1;
+      }
+      // the next step is evaluated by a RO_NEXT batch (kept out of this code path: its
+      // registers would add to the option loops')
+      const uint8_t nk = t >= R.steps ? RO_RETIRE : RO_TONEXT;
+      dest = (e.mti & MT_STALE) ? RO_REFILL : nk == RO_RETIRE ? -1 : RO_NEXT;
+      if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+      S.st4[i] = pack(e);
+      S.ang[i] = make_double2(e.ang0, e.ang1);
+      S.ep[i] = ep;
+      Q.tstep[j] = (uint16_t)t;
+      Q.nextk[j] = nk;
+    }
+    const int wt = wave_max(r.ticks);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the envs' stores before their bits
+    ro_push(Q, dest, j);
+    ro_count(Q, c);
+    if (lane == 0) {
+      if (wt) atomicAdd(&Q.wticks, (unsigned long long)wt);
+      atomicSub(&Q.running, 1);
+    }
   }
   __syncthreads();  // every wave has left the loop: the workgroup's counts are final
   if (threadIdx.x < 7) {

@@ -7,6 +7,6 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_rollout.py -x -v --timeout 
 tail -15 gpurun_out/ro_t.log
 [ $rc -eq 0 ] || exit $rc
 [ "${AB:-1}" = 1 ] || exit 0
-timeout -k 10 300 python -u scripts/ro_ab.py > gpurun_out/ro_ab.log 2>&1; rc=$?
+timeout -k 10 300 python -u scripts/ro_ab.py ${RO_ARGS:-} > gpurun_out/ro_ab.log 2>&1; rc=$?
 tail -60 gpurun_out/ro_ab.log
 exit $rc
