@@ -117,7 +117,10 @@ __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t CODE_CHUNKS = MT_CODES / 16;  // 39
 static_assert(MT_CODES % 16 == 0, "whole 16-B code chunks per env");
-constexpr int WIN_CHUNKS = 7;
+#ifndef TG_WIN_CHUNKS
+#define TG_WIN_CHUNKS 7
+#endif
+constexpr int WIN_CHUNKS = TG_WIN_CHUNKS;
 constexpr int WIN_SLOT_BYTES = 64 * 16;
 constexpr int WIN_WAVE_BYTES = WIN_CHUNKS * WIN_SLOT_BYTES;  // 7 KB per wave
 constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
@@ -815,8 +818,13 @@ __device__ unsigned long long g_stamps[(1 << 16) * 6];  // per wave: 4 durations
 #define TG_STAMP(v) (void)0
 #endif
 
+#ifdef TG_RUN_MINW  // waves per SIMD k_run's register budget is sized for (A/B builds)
+#define TG_RUN_BOUNDS __launch_bounds__(BLOCK, TG_RUN_MINW)
+#else
+#define TG_RUN_BOUNDS __launch_bounds__(BLOCK)
+#endif
 template <bool AUTORESET, bool FINAL>
-__global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
+__global__ TG_RUN_BOUNDS void k_run(Soa S, int64_t n, Level L,
                                                 const uint32_t* __restrict__ grid, StepIO io,
                                                 EpQueue q, Work w, int64_t g0,
                                                 unsigned long long* __restrict__ stats,

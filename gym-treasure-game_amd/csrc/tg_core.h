@@ -1084,58 +1084,6 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
     }
   } while (!o.done);
 }
-// One round of option K's loop, for the device's lane-refilling rollout (k_rollout), which
-// keeps an option's state across rounds and swaps finished lanes for new envs between them:
-// for go and ladders, the plain ticks of the current span and then one full tick; else one
-// tick.  Returns true when the option has ended (o.done, or TICK_CAP).  Start with
-// r.ran = 1, o = {0, false, false}, lim = round_no_span(K).  Per lane the rounds replay
-// run_option_k's tick sequence exactly (the same code, cut at its loop's back-edge).
-TG_HD int round_no_span(int k) {
-  return (k == O_GO_RIGHT || k == O_DOWN_LADDER) ? -0x40000000 : 0x40000000;
-}
-template <int K, class R>
-TG_HD bool run_round_k(const Level& L, const uint32_t* trig, const Map& m, Env& e, R& rng,
-                       StepResult& r, Opt& o, int& lim) {
-  if constexpr (K == O_GO_LEFT || K == O_GO_RIGHT || K == O_UP_LADDER || K == O_DOWN_LADDER) {
-    constexpr bool GO = K == O_GO_LEFT || K == O_GO_RIGHT;
-    constexpr int DIR = (K == O_GO_LEFT || K == O_UP_LADDER) ? -1 : 1;
-    while ((DIR > 0 ? (GO ? e.px : e.py) <= lim : (GO ? e.px : e.py) >= lim) &&
-           rng.has(TICK_DRAWS)) {  // a plain tick
-      if (GO) {
-        e.px += code_step(rng.code(), DIR < 0);
-        e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
-      } else {
-        e.py += code_step(rng.code(), DIR < 0);
-      }
-      r.reward += -1;
-      const int v = GO ? e.px : e.py;
-      if (DIR > 0 ? v > lim : v < lim) pickups(L, e);  // left the span: as the full tick
-      if (++r.ticks >= TICK_CAP) {
-        e.f |= E_TICKCAP;
-        return true;
-      }
-    }
-    rng.reserve(TICK_DRAWS);
-    const int prim = policy<K>(L, m, e, o);
-    r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
-    if (!o.done) lim = GO ? go_plain_limit<DIR>(m, e, o.tx) : ladder_plain_limit<DIR>(m, e);
-  } else {
-    rng.reserve(TICK_DRAWS);
-    if ((K == O_JUMP_LEFT || K == O_JUMP_RIGHT || K == O_DOWN_LEFT || K == O_DOWN_RIGHT) &&
-        o.init) {
-      r.reward += air_tick<K>(L, m, e, o, rng);
-    } else {
-      const int prim = policy<K>(L, m, e, o);
-      r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
-    }
-  }
-  if (++r.ticks >= TICK_CAP) {
-    e.f |= E_TICKCAP;
-    return true;
-  }
-  return o.done;
-}
-
 template <class R>
 TG_HD void run_option(const Level& L, const uint32_t* trig, const Map& m, Env& e, int k,
                       R& rng, StepResult& r) {

@@ -41,7 +41,6 @@ def hostcheck():
     L.hc_run.argtypes = [P, P, P, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                          ctypes.c_uint64, ctypes.c_int, ctypes.c_int] + [P] * 8
     L.hc_set_gotab.argtypes = [ctypes.c_int]
-    L.hc_set_rounds.argtypes = [ctypes.c_int]
     L.hc_predicates.restype = ctypes.c_uint
     L.hc_predicates.argtypes = [ctypes.c_int] * 3
     L.hc_predicate_table.argtypes = [ctypes.c_int] * 4 + [ctypes.c_uint, P]

@@ -33,50 +33,11 @@ uint64_t rec_hash(uint64_t h, const double o[9], int32_t r, int v, int d) {
 }
 }  // namespace
 
-namespace {
-// options run as run_option_k (0, default) or as k_rollout's resumable rounds (1)
-static int g_rounds = 0;
-template <int K>
-static void run_rounds(const Level& L, const uint32_t* trig, const Map& m, Env& e, Rng& rng,
-                       StepResult& r) {
-  r.ran = 1;
-  Opt o{0, false, false};
-  int lim = round_no_span(K);
-  while (!run_round_k<K>(L, trig, m, e, rng, r, o, lim)) {
-  }
-}
-static StepResult step_env(const Level& L, const uint32_t* trig, const Map& m, Env& e, int a,
-                           Rng& rng) {
-  if (!g_rounds) return env_step(L, trig, m, e, a, rng);
-  StepResult r{0, 0, 0, 0};
-  const int k = option_index(a);
-  if (k < 0) {
-    e.f |= E_ACTION;
-  } else if (can_run(L, m, e, k)) {
-    switch (k) {
-      case O_GO_LEFT: run_rounds<O_GO_LEFT>(L, trig, m, e, rng, r); break;
-      case O_GO_RIGHT: run_rounds<O_GO_RIGHT>(L, trig, m, e, rng, r); break;
-      case O_UP_LADDER: run_rounds<O_UP_LADDER>(L, trig, m, e, rng, r); break;
-      case O_DOWN_LADDER: run_rounds<O_DOWN_LADDER>(L, trig, m, e, rng, r); break;
-      case O_INTERACT: run_rounds<O_INTERACT>(L, trig, m, e, rng, r); break;
-      case O_DOWN_LEFT: run_rounds<O_DOWN_LEFT>(L, trig, m, e, rng, r); break;
-      case O_DOWN_RIGHT: run_rounds<O_DOWN_RIGHT>(L, trig, m, e, rng, r); break;
-      case O_JUMP_LEFT: run_rounds<O_JUMP_LEFT>(L, trig, m, e, rng, r); break;
-      default: run_rounds<O_JUMP_RIGHT>(L, trig, m, e, rng, r); break;
-    }
-  }
-  r.done = is_done(e);
-  return r;
-}
-
-}  // namespace
-
 extern "C" {
 
 // go_left / go_right answered from the GoTable as on the device (1, default) or directly (0)
 static int g_gotab = 1;
 void hc_set_gotab(int on) { g_gotab = on; }
-void hc_set_rounds(int on) { g_rounds = on; }
 
 static bool load_level(const char* dom, const char* objs, const char* inter, Level& L,
                        std::vector<uint8_t>& grid, std::vector<uint32_t>& tab) {
@@ -151,7 +112,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
       }
       e.mti = refill_after(mt.data(), e.mti);  // the classify pass: last step's stale half
       Rng rng(mt.data(), e.mti);  // per step, as each launch
-      const StepResult r = step_env(*L, trig, m, e, a, rng);
+      const StepResult r = env_step(*L, trig, m, e, a, rng);
       nt += r.ticks;
       observe(*L, e, fo);
       memcpy(o, fo, sizeof o);
@@ -287,7 +248,7 @@ int hc_render_run(const char* dom, const char* objs, const char* inter, uint64_t
       }
       e.mti = refill_after(mt.data(), e.mti);
       Rng rng(mt.data(), e.mti);
-      const StepResult r = step_env(*L, trig, m, e, a, rng);
+      const StepResult r = env_step(*L, trig, m, e, a, rng);
       if (autoreset && r.done) reset_env(*L, e, rng);
       e.mti = rng.finish();
     }

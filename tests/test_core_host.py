@@ -166,31 +166,3 @@ def test_core_gotable_matches_direct(hostcheck, level, policy):
     assert_same(direct, table)
     np.testing.assert_array_equal(direct["ticks"], table["ticks"])
 
-
-@pytest.mark.parametrize("level", [None, "corridor", "gen1", "exit"])
-@pytest.mark.parametrize("policy", [0, 1])
-def test_core_rounds_match_run_option(hostcheck, level, policy):
-    """k_rollout's resumable option rounds (tg_core.h run_round_k, cut at run_option_k's loop
-    back-edge) replay run_option_k tick for tick: same outputs, draws and tick counts."""
-    ld = None if level is None else os.path.join(LEVELS, level)
-    whole = hc_run(hostcheck, 13, 0, 256, 60, 0xD1CE, policy, True, level_dir=ld)
-    try:
-        hostcheck.hc_set_rounds(1)
-        rounds = hc_run(hostcheck, 13, 0, 256, 60, 0xD1CE, policy, True, level_dir=ld)
-    finally:
-        hostcheck.hc_set_rounds(0)
-    assert_same(whole, rounds)
-    np.testing.assert_array_equal(whole["ticks"], rounds["ticks"])
-
-
-def test_core_rounds_vs_golden(hostcheck):
-    """the rounds against the reference's own trajectories"""
-    d = golden("traj_masked.npz")
-    n, t1 = d["valid"].shape
-    try:
-        hostcheck.hc_set_rounds(1)
-        o = hc_run(hostcheck, int(d["seed_base"]), 0, n, t1 - 1, int(d["action_seed"]), 1, False)
-    finally:
-        hostcheck.hc_set_rounds(0)
-    g = {k: d[k] for k in ("obs", "final_obs", "reward", "valid", "done")}
-    assert_same(o, g, keys=list(g))
