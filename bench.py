@@ -115,6 +115,25 @@ def parse(argv=None):
 
 
 # ---- CPU legs (the oracle is loaded here only: bench's cpu_baseline leg) ------------------
+def dropin_latency(tg, steps=300, seed=0):
+    """The N=1 drop-in's own hot call: TreasureGame.step(a) (TG/:91-96) from Python, one env
+    on the GPU (tg_step1: one launch, the row written into pinned host memory, one sync),
+    uniform random actions from a host RNG, resetting when done.  Mean µs per call."""
+    import random
+    env = tg.TreasureGame(seed=seed)
+    env.reset()
+    r = random.Random(seed)
+    for _ in range(20):
+        env.step(r.randrange(9))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if env.step(r.randrange(9))[2]:
+            env.reset()
+    dt = time.perf_counter() - t0
+    return {"step_us": dt / steps * 1e6, "steps": steps,
+            "api": "TreasureGame.step (tg_step1), host RNG actions, synchronous"}
+
+
 def cpu_baseline(seconds, policy, parity_envs=0):
     """The C oracle (oracle/, the CPU restatement of the reference) on this box's host cores:
     a bounded sample of the same workload (same seeds, action stream and auto-reset).  Also
@@ -511,6 +530,7 @@ def main():
         sec["episodes"] = n2["episodes"]
         r2.vec.close()
         line[other + "_policy"] = sec
+        line["dropin_n1"] = dropin_latency(tg)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         if c5:
@@ -522,6 +542,9 @@ def main():
                 cb["reference_python"] = python_baseline(min(args.cpu_seconds, 10.0), args.policy)
             except ImportError:
                 cb["reference_python"] = None
+            if cb["reference_python"] and "dropin_n1" in line:  # the same call, on one core
+                line["dropin_n1"]["reference_python_step_us"] = \
+                    1e6 / cb["reference_python"]["value_1proc"]
             line["cpu_baseline"] = cb
             got, gerr = gpu_hashes(tg, pe, steps_h, args.policy, args.mode, dev)
             bad = int(np.count_nonzero(got != ref_h))

@@ -27,7 +27,7 @@ OBS_DIM = 9
 NUM_ACTIONS = 9
 
 # every symbol include/tg_amd.h declares (tests check the library exports all of them)
-EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_rollout",
+EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_step1", "tg_rollout",
            "tg_available_mask",
            "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing",
            "tg_set_episode_capacity", "tg_predicate_table",
@@ -76,6 +76,7 @@ def load():
         "tg_num_envs": (i64, [P]),
         "tg_reset": (i32, [P, P, P, P]),
         "tg_step": (i32, [P, P, P, P, P, P, P, u32, P]),
+        "tg_step1": (i32, [P, i32, P, P, P, P, P]),
         "tg_rollout": (i32, [P, i32, u64, i64, i32, u32, P, P, P, P, P, P]),
         "tg_available_mask": (i32, [P, P, P]),
         "tg_observe": (i32, [P, P, P]),

@@ -582,7 +582,9 @@ __device__ __forceinline__ void store_obs_wave(double* __restrict__ out, int64_t
 }
 
 // ---- one-pass step: one lane per env, the option runs in place (TG_MODE_DIRECT) ----------
-// POL: -1 actions given; else the TG_POLICY_* evaluated here (tg_rollout).  A template
+constexpr int POL_IMMEDIATE = -2;  // k_step's action is io.a0 (tg_step1), not an array entry
+// POL: -1 actions given; POL_IMMEDIATE one action for all (tg_step1); else the TG_POLICY_*
+// evaluated here (tg_rollout).  A template
 // parameter, so the per-step kernels carry none of the policy's code or registers.
 template <bool AUTORESET, bool FINAL, int POL = -1>
 __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
@@ -609,6 +611,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     if constexpr (POL >= 0) {
       act = policy_action(L, m, e, POL, io.a0, g0 + i, io.t);
       if (io.actions) io.actions[i] = act;
+    } else if constexpr (POL == POL_IMMEDIATE) {
+      act = (int)(int64_t)io.a0;  // tg_step1: the action is a kernel argument
     } else {
       act = io.actions[i];
     }
@@ -1662,6 +1666,7 @@ void tg_destroy(tg_batch* h) {
                   h->wctr,  h->refill,  h->nrefill,   h->obs_scratch};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  if (h->one) (void)hipHostFree(h->one);
   delete h;
 }
 
@@ -1790,6 +1795,32 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
     return fail(TG_E_INVAL, "tg_step: actions/obs/reward/valid/done are required");
   const StepIO io{const_cast<int32_t*>(actions), obs, reward, valid, done, final_obs, -1, 0, 0};
   return launch_step(h, io, (flags & TG_STEP_AUTORESET) != 0, (hipStream_t)stream);
+}
+
+int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t* valid,
+             uint8_t* done, void* stream) {
+  BIND(h);
+  if (h->n != 1 || !obs || !reward || !valid || !done)
+    return fail(TG_E_INVAL, "tg_step1: a 1-env handle and host obs/reward/valid/done");
+  if (!h->one) {  // the step's row, written by the kernel straight into pinned host memory
+    if (hipHostMalloc((void**)&h->one, sizeof(TgOne), hipHostMallocMapped) != hipSuccess)
+      return fail(TG_E_NOMEM, "tg_step1: pinned result buffer");
+    HIP_TRY(hipHostGetDevicePointer((void**)&h->one_dev, h->one, 0));
+  }
+  hipStream_t st = (hipStream_t)stream;
+  TgOne* const d = h->one_dev;
+  const StepIO io{nullptr, d->obs, &d->reward, &d->valid, &d->done, nullptr, POL_IMMEDIATE,
+                  (uint64_t)(int64_t)action, 0};
+  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
+  hipLaunchKernelGGL((k_step<false, false, POL_IMMEDIATE>), dim3(1), dim3(BLOCK), 0, st, h->S,
+                     h->n, h->L, h->grid, io, q, h->g0, h->stats, h->err);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  memcpy(obs, h->one->obs, sizeof h->one->obs);
+  *reward = h->one->reward;
+  *valid = h->one->valid;
+  *done = h->one->done;
+  return TG_OK;
 }
 
 int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int policy,

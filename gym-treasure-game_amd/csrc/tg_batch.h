@@ -38,6 +38,13 @@ struct Soa {
   uint8_t* mc;    // [N][MT_CODES]: the draw codes of both generations (tg_core.h draw_code)
 };
 
+// tg_step1's result row (one env)
+struct TgOne {
+  double obs[9];
+  int32_t reward;
+  uint8_t valid, done;
+};
+
 struct RenderState;  // tg_render.hip
 void render_free(RenderState* rs);
 
@@ -77,6 +84,8 @@ struct tg_batch {
   double kernel_ms_done = 0.0;
   std::string domain;              // domain.txt text (the renderer's cell sprites)
   double* obs_scratch = nullptr;   // tg_rollout without an obs output
+  tg::TgOne* one = nullptr;            // tg_step1's row: pinned host memory the kernel writes
+  tg::TgOne* one_dev = nullptr;        //   (its device-side address)
   tg::RenderState* rs = nullptr;   // tg_render_init
 };
 

@@ -465,7 +465,8 @@ class TreasureGame:
         self.action_space = Discrete(_lib.NUM_ACTIONS)
         self.observation_space = Box(np.float32(0.0), np.float32(1.0), shape=(_lib.OBS_DIM,))
         self.viewer = None
-        self._act = torch.empty(1, dtype=torch.int32, device=self._vec.device)
+        self._h_obs = np.zeros(_lib.OBS_DIM, np.float64)  # tg_step1's host outputs
+        self._h_rew, self._h_valid, self._h_done = ctypes.c_int32(), ctypes.c_uint8(), ctypes.c_uint8()
 
     def reset(self):
         return self._vec.reset().cpu().numpy()[0].tolist()
@@ -479,14 +480,14 @@ class TreasureGame:
         return np.array([(m >> k) & 1 for k in range(_lib.NUM_ACTIONS)])
 
     def _run(self, a):
-        """option_list[a].run() on the device + get_state + done (TG/:91-96)"""
-        self._act.fill_(a)
-        obs, rew, valid, done, _ = self._vec.step(self._act)
-        packed = torch.cat([obs[0], rew.to(torch.float64), valid.to(torch.float64),
-                            done.to(torch.float64)]).cpu().numpy()
-        state = packed[:9].tolist()
-        r = int(packed[9]) if packed[10] else None
-        return state, r, bool(packed[11])
+        """option_list[a].run() on the device + get_state + done (TG/:91-96): tg_step1, one
+        launch whose kernel writes the row into pinned host memory, one synchronisation"""
+        v = self._vec
+        check(v._L.tg_step1(v.handle, int(a), self._h_obs.ctypes.data, ctypes.byref(self._h_rew),
+                            ctypes.byref(self._h_valid), ctypes.byref(self._h_done),
+                            v._stream()), "tg_step1")
+        r = int(self._h_rew.value) if self._h_valid.value else None
+        return self._h_obs.tolist(), r, bool(self._h_done.value)
 
     def step(self, action):
         a = operator.index(action)  # list indexing accepts ints only (TG/:92)
