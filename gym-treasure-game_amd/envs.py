@@ -444,7 +444,13 @@ class TreasureGame:
     ``observation_space`` Box(0, 1, (9,), float32), ``option_names``.  ``TreasureGame(seed=s)``
     equals ``random.seed(s); TreasureGame()`` in a fresh reference process; ``seed=None``
     draws a seed from Python's global ``random`` (so ``random.seed`` still makes runs
-    reproducible, but not draw-for-draw identical to the reference's shared stream).
+    reproducible, but not draw-for-draw identical to the reference's shared stream), unless
+    ``share_global_random=True``: then the env draws from Python's global ``random`` itself,
+    as the reference's module-level ``random`` calls do (IM/:2, OB/): its MT state is loaded
+    from ``random.getstate()`` before every call that draws (construction, ``reset``, ``step``,
+    ``option.run``) when the global stream has moved, and stored back after, so user code that
+    interleaves its own ``random`` calls sees the reference's stream draw for draw (one
+    device round trip per call; the global ``gauss_next`` must be unset, as after ``seed``).
     ``render(mode='rgb_array')`` returns the frame as a uint8 numpy array [624, 672, 3]
     (TG/:98-105; the sprites are the installed reference's unless ``sprites=`` is given);
     ``mode='human'`` needs gym's image viewer and raises.
@@ -452,14 +458,19 @@ class TreasureGame:
 
     metadata = {"render.modes": ["human", "rgb_array"]}
 
-    def __init__(self, seed=None, device=None, level_dir=None, sprites=None):
+    def __init__(self, seed=None, device=None, level_dir=None, sprites=None,
+                 share_global_random=False):
         self._sprites = sprites
+        self._shared = bool(share_global_random)
+        if self._shared and seed is not None:
+            raise ValueError("share_global_random draws from the global random: no seed")
         if seed is None:
-            seed = random.getrandbits(64)
+            seed = 0 if self._shared else random.getrandbits(64)
         seed = abs(int(seed))  # random.seed(s) keys on abs(s) (CPython random_seed)
         if seed >= 2**64:
             raise ValueError("seed must satisfy |seed| < 2**64 (a two-word init_by_array key)")
         self._vec = TreasureGameVec(1, seed=seed, device=device, level_dir=level_dir)
+        self._gstate = None  # the global random state this env last stored
         self.option_list = [GpuOption(self, k) for k in range(_lib.NUM_ACTIONS)]
         self.option_names = list(OPTION_NAMES)
         self.action_space = Discrete(_lib.NUM_ACTIONS)
@@ -468,8 +479,37 @@ class TreasureGame:
         self._h_obs = np.zeros(_lib.OBS_DIM, np.float64)  # tg_step1's host outputs
         self._h_rew, self._h_valid, self._h_done = ctypes.c_int32(), ctypes.c_uint8(), ctypes.c_uint8()
 
+        if self._shared:  # _TreasureGameImpl.__init__'s build draws from the global stream
+            self._load_global(force=True)
+            self._vec.reset()
+            self._store_global()
+
+    # -- the reference's shared module-level random stream (share_global_random=True) ----------
+    def _load_global(self, force=False):
+        st = random.getstate()
+        if not force and st == self._gstate:
+            return  # nobody drew from the global stream since this env stored it
+        if st[2] is not None:
+            raise NotImplementedError("share_global_random: the global random holds a cached "
+                                      "gauss value (random.gauss was called an odd number of times)")
+        snap = self._vec.read_state(mt=True)
+        snap["mt"][0] = np.asarray(st[1][:624], np.uint32)
+        snap["mt_pos"][0] = st[1][624]
+        self._vec.write_state(snap)
+
+    def _store_global(self):
+        snap = self._vec.read_state(mt=True)
+        st = (3, tuple(int(w) for w in snap["mt"][0]) + (int(snap["mt_pos"][0]),), None)
+        random.setstate(st)
+        self._gstate = st
+
     def reset(self):
-        return self._vec.reset().cpu().numpy()[0].tolist()
+        if self._shared:
+            self._load_global()
+        obs = self._vec.reset().cpu().numpy()[0].tolist()
+        if self._shared:
+            self._store_global()
+        return obs
 
     def _mask_bits(self):
         return int(self._vec.available_mask().cpu().item()) & 0x1FF
@@ -483,10 +523,14 @@ class TreasureGame:
         """option_list[a].run() on the device + get_state + done (TG/:91-96): tg_step1, one
         launch whose kernel writes the row into pinned host memory, one synchronisation"""
         v = self._vec
+        if self._shared:
+            self._load_global()
         check(v._L.tg_step1(v.handle, int(a), self._h_obs.ctypes.data, ctypes.byref(self._h_rew),
                             ctypes.byref(self._h_valid), ctypes.byref(self._h_done),
                             v._stream()), "tg_step1")
         r = int(self._h_rew.value) if self._h_valid.value else None
+        if self._shared:
+            self._store_global()
         return self._h_obs.tolist(), r, bool(self._h_done.value)
 
     def step(self, action):

@@ -569,3 +569,33 @@ def test_vector_env_gymnasium_surface(tg, oracle):
         n_trunc += int(trunc.sum())
     assert n_trunc > 0
     ve.close()
+
+
+def test_dropin_shares_the_global_random_stream(tg):
+    """TreasureGame(share_global_random=True) draws from Python's global random like the
+    reference's module-level calls: after random.seed(s), construction, reset, step and user
+    code's own random() calls between steps interleave on ONE stream, draw for draw.  The
+    reference side is oracle/pyref.py's Env over one Random(s) that the "user" draws from too."""
+    import random
+    import pyref  # test infrastructure (oracle/), on sys.path via conftest
+    seed = 2024
+    saved = random.getstate()
+    try:
+        random.seed(seed)
+        env = tg.TreasureGame(share_global_random=True)
+        ref = pyref.Env(seed)
+        assert env.reset() == ref.reset()
+        u = random.Random(7)
+        for t in range(150):
+            a = u.randrange(9)
+            if t % 10 == 5:  # the user's own draws from the shared stream
+                assert random.random() == ref.rng.random()
+            st, r, d, _ = env.step(a)
+            rs, rr, rd, _ = ref.step(a)
+            assert (st, r, d) == (list(rs), rr, rd), t
+            if d:
+                assert env.reset() == ref.reset()
+        assert random.getstate() == ref.rng.getstate()
+        env.close()
+    finally:
+        random.setstate(saved)
