@@ -945,6 +945,9 @@ template <int K, class R>
 TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng) {
   constexpr int DIR = (K == O_JUMP_LEFT || K == O_DOWN_LEFT) ? -1 : 1;
   constexpr bool JUMP = K == O_JUMP_LEFT || K == O_JUMP_RIGHT;
+#if defined(__HIP_DEVICE_COMPILE__) && defined(TG_DIAG_MARK)
+  asm volatile("; AIR_TICK_BEGIN");
+#endif
   const bool cf0 = m.can_fall(e);
   const bool fwd = m.can_go_side(e, DIR);
   const bool bwd = JUMP ? m.can_go_side(e, -DIR) : false;
@@ -979,6 +982,9 @@ TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng) {
   }
   e.py += yd;
   pickups(L, e);
+#if defined(__HIP_DEVICE_COMPILE__) && defined(TG_DIAG_MARK)
+  asm volatile("; AIR_TICK_END");
+#endif
   return -1;  // STEP_REWARD (no JUMP after the first tick)
 }
 
