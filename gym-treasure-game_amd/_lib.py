@@ -22,6 +22,7 @@ TG_ERR_BAG = 1 << 25
 TG_ERR_ACTION = 1 << 26
 TG_ERR_NEARINT = 1 << 27
 TG_ERR_RENDER = 1 << 28
+TG_ERR_STALL = 1 << 31
 TG_SPR_COUNT = 24
 OBS_DIM = 9
 NUM_ACTIONS = 9

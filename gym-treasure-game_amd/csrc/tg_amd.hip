@@ -991,7 +991,7 @@ constexpr int RO_NEXT = O_COUNT + 1;     // queue of envs whose next step is to 
 constexpr int RO_NQ = O_COUNT + 2;
 constexpr uint8_t RO_RETIRE = 0xFF;      // nextk: the env has done its K steps
 constexpr uint8_t RO_TONEXT = 0xFE;      // nextk: after the refill, on to RO_NEXT
-constexpr uint32_t RO_E_STALL = 1u << 31;  // err bit: a workgroup's waves found no work (bug)
+constexpr uint32_t RO_E_STALL = TG_ERR_STALL;  // a workgroup's queues stopped making progress (bug)
 constexpr unsigned long long RO_STALL_TICKS = 200000000ull;  // 2 s of the 100 MHz clock without progress
 static_assert(RO_WORDS == 64, "one bitmap word per lane");
 

@@ -57,6 +57,8 @@ extern "C" {
 #define TG_ERR_NEARINT (1u << 27)  /* reset gauss within 1e-9 of an int() boundary (libm watch) */
 #define TG_ERR_RENDER (1u << 28)   /* render: a handle shaft end point within 1e-9 of an int()
                                       boundary (libm watch), or a shaft off the screen */
+#define TG_ERR_STALL (1u << 31)   /* TG_MODE_ASYNC tg_rollout: a workgroup's queues stopped
+                                      making progress (a bookkeeping bug; the launch gave up) */
 
 /* step flags */
 #define TG_STEP_AUTORESET 1u       /* reset() an env right after a step that returned done */

@@ -599,3 +599,21 @@ def test_dropin_shares_the_global_random_stream(tg):
         env.close()
     finally:
         random.setstate(saved)
+
+
+def test_step1_rejects_batches_and_bad_outputs(tg):
+    """tg_step1 is the 1-env drop-in's call: a batch handle or a null output is an error"""
+    import ctypes
+    from gym_treasure_game_amd import _lib
+    v = tg.TreasureGameVec(2, seed=0)
+    obs = np.zeros(9)
+    r, va, d = ctypes.c_int32(), ctypes.c_uint8(), ctypes.c_uint8()
+    with pytest.raises(tg.TgError):
+        _lib.check(v._L.tg_step1(v.handle, 0, obs.ctypes.data, ctypes.byref(r), ctypes.byref(va),
+                                 ctypes.byref(d), None), "tg_step1")
+    v.close()
+    one = tg.TreasureGameVec(1, seed=0)
+    with pytest.raises(tg.TgError):
+        _lib.check(one._L.tg_step1(one.handle, 0, None, ctypes.byref(r), ctypes.byref(va),
+                                   ctypes.byref(d), None), "tg_step1")
+    one.close()
