@@ -270,6 +270,40 @@ TG_HD void seed_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed)
 // Map probes.  Every probe is a clamped index into the bordered grid plus one LDS byte read;
 // predicates combine probes with bitwise &/| so their LDS reads issue back to back.
 // ==========================================================================================
+// The cells one air tick at (px, py) can probe, as two 6-bit masks (bit 2*ri + ci: row r0 + ri,
+// column c0 + ci): every probe x of the tick lies in [px - 16, px + 16] (33 px: columns c0 =
+// colx(px - 16) and c0 + 1), every probe y in [py - 4, py + 53] (58 px: rows r0 = rowy(py - 4)
+// .. r0 + 2), the moved player's can_fall4 included (|x step| <= 4).  A probe's cell is then two
+// compares against the column / row starts instead of a clamped pixel -> cell division and an
+// LDS read; past the border the compares select the clamped cell, as colx / rowy do.
+struct AirCells {
+  uint32_t open, block;  // is_open; is_wall | is_door (can_go_side's blockers)
+  int bx, by1, by2;      // first pixel of column c0 + 1, of rows r0 + 1 and r0 + 2
+  TG_HD uint32_t ci(int x) const { return (uint32_t)(x >= bx); }
+  TG_HD uint32_t ri2(int y) const { return (uint32_t)((y >= by1) + (y >= by2)) * 2u; }
+  // bit 2*ri: the cells of xa and of xb in row ri are both open
+  TG_HD uint32_t rows_open(int xa, int xb) const { return (open >> ci(xa)) & (open >> ci(xb)) & 0x15u; }
+  TG_HD bool can_fall(int px, int py) const {  // can_fall_at
+    const uint32_t r = rows_open(px - HALFW + 2, px + HALFW - 2);
+    return ((r >> ri2(py)) & (r >> ri2(py + S + 2)) & 1u) != 0;
+  }
+  TG_HD uint32_t can_fall4(int px, int py) const {  // Map::can_fall4
+    const uint32_t r = rows_open(px - HALFW + 2, px + HALFW - 2);
+    uint32_t b = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b |= ((r >> ri2(py + k)) & (r >> ri2(py + S + 2 + k)) & 1u) << k;
+    return b;
+  }
+  TG_HD bool side(int px, int py, int dir) const {  // can_go_side
+    const uint32_t c = ci(px + dir * (HALFW + INCR));
+    return (((block >> (ri2(py + INCR) + c)) | (block >> (ri2(py + S - INCR) + c))) & 1u) == 0;
+  }
+  TG_HD bool up_clear(int px, int py) const {  // Map::up_clear
+    const uint32_t r = rows_open(px - INCR, px + INCR);
+    return ((r >> ri2(py - INCR)) & (r >> ri2(py - 1)) & 1u) != 0;
+  }
+};
+
 struct Map {
   const uint8_t* g;  // LDS on device: (H + 2*PAD) rows of (W + 2*PAD) cells
   int W, H;
@@ -342,6 +376,22 @@ struct Map {
     return open_at(dc, xa, ya) & open_at(dc, xa, yb) & open_at(dc, xb, ya) & open_at(dc, xb, yb);
   }
   TG_HD bool can_fall(const Env& e) const { return can_fall_at(dc_of(e.f), e.px, e.py); }
+  // AirCells at (px, py): six LDS reads in one batch (rows and the second column clamped)
+  TG_HD AirCells air_cells(uint32_t dc, int px, int py) const {
+    const int c0 = colx(px - (HALFW + INCR)), r0 = rowy(py - INCR);
+    const uint32_t x0 = (uint32_t)(c0 + PAD), x1 = (uint32_t)(c0 + 1 < W + PAD ? c0 + 1 + PAD : c0 + PAD);
+    uint32_t op = 0, bl = 0;
+#pragma unroll
+    for (int ri = 0; ri < 3; ++ri) {
+      const int r = r0 + ri < H + PAD ? r0 + ri : H + PAD - 1;
+      const uint8_t* const row = g + mul24((uint32_t)(r + PAD), (uint32_t)pw());
+      const uint32_t ca = row[x0], cb = row[x1];
+      op |= ((uint32_t)is_open(ca, dc) | (uint32_t)is_open(cb, dc) << 1) << (2 * ri);
+      bl |= ((uint32_t)(is_wall(ca) | is_door(ca, dc)) | (uint32_t)(is_wall(cb) | is_door(cb, dc)) << 1)
+            << (2 * ri);
+    }
+    return AirCells{op, bl, (c0 + 1) * S, (r0 + 1) * S, (r0 + 2) * S};
+  }
   // can_fall at (px, py + k) for k = 0..3 as bits 0..3: the probes (px -+ 10 at py + k and
   // py + 50 + k) span at most two rows each, so 8 lookups instead of 16
   TG_HD uint32_t can_fall4(uint32_t dc, int px, int py) const {
@@ -941,6 +991,9 @@ TG_HD int ladder_plain_limit(const Map& m, const Env& e) {
 // tick's precondition), up_clear (the jump ticker's rise).  Same outcomes and draws as
 // policy<K> + tick<prims_of(K)>.
 // ==========================================================================================
+#ifndef TG_AIR_NBHD
+#define TG_AIR_NBHD 1  // 0: every predicate through Map's pixel probes (A/B builds)
+#endif
 template <int K, class R>
 TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng) {
   constexpr int DIR = (K == O_JUMP_LEFT || K == O_DOWN_LEFT) ? -1 : 1;
@@ -948,10 +1001,18 @@ TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng) {
 #if defined(__HIP_DEVICE_COMPILE__) && defined(TG_DIAG_MARK)
   asm volatile("; AIR_TICK_BEGIN");
 #endif
+#if TG_AIR_NBHD
+  const AirCells ac = m.air_cells(Map::dc_of(e.f), e.px, e.py);
+  const bool cf0 = ac.can_fall(e.px, e.py);
+  const bool fwd = ac.side(e.px, e.py, DIR);
+  const bool bwd = JUMP ? ac.side(e.px, e.py, -DIR) : false;
+  const bool uc = ac.up_clear(e.px, e.py);
+#else
   const bool cf0 = m.can_fall(e);
   const bool fwd = m.can_go_side(e, DIR);
   const bool bwd = JUMP ? m.can_go_side(e, -DIR) : false;
   const bool uc = m.up_clear(e);
+#endif
   int mv = 0;  // the primitive: -1 LEFT, +1 RIGHT, 0 NOP
   if (close_x(e, o.tx)) {
     if (!cf0) o.done = true;
@@ -971,8 +1032,12 @@ TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng) {
     yd = INCR;
   }
   e.px += xd;
-  if (yd > 0) {  // IM/:341-348
+  if (yd > 0) {  // IM/:341-348 (e.px moved by <= 4: still inside the AirCells)
+#if TG_AIR_NBHD
+    const uint32_t cf = ac.can_fall4(e.px, e.py);
+#else
     const uint32_t cf = m.can_fall4(Map::dc_of(e.f), e.px, e.py);
+#endif
     if (cf & 1u) {
       int dist = yd;
       for (int k = yd - 1; k >= 1; --k)
