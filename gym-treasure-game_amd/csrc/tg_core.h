@@ -279,6 +279,13 @@ TG_HD void seed_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed)
 struct AirCells {
   uint32_t open, block;  // is_open; is_wall | is_door (can_go_side's blockers)
   int bx, by1, by2;      // first pixel of column c0 + 1, of rows r0 + 1 and r0 + 2
+  uint32_t dc;           // the door state the masks were built for
+  // still the window of (dc, px, py): colx(px - 16) == c0 and rowy(py - 4) == r0 (at a clamped
+  // border this is false, and the caller rebuilds every tick)
+  TG_HD bool holds(uint32_t d, int px, int py) const {
+    return (d == dc) & (px - (HALFW + INCR) < bx) & (px - (HALFW + INCR) >= bx - S) &
+           (py - INCR < by1) & (py - INCR >= by1 - S);
+  }
   TG_HD uint32_t ci(int x) const { return (uint32_t)(x >= bx); }
   TG_HD uint32_t ri2(int y) const { return (uint32_t)((y >= by1) + (y >= by2)) * 2u; }
   // bit 2*ri: the cells of xa and of xb in row ri are both open
@@ -390,7 +397,7 @@ struct Map {
       bl |= ((uint32_t)(is_wall(ca) | is_door(ca, dc)) | (uint32_t)(is_wall(cb) | is_door(cb, dc)) << 1)
             << (2 * ri);
     }
-    return AirCells{op, bl, (c0 + 1) * S, (r0 + 1) * S, (r0 + 2) * S};
+    return AirCells{op, bl, (c0 + 1) * S, (r0 + 1) * S, (r0 + 2) * S, dc};
   }
   // can_fall at (px, py + k) for k = 0..3 as bits 0..3: the probes (px -+ 10 at py + k and
   // py + 50 + k) span at most two rows each, so 8 lookups instead of 16
@@ -994,15 +1001,24 @@ TG_HD int ladder_plain_limit(const Map& m, const Env& e) {
 #ifndef TG_AIR_NBHD
 #define TG_AIR_NBHD 1  // 0: every predicate through Map's pixel probes (A/B builds)
 #endif
+#ifndef TG_AIR_CACHE
+#define TG_AIR_CACHE 1  // 0: AirCells rebuilt every tick (A/B builds)
+#endif
+// ac: the option loop's AirCells, rebuilt only when the player leaves its window (a jump
+// changes cell column or row every ~12 ticks)
 template <int K, class R>
-TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng) {
+TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng, AirCells& ac) {
   constexpr int DIR = (K == O_JUMP_LEFT || K == O_DOWN_LEFT) ? -1 : 1;
   constexpr bool JUMP = K == O_JUMP_LEFT || K == O_JUMP_RIGHT;
 #if defined(__HIP_DEVICE_COMPILE__) && defined(TG_DIAG_MARK)
   asm volatile("; AIR_TICK_BEGIN");
 #endif
 #if TG_AIR_NBHD
-  const AirCells ac = m.air_cells(Map::dc_of(e.f), e.px, e.py);
+#if TG_AIR_CACHE
+  if (!ac.holds(Map::dc_of(e.f), e.px, e.py)) ac = m.air_cells(Map::dc_of(e.f), e.px, e.py);
+#else
+  ac = m.air_cells(Map::dc_of(e.f), e.px, e.py);
+#endif
   const bool cf0 = ac.can_fall(e.px, e.py);
   const bool fwd = ac.side(e.px, e.py, DIR);
   const bool bwd = JUMP ? ac.side(e.px, e.py, -DIR) : false;
@@ -1129,10 +1145,11 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
     return;
   }
   if constexpr (K == O_JUMP_LEFT || K == O_JUMP_RIGHT || K == O_DOWN_LEFT || K == O_DOWN_RIGHT) {
+    AirCells ac{0u, 0u, -0x40000000, 0, 0, 0u};  // holds nothing: built on the first air tick
     do {
       rng.reserve(TICK_DRAWS);
       if (o.init) {
-        r.reward += air_tick<K>(L, m, e, o, rng);
+        r.reward += air_tick<K>(L, m, e, o, rng, ac);
       } else {  // the first tick (the jump itself; the drop's target)
         const int prim = policy<K>(L, m, e, o);
         r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
