@@ -291,25 +291,31 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
 // coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
 // earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart).  src / dst are
 // wave-uniform; must be reached by all 64 lanes of the wave.
-__device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
-                                           lds_u32* scratch) {
-  const int lane = threadIdx.x & 63;
-  constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
+struct TwistIn {
+  static constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
   uint32_t a[ROUNDS], b[ROUNDS], c[4];
+};
+// the loads of wave_twist (issued, not waited for: a caller can overlap them with other work)
+__device__ __forceinline__ void twist_load(const glb_u32* src, TwistIn& t) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int r = 0; r < ROUNDS; ++r) {
+  for (int r = 0; r < TwistIn::ROUNDS; ++r) {
     const int p = r * 64 + lane;
-    a[r] = p < MT_N ? src[p] : 0u;
-    b[r] = p + 1 < MT_N ? src[p + 1] : 0u;
-    if (r < 4) c[r] = p < MT_N - MT_M ? src[p + MT_M] : 0u;
+    t.a[r] = p < MT_N ? src[p] : 0u;
+    t.b[r] = p + 1 < MT_N ? src[p + 1] : 0u;
+    if (r < 4) t.c[r] = p < MT_N - MT_M ? src[p + MT_M] : 0u;
   }
+}
+__device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint8_t* dst_c,
+                                            lds_u32* scratch) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int r = 0; r < ROUNDS; ++r) {
+  for (int r = 0; r < TwistIn::ROUNDS; ++r) {
     const int p = r * 64 + lane;
     if (p < MT_N) {
-      const uint32_t bb = p + 1 < MT_N ? b[r] : scratch[0];
-      const uint32_t cc = p < MT_N - MT_M ? c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
-      const uint32_t w = mt_twist(a[r], bb, cc);
+      const uint32_t bb = p + 1 < MT_N ? t.b[r] : scratch[0];
+      const uint32_t cc = p < MT_N - MT_M ? t.c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
+      const uint32_t w = mt_twist(t.a[r], bb, cc);
       scratch[p] = w;
       dst[p] = w;
     }
@@ -326,6 +332,17 @@ __device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, uin
       reinterpret_cast<uint32_t*>(dst_c)[k] = v;
     }
   }
+}
+// Regenerate one env's stale half with the whole wave: dst = twist_gen(src), 64 words per round,
+// coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
+// earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart; the wait after each
+// round is needed: without it the results differ).  src / dst are wave-uniform; must be reached
+// by all 64 lanes of the wave.
+__device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
+                                           lds_u32* scratch) {
+  TwistIn t;
+  twist_load(src, t);
+  twist_store(t, dst, dst_c, scratch);
 }
 // For every lane in `need`: regenerate the stale half of its env (the one not holding the
 // position in its state word), one env at a time.  Must be reached by all 64 lanes.
@@ -666,6 +683,12 @@ struct Work {
   uint8_t* __restrict__ nrefill;  // [n / 64]: entries of classify wave w (no atomics)
   int64_t shard_cap;
 };
+#ifndef TG_TWIST_PIPE
+#define TG_TWIST_PIPE 1  // 0: the idle waves' twists one after another (A/B builds)
+#endif
+#ifndef TG_IDLE_WAVES
+#define TG_IDLE_WAVES 0  // > 0: at most this many idle waves regenerate (each loops over more)
+#endif
 constexpr int REFILL_BLOCKS = 64;  // k_run workgroups beyond the padded worklists (>= 256 idle waves)
 // worklist order = the order the chunks' loads reach HBM at the kernel's start (all option
 // waves are resident at once and issue their loads together): the jump waves first, whose
@@ -916,20 +939,50 @@ __global__ TG_RUN_BOUNDS void k_run(Soa S, int64_t n, Level L,
     // an idle wave: regenerate stale MT halves listed by k_classify, beside the option loops
     // (an env's half may also be regenerated by its own lane if it needs it first; both write
     // the same generation)
-    const int nidle = (int)gridDim.x * (BLOCK / 64) - total / 64;
+    const int nidle_all = (int)gridDim.x * (BLOCK / 64) - total / 64;
+#if TG_IDLE_WAVES
+    const int nidle = nidle_all < TG_IDLE_WAVES ? nidle_all : TG_IDLE_WAVES;
+#else
+    const int nidle = nidle_all;
+#endif
     const int nregions = (int)((n + 63) >> 6);  // k_classify's waves
-    for (int rg = (base - total) / 64; rg < nregions; rg += nidle) {
-      // the stale MT halves k_classify listed for these 64 envs
-      const int cnt = w.nrefill[rg];
+    const int iw = (base - total) / 64;  // this idle wave; those past nidle have nothing to do
+    for (int rg = iw; iw < nidle && rg < nregions; rg += nidle) {
+      // the stale MT halves k_classify listed for these 64 envs: lane j loads entry j, and the
+      // twists are software-pipelined (twist j + 1's loads are in flight while twist j computes
+      // and stores: A/B in DESIGN.md §3.3)
+      const int cnt = __builtin_amdgcn_readfirstlane((int)w.nrefill[rg]);
       regens += cnt;
+      if (!cnt) continue;
+      const int lane = threadIdx.x & 63;
+      const uint32_t ent_l = lane < cnt ? w.refill[(int64_t)rg * 64 + lane] : 0u;
+#if TG_TWIST_PIPE
+      TwistIn t;
+      uint32_t ent = __builtin_amdgcn_readfirstlane(ent_l);
+      twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
+                                  ((ent >> 31) ? MT_N : 0)), t);
       for (int j = 0; j < cnt; ++j) {
-        const uint32_t ent = w.refill[(int64_t)rg * 64 + j];
+        const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
+        const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
+        TwistIn u = t;
+        if (j + 1 < cnt) {
+          ent = __builtin_amdgcn_readlane(ent_l, j + 1);
+          twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
+                                      ((ent >> 31) ? MT_N : 0)), t);
+        }
+        twist_store(u, (glb_u32*)(S.mt + env * MT_WORDS + (MT_N - src)),
+                    S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
+      }
+#else
+      for (int j = 0; j < cnt; ++j) {
+        const uint32_t ent = __builtin_amdgcn_readlane(ent_l, j);
         const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
         uint32_t* const env_mt = S.mt + env * MT_WORDS;
         const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
         wave_twist((const glb_u32*)(env_mt + src), (glb_u32*)(env_mt + (MT_N - src)),
                    S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
       }
+#endif
     }
   }
   wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
