@@ -118,11 +118,11 @@ __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o
 constexpr uint32_t CODE_CHUNKS = MT_CODES / 16;  // 39
 static_assert(MT_CODES % 16 == 0, "whole 16-B code chunks per env");
 #ifndef TG_WIN_CHUNKS
-#define TG_WIN_CHUNKS 7
+#define TG_WIN_CHUNKS 4
 #endif
 constexpr int WIN_CHUNKS = TG_WIN_CHUNKS;
 constexpr int WIN_SLOT_BYTES = 64 * 16;
-constexpr int WIN_WAVE_BYTES = WIN_CHUNKS * WIN_SLOT_BYTES;  // 7 KB per wave
+constexpr int WIN_WAVE_BYTES = WIN_CHUNKS * WIN_SLOT_BYTES;  // 4 KB per wave
 constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
 static_assert(WIN_WAVE_BYTES >= WAVE_SCRATCH, "wave_refill reuses the window as scratch");
 
