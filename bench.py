@@ -430,7 +430,8 @@ def step_line(args, runner, dt, st, node, world, total):
             "frac_survey": surv / kern_s / 1e9 / HBM_PEAK_GBS,
             # what ends the kernels: the go waves' dependent per-tick chains,
             # not HBM bandwidth; the counters below are the evidence
-            "limiter": "issue-latency of the option tick loops (lane_efficiency, valu_util)",
+            "limiter": ("latency: k_run ends on its idle waves' MT refills (latency-bound twists, "
+                        "DESIGN.md §3.3) and the option tick loops (lane_efficiency, valu_util)"),
             "valu_util": pmc.get("valu_util") if pmc else None,
             "lane_efficiency": lane_eff}
     return {

@@ -683,6 +683,9 @@ struct Work {
   uint8_t* __restrict__ nrefill;  // [n / 64]: entries of classify wave w (no atomics)
   int64_t shard_cap;
 };
+#ifndef TG_CLS_REFILL
+#define TG_CLS_REFILL 0  // 1: k_classify regenerates the stale halves itself (A/B builds)
+#endif
 #ifndef TG_TWIST_PIPE
 #define TG_TWIST_PIPE 1  // 0: the idle waves' twists one after another (A/B builds)
 #endif
@@ -758,7 +761,11 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   }
   // halves left in the previous step (MT_STALE) go on the refill list; k_run's idle waves
   // regenerate them beside the option loops (a lane that needs one first does it itself)
+#if TG_CLS_REFILL
+  if (false) {
+#else
   {
+#endif
     const bool stale = live && (e.mti & MT_STALE);
     const unsigned long long b = __ballot(stale);
     const int64_t wv = i >> 6;
@@ -790,6 +797,23 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     const int c = bcnt[threadIdx.x];
     my_base = c ? atomicAdd(&w.ctr[(threadIdx.x * SHARDS + shard) * CTR_STRIDE], c) : 0;
   }
+  uint4 s4w = s4;  // the state the worklist copy carries
+  int cls_regens = 0;
+#if TG_CLS_REFILL
+  // (A/B) the stale halves regenerated here, by this wave (its obs staging area as the twist's
+  // scratch: the grid is no longer read after the barrier above), instead of k_run's idle waves
+  {
+    const unsigned long long need = __ballot(live && (e.mti & MT_STALE));
+    if (lane == 0) w.nrefill[i >> 6] = 0;
+    if (need) {
+      wave_refill(need, S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES, e.mti,
+                  (lds_u32*)(ostage + (threadIdx.x & ~63) * 9));
+      e.mti &= ~MT_STALE;
+      s4w.w &= ~MT_STALE;
+    }
+    cls_regens = __popcll(need);
+  }
+#endif
 
   // envs whose option cannot run: reward None, state unchanged (TG/:91-96, OP/:22-23)
   bool dn = false;
@@ -832,12 +856,12 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   if (runs) {
     const int64_t at = (int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot;
     w.lists[at] = (int32_t)i;
-    w.wst4[at] = s4;
+    w.wst4[at] = s4w;
     w.wang[at] = a2;
     w.wep[at] = ep;
   }
   wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
-              AUTORESET ? (live && !runs && dn) : 0);
+              AUTORESET ? (live && !runs && dn) : 0, cls_regens);
 }
 
 #ifdef TG_DIAG_STAMPS
