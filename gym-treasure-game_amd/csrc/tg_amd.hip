@@ -291,6 +291,9 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
 // coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
 // earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart).  src / dst are
 // wave-uniform; must be reached by all 64 lanes of the wave.
+#ifndef TG_TWIST_FENCE
+#define TG_TWIST_FENCE 1  // 0: s_waitcnt lgkmcnt(0) after every round of the twist (A/B builds)
+#endif
 struct TwistIn {
   static constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
   uint32_t a[ROUNDS], b[ROUNDS], c[4];
@@ -319,7 +322,16 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
       scratch[p] = w;
       dst[p] = w;
     }
+#if TG_TWIST_FENCE
+    // round r visible to later rounds, whose lanes read what other lanes wrote: a wavefront-scope
+    // fence orders the LDS accesses in the compiler (one wave's LDS operations execute in
+    // order), without the hardware wait for the store's completion
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // round r visible to later rounds
+#endif
   }
   // the generation's 312 draw codes, 4 per lane (one 4-B store each)
 #pragma unroll
