@@ -992,7 +992,40 @@ __global__ TG_RUN_BOUNDS void k_run(Soa S, int64_t n, Level L,
       if (!cnt) continue;
       const int lane = threadIdx.x & 63;
       const uint32_t ent_l = lane < cnt ? w.refill[(int64_t)rg * 64 + lane] : 0u;
-#if TG_TWIST_PIPE
+#if TG_TWIST_PIPE == 2
+      // two twists in flight: t0 / t1 hold entries j / j + 1; each is reloaded right after its
+      // twist is stored, while the other one computes (no register copies of pending loads)
+      TwistIn t0, t1;
+      auto src_of = [&](uint32_t en) {
+        return (const glb_u32*)(S.mt + (int64_t)(en & 0x7FFFFFFFu) * MT_WORDS + ((en >> 31) ? MT_N : 0));
+      };
+      auto store_to = [&](const TwistIn& u, uint32_t en) {
+        const int64_t env = (int64_t)(en & 0x7FFFFFFFu);
+        const uint32_t src = (en >> 31) ? (uint32_t)MT_N : 0u;
+        twist_store(u, (glb_u32*)(S.mt + env * MT_WORDS + (MT_N - src)),
+                    S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
+      };
+      uint32_t e0 = __builtin_amdgcn_readfirstlane(ent_l), e1 = 0u;
+      twist_load(src_of(e0), t0);
+      if (cnt > 1) {
+        e1 = __builtin_amdgcn_readlane(ent_l, 1);
+        twist_load(src_of(e1), t1);
+      }
+      for (int j = 0; j < cnt; j += 2) {
+        store_to(t0, e0);
+        if (j + 2 < cnt) {
+          e0 = __builtin_amdgcn_readlane(ent_l, j + 2);
+          twist_load(src_of(e0), t0);
+        }
+        if (j + 1 < cnt) {
+          store_to(t1, e1);
+          if (j + 3 < cnt) {
+            e1 = __builtin_amdgcn_readlane(ent_l, j + 3);
+            twist_load(src_of(e1), t1);
+          }
+        }
+      }
+#elif TG_TWIST_PIPE
       TwistIn t;
       uint32_t ent = __builtin_amdgcn_readfirstlane(ent_l);
       twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
