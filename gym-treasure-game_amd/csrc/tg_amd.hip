@@ -695,6 +695,9 @@ struct Work {
   uint8_t* __restrict__ nrefill;  // [n / 64]: entries of classify wave w (no atomics)
   int64_t shard_cap;
 };
+#ifndef TG_PRIO_IDLE
+#define TG_PRIO_IDLE 0  // > 0: the idle waves' issue priority while they regenerate (A/B builds)
+#endif
 #ifndef TG_CLS_REFILL
 #define TG_CLS_REFILL 0  // 1: k_classify regenerates the stale halves itself (A/B builds)
 #endif
@@ -975,6 +978,9 @@ __global__ TG_RUN_BOUNDS void k_run(Soa S, int64_t n, Level L,
     // an idle wave: regenerate stale MT halves listed by k_classify, beside the option loops
     // (an env's half may also be regenerated by its own lane if it needs it first; both write
     // the same generation)
+#if TG_PRIO_IDLE
+    __builtin_amdgcn_s_setprio(TG_PRIO_IDLE);  // (A/B) the refills end the kernel (§3.3)
+#endif
     const int nidle_all = (int)gridDim.x * (BLOCK / 64) - total / 64;
 #if TG_IDLE_WAVES
     const int nidle = nidle_all < TG_IDLE_WAVES ? nidle_all : TG_IDLE_WAVES;
