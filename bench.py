@@ -18,10 +18,14 @@ SURVEY §8e); rank 0 keeps them and reports their number and an order-independen
 (1,048,576 envs per GPU = config C3; C4 at 8 GPUs), so scaling is weak.  Inputs are resident
 in HBM when the timed region starts.
 
-Before timing: W warm-up steps, then ``--burn-in`` steps (default 300) so that the envs'
-positions in their MT19937 generations are spread out and the timed steps regenerate
-generations at the steady-state rate (N x draws per env-step / 312 per step); the line
-reports the measured and the expected rate.
+Before timing: W warm-up steps, then ``--burn-in`` steps (default 3,000 uniform / 1,500
+masked) so that the batch is in its steady state when timing starts: the envs' positions in
+their MT19937 generations are spread out, so the timed steps regenerate generations at the
+steady-state rate (N x draws per env-step / 312 per step; the line reports the measured and
+the expected rate), and episodes complete and flow through the gather at their steady-state
+rate (the first episodes end after ~550 masked / ~2,000 uniform steps).  The gathered records
+of global envs [0, E) are compared with the oracle's replay of those envs over every step of
+the run (``episode_check``).
 
 Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (tg_step's kernels:
 algorithmic bytes per launch over their HIP-event-timed duration vs the 8 TB/s HBM peak),
@@ -86,13 +90,17 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--burn-in", type=int, default=None,
-                    help="untimed steps after the warm-up so that MT regenerations reach their "
-                         "steady-state rate (default 300 uniform / 60 masked; 0 disables)")
+                    help="untimed steps after the warm-up so that MT regenerations and episode "
+                         "completions reach their steady-state rates (default 3000 uniform / "
+                         "1500 masked; 0 disables)")
     ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
                     help="c3: vector-obs step (default, the headline); c5: step + RGB render")
     ap.add_argument("--envs", type=int, default=None,
                     help="envs per GPU (default 1,048,576 for c3, 65,536 for c5)")
     ap.add_argument("--policy", default="uniform", choices=["uniform", "masked"])
+    ap.add_argument("--level", default=None,
+                    help="a level directory in the reference's three-file format (default: the "
+                         "reference's own level)")
     ap.add_argument("--no-autoreset", action="store_true")
     ap.add_argument("--mode", default="compact", choices=["compact", "direct"],
                     help="step implementation (bit-identical): two-pass compacted or one-pass")
@@ -113,8 +121,12 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU-baseline sample (0 disables it and the "
                          "parity check)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_step.json"),
-                    help="PMC-derived HBM bytes per tg_step (profiles/), if measured")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per tg_step (default profiles/"
+                         "traffic_step_<policy>.json), if measured")
+    ap.add_argument("--episode-envs", type=int, default=None,
+                    help="episode_check: the oracle replays global envs [0, E) over the whole "
+                         "run (default 16384 uniform / 8192 masked; 0 disables)")
     return ap.parse_args(argv)
 
 
@@ -162,6 +174,18 @@ def cpu_baseline(seconds, policy, parity_envs=0):
                      "envs 0..%d x %d steps, %s policy, auto-reset, %d OpenMP threads, %.1f s"
                      % (n - 1, steps, policy, threads, dt)}
     return out, r["hash"][:parity_envs], steps
+
+
+def oracle_episodes(policy, steps, t_from, envs, level=None):
+    """(count, digest) of the auto-reset episodes of global envs [0, envs) that end at step
+    index >= t_from, from the C oracle's replay of the run (bench's cpu leg only)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # noqa: E402 — bench's cpu_baseline leg only
+    O.build()
+    cores = len(os.sched_getaffinity(0))
+    threads = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    return O.run_episodes(0, 0, envs, steps, ACTION_SEED, 1 if policy == "masked" else 0, t_from,
+                          threads, level_dir=level)
 
 
 def python_baseline(seconds, policy):
@@ -245,7 +269,8 @@ class Runner:
         self.tg, self.D, self.args, self.world, self.dev = tg, D, args, world, dev
         self.count = count
         self.autoreset = not args.no_autoreset
-        vec = tg.TreasureGameVec(count, seed=0, global_offset=offset, autoreset=False, device=dev)
+        vec = tg.TreasureGameVec(count, seed=0, global_offset=offset, autoreset=False, device=dev,
+                                 level_dir=args.level)
         vec.set_mode(args.mode, args.run_blocks)
         vec.autoreset = self.autoreset  # final_obs is not requested: obs/reward/valid/done only
         vec.reset()
@@ -387,9 +412,20 @@ def node_totals(st, world, dev):
     return dict(zip(keys, tot.tolist()))
 
 
+def default_burn_in(policy):
+    """untimed steps before timing: the batch's steady state (module docstring)"""
+    return 3000 if policy == "uniform" else 1500
+
+
+def default_episode_envs(policy):
+    return 16384 if policy == "uniform" else 8192
+
+
 def load_pmc(path, envs, policy, mode, regens_per_step, burn_in):
-    """profiles/traffic_step.json (scripts/prof_summary.py) when its PMC source run matches
-    this run: same envs, policy and step mode, and a regeneration rate within 10 %."""
+    """profiles/traffic_step_<policy>.json (scripts/prof_summary.py) when its PMC source run
+    matches this run: same envs, policy and step mode, and a regeneration rate within 10 %."""
+    if path is None:
+        path = os.path.join(ROOT, "profiles", "traffic_step_%s.json" % policy)
     if not os.path.exists(path):
         return None
     tj = json.load(open(path))
@@ -474,13 +510,21 @@ def main():
     offset, count = D.shard(total, rank, world)
     args.policy_used = args.policy
     args.burn_in_used = (args.burn_in if args.burn_in is not None
-                         else (300 if args.policy == "uniform" else 60))
+                         else default_burn_in(args.policy))
+    ep_envs = (args.episode_envs if args.episode_envs is not None
+               else default_episode_envs(args.policy))
+    ep_envs = min(ep_envs, total)
     run = Runner(tg, D, args, args.policy, count, offset, world, dev, keep_log=(rank == 0))
     dt, st = run.measure(args.warmup, args.burn_in_used, args.steps)
     node = node_totals(st, world, dev)
     errs = run.vec.errors()
     rec, digest = run.log.digest() if rank == 0 else (None, None)
     autoreset = run.autoreset
+    # (policy, warmup, burn-in, steps, E, the gathered records of envs [0, E) and their digest)
+    checks = []
+    if rank == 0 and autoreset and ep_envs > 0:
+        checks.append((args.policy, args.warmup, args.burn_in_used, args.steps, ep_envs,
+                       run.log.digest(env_below=ep_envs), "line"))
 
     line = None
     if rank == 0:
@@ -489,8 +533,9 @@ def main():
             # every episode the step kernels counted reached rank 0 through the gather
             assert rec == node["episodes"] - node["episodes_dropped"], (rec, node)
         workload = ("C3/C4: %d batched treasure_game-v0 envs per GPU, vector obs, %s random "
-                    "options, auto-reset%s" % (args.envs, args.policy,
-                                               " + RCCL episode gather" if world > 1 else ""))
+                    "options, auto-reset%s%s" % (args.envs, args.policy,
+                                                 " + RCCL episode gather" if world > 1 else "",
+                                                 ", level %s" % args.level if args.level else ""))
         extra = step_line(args, run, dt, st, node, world, total)
         if c5:
             fh, fw, _ = run.vec.frame_shape
@@ -543,15 +588,23 @@ def main():
         a2 = parse(sys.argv[1:])
         a2.envs, a2.policy, a2.policy_used = args.envs, other, other
         a2.steps = args.secondary_steps
-        a2.burn_in_used = 60 if other == "masked" else 300
+        a2.burn_in_used = default_burn_in(other)
+        w2 = min(args.warmup, 5)
         r2 = Runner(tg, D, a2, other, count, offset, world, dev, keep_log=True)
-        dt2, st2 = r2.measure(min(args.warmup, 5), a2.burn_in_used, a2.steps)
+        dt2, st2 = r2.measure(w2, a2.burn_in_used, a2.steps)
         n2 = node_totals(st2, 1, dev)
         sec = {"policy": other, "value": total * a2.steps / dt2, "unit": "env-steps/s",
                "steps": a2.steps, "burn_in": a2.burn_in_used,
                "ms_per_step": dt2 / a2.steps * 1e3}
         sec.update(step_line(a2, r2, dt2, st2, n2, 1, total))
-        sec["episodes"] = n2["episodes"]
+        rec2, dig2 = r2.log.digest()
+        assert rec2 == n2["episodes"] - n2["episodes_dropped"], (rec2, n2)
+        sec.update({"episodes": n2["episodes"], "episodes_dropped": n2["episodes_dropped"],
+                    "episodes_gathered": rec2, "episode_digest": dig2})
+        e2 = min(default_episode_envs(other), total)
+        if r2.autoreset and e2 > 0 and args.episode_envs != 0:
+            checks.append((other, w2, a2.burn_in_used, a2.steps, e2, r2.log.digest(env_below=e2),
+                           other + "_policy"))
         r2.vec.close()
         line[other + "_policy"] = sec
         line["dropin_n1"] = dropin_latency(tg)
@@ -575,6 +628,16 @@ def main():
             line["parity_check"] = {"envs": pe, "steps": steps_h, "policy": args.policy,
                                     "autoreset": True, "mismatched_envs": bad,
                                     "error_flags": gerr, "bit_exact": bad == 0 and gerr == 0}
+        for pol, w, b, k, e, got, where in checks:
+            want = oracle_episodes(pol, w + b + k, w + b, e, args.level)
+            chk = {"envs": e, "policy": pol, "steps": [w + b, w + b + k],
+                   "gathered": got[0], "digest": got[1],
+                   "oracle": want[0], "oracle_digest": want[1],
+                   "match": tuple(got) == tuple(want),
+                   "what": "episodes of global envs [0, E) ending in the timed steps, gathered "
+                           "(tg_episodes -> dist.gather_padded -> EpisodeLog) vs the oracle's "
+                           "auto-reset replay of those envs over every step of the run"}
+            (line if where == "line" else line[where])["episode_check"] = chk
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

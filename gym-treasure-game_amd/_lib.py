@@ -22,13 +22,15 @@ TG_ERR_BAG = 1 << 25
 TG_ERR_ACTION = 1 << 26
 TG_ERR_NEARINT = 1 << 27
 TG_ERR_RENDER = 1 << 28
+TG_ERR_WINDOW = 1 << 29
 TG_ERR_STALL = 1 << 31
 TG_SPR_COUNT = 24
 OBS_DIM = 9
 NUM_ACTIONS = 9
 
 # every symbol include/tg_amd.h declares (tests check the library exports all of them)
-EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_step1", "tg_rollout",
+EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_step1", "tg_step1_py",
+           "tg_reset1_py", "tg_rollout",
            "tg_available_mask",
            "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing",
            "tg_set_episode_capacity", "tg_predicate_table",
@@ -42,6 +44,12 @@ class TgError(RuntimeError):
 
 class Episode(ctypes.Structure):
     _fields_ = [("env", ctypes.c_int64), ("ret", ctypes.c_int32), ("len", ctypes.c_int32)]
+
+
+class PyState(ctypes.Structure):
+    """tg_pystate: random.getstate()'s (624 words, index, gauss_next)"""
+    _fields_ = [("mt", ctypes.c_uint32 * 624), ("index", ctypes.c_uint32),
+                ("has_gauss", ctypes.c_uint32), ("gauss_next", ctypes.c_double)]
 
 
 class Stats(ctypes.Structure):
@@ -78,6 +86,8 @@ def load():
         "tg_reset": (i32, [P, P, P, P]),
         "tg_step": (i32, [P, P, P, P, P, P, P, u32, P]),
         "tg_step1": (i32, [P, i32, P, P, P, P, P]),
+        "tg_step1_py": (i32, [P, i32, P, P, P, P, P, P]),
+        "tg_reset1_py": (i32, [P, P, P, P]),
         "tg_rollout": (i32, [P, i32, u64, i64, i32, u32, P, P, P, P, P, P]),
         "tg_available_mask": (i32, [P, P, P]),
         "tg_observe": (i32, [P, P, P]),

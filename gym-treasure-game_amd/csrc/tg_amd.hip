@@ -125,6 +125,7 @@ constexpr int WIN_SLOT_BYTES = 64 * 16;
 constexpr int WIN_WAVE_BYTES = WIN_CHUNKS * WIN_SLOT_BYTES;  // 4 KB per wave
 constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
 static_assert(WIN_WAVE_BYTES >= WAVE_SCRATCH, "wave_refill reuses the window as scratch");
+static_assert(WIN_CHUNKS * 16 - 15 >= (int)MAX_TICK_DRAWS, "a refilled window holds a tick's draws");
 
 typedef __attribute__((address_space(1))) uint32_t glb_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -243,6 +244,8 @@ struct RngCodes {
   }
   // at least k draws staged (no refill: the plain go loop's exit test)
   __device__ __forceinline__ bool has(uint32_t k) const { return left >= k; }
+  // a draw was taken past the staged window (reserve's bound broken: flagged E_WINDOW)
+  __device__ __forceinline__ bool overrun() const { return left > (uint32_t)WIN_CHUNKS * 16u; }
   // one draw, consumed for its outcomes (draw_code); reserve() guarantees it is in the window
   __device__ __forceinline__ uint32_t code() {
 #ifdef TG_DIAG_CODEHASH  // DIAGNOSTIC BUILD ONLY: codes from a register hash (prices the window)
@@ -566,6 +569,7 @@ template <bool AUTORESET, bool FINAL, class R>
 __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int64_t i,
                                             const StepResult& r, int2& ep, const StepIO& io,
                                             double* keep = nullptr) {
+  if (rng.overrun()) e.f |= E_WINDOW;
   double o[9];
   observe(L, e, o);  // get_state (TG/:94)
   io.reward[i] = r.reward;
@@ -1650,6 +1654,113 @@ __global__ __launch_bounds__(BLOCK) void k_gather_mt(Soa S, int64_t first, int64
   reinterpret_cast<uint4*>(dst)[t] = src[q];
 }
 
+// ---- the N=1 drop-in over a Python-level random stream (tg_step1_py / tg_reset1_py) ---------
+// One wave.  The stream's generation (tg_pystate: random.getstate()'s 624 words + index) is read
+// from pinned host memory into LDS with its two successors (twisted by the wave), lane 0 runs the
+// step / reset with a PyRng over them, and the wave writes back the generation holding the
+// stream's new position, so the caller's random.setstate continues exactly where CPython's
+// would: any index, odd ones too (the twist is a recurrence on consecutive words, so words are
+// read by absolute position across generations), and gauss_next carried in and out.
+constexpr int PY_GENS = 3;  // generations held in LDS; a 4th+ is twisted in place by lane 0
+struct PyRng {
+  uint32_t* w;     // LDS: PY_GENS slots of MT_N words, generation g in slot g % PY_GENS
+  uint32_t q;      // absolute word position (generation g holds positions [g*624, g*624 + 624))
+  uint32_t lo;     // oldest generation held
+  uint32_t draws;
+  __device__ __forceinline__ uint32_t word(uint32_t pos) {
+    const uint32_t g = pos / MT_N;
+    while (g >= lo + PY_GENS) {  // > 2 generations in one call (long levels): twist in place
+      twist_gen(w + ((lo + PY_GENS - 1) % PY_GENS) * MT_N, w + (lo % PY_GENS) * MT_N);
+      ++lo;
+    }
+    return w[(g % PY_GENS) * MT_N + (pos - g * MT_N)];
+  }
+  __device__ __forceinline__ double random() {
+    const uint32_t a = word(q), b = word(q + 1);
+    q += 2;
+    ++draws;
+    return mt_double(a, b);
+  }
+  __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
+  __device__ __forceinline__ uint32_t code() { return draw_code(random()); }
+  __device__ __forceinline__ void reserve(uint32_t) {}
+  __device__ __forceinline__ bool has(uint32_t) const { return true; }
+  __device__ __forceinline__ bool overrun() const { return false; }
+};
+// dst = twist_gen(src) with the 64 lanes of the (only) wave, both in LDS
+__device__ __forceinline__ void lds_twist64(const uint32_t* src, uint32_t* dst) {
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < (MT_N + 63) / 64; ++r) {
+    const int p = r * 64 + lane;
+    if (p < MT_N) {
+      const uint32_t b = p + 1 < MT_N ? src[p + 1] : dst[0];
+      const uint32_t c = p < MT_N - MT_M ? src[p + MT_M] : dst[p - (MT_N - MT_M)];
+      dst[p] = mt_twist(src[p], b, c);
+    }
+    __syncthreads();
+  }
+}
+template <bool RESET>
+__global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __restrict__ grid,
+                                            int action, tg_pystate* py, TgOne* out,
+                                            unsigned long long* __restrict__ stats,
+                                            uint32_t* __restrict__ err_or) {
+  __shared__ uint32_t W[PY_GENS * MT_N];
+  __shared__ LdsLevel lv;
+  __shared__ uint32_t out_gen, out_idx;
+  const int lane = threadIdx.x;
+  const int nwords = ((L.W + 2 * PAD) * (L.H + 2 * PAD) + 3) / 4;
+  for (int i = lane; i < nwords; i += 64) lv.grid[i] = grid[i];
+  if (lane < 12) lv.trig[lane] = L.trig[lane >> 1][lane & 1];
+  for (int i = lane; i < MT_N; i += 64) W[i] = py->mt[i];
+  __syncthreads();
+  lds_twist64(W, W + MT_N);
+  lds_twist64(W + MT_N, W + 2 * MT_N);
+  StepResult r{0, 0, 0, 0};
+  uint32_t draws = 0;
+  if (lane == 0) {
+    const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
+    const uint32_t q0 = py->index;
+    PyRng rng{W, q0, 0u, 0u};
+    Env e;
+    unpack(S.st4[0], S.ang[0], e);
+    int2 ep = S.ep[0];
+    double o[9];
+    if (RESET) {
+      GaussNext g{py->has_gauss != 0u, py->gauss_next};
+      reset_env_gauss(L, e, rng, g);
+      py->has_gauss = g.has ? 1u : 0u;
+      py->gauss_next = g.has ? g.v : 0.0;
+      ep = make_int2(0, 0);
+    } else {
+      r = env_step(L, lv.trig, m, e, action, rng);
+      ep.x += r.reward;
+      ep.y += 1;
+    }
+    observe(L, e, o);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) out->obs[k] = o[k];
+    out->reward = r.reward;
+    out->valid = (uint8_t)r.ran;
+    out->done = (uint8_t)r.done;
+    S.st4[0] = pack(e);
+    S.ang[0] = make_double2(e.ang0, e.ang1);
+    S.ep[0] = ep;
+    if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+    // CPython's state after the last word read: its generation and the index past it
+    const uint32_t g = rng.q == q0 ? 0u : (rng.q - 1u) / MT_N;
+    out_gen = g % PY_GENS;
+    out_idx = rng.q == q0 ? q0 : rng.q - g * MT_N;
+    draws = rng.draws;
+  }
+  __syncthreads();
+  const uint32_t* src = W + out_gen * MT_N;
+  for (int i = lane; i < MT_N; i += 64) py->mt[i] = src[i];
+  if (lane == 0) py->index = out_idx;
+  wave_stats(stats, lane == 0 && !RESET ? 1 : 0, r.ran, r.ticks, (int)draws, 0);
+}
+
 __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4, int64_t n,
                                                    uint32_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -1798,6 +1909,7 @@ void tg_destroy(tg_batch* h) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->one) (void)hipHostFree(h->one);
+  if (h->py) (void)hipHostFree(h->py);
   delete h;
 }
 
@@ -1951,6 +2063,58 @@ int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t*
   *reward = h->one->reward;
   *valid = h->one->valid;
   *done = h->one->done;
+  return TG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// one k_py1 launch: the caller's stream state in, the result row and the advanced state out
+template <bool RESET>
+int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) {
+  if (h->n != 1 || !st) return fail(TG_E_INVAL, "tg_*1_py: a 1-env handle and a stream state");
+  if (st->index > (uint32_t)MT_N)
+    return fail(TG_E_INVAL, "tg_*1_py: index %u outside [0, 624]", st->index);
+  if (!h->one) {
+    if (hipHostMalloc((void**)&h->one, sizeof(TgOne), hipHostMallocMapped) != hipSuccess)
+      return fail(TG_E_NOMEM, "tg_*1_py: pinned result buffer");
+    HIP_TRY(hipHostGetDevicePointer((void**)&h->one_dev, h->one, 0));
+  }
+  if (!h->py) {
+    if (hipHostMalloc((void**)&h->py, sizeof(tg_pystate), hipHostMallocMapped) != hipSuccess)
+      return fail(TG_E_NOMEM, "tg_*1_py: pinned stream state");
+    HIP_TRY(hipHostGetDevicePointer((void**)&h->py_dev, h->py, 0));
+  }
+  memcpy(h->py, st, sizeof(tg_pystate));
+  hipLaunchKernelGGL(k_py1<RESET>, dim3(1), dim3(64), 0, stream, h->S, h->L, h->grid, (int)action,
+                     h->py_dev, h->one_dev, h->stats, h->err);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(stream));
+  memcpy(st, h->py, sizeof(tg_pystate));
+  return TG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int tg_step1_py(tg_batch* h, int32_t action, tg_pystate* st, double* obs, int32_t* reward,
+                uint8_t* valid, uint8_t* done, void* stream) {
+  BIND(h);
+  if (!obs || !reward || !valid || !done) return fail(TG_E_INVAL, "tg_step1_py: null output");
+  const int rc = launch_py1<false>(h, action, st, (hipStream_t)stream);
+  if (rc) return rc;
+  memcpy(obs, h->one->obs, sizeof h->one->obs);
+  *reward = h->one->reward;
+  *valid = h->one->valid;
+  *done = h->one->done;
+  return TG_OK;
+}
+
+int tg_reset1_py(tg_batch* h, tg_pystate* st, double* obs, void* stream) {
+  BIND(h);
+  const int rc = launch_py1<true>(h, 0, st, (hipStream_t)stream);
+  if (rc) return rc;
+  if (obs) memcpy(obs, h->one->obs, sizeof h->one->obs);
   return TG_OK;
 }
 

@@ -59,9 +59,9 @@ struct tg_batch {
   tg::Level L{};
   uint32_t* grid = nullptr;  // bordered cell grid, padded to whole words
   uint32_t* genrand = nullptr;
-  uint32_t* gotab = nullptr;
+  uint32_t* gotab = nullptr;  // GoTable (tg_core.h go_lookup), W * H * 32 entries
   int cus = 0;               // compute units (k_rollout sizes its workgroups to fill them once)
-  int ro_per_cu = 0;         // k_rollout workgroups resident per CU (occupancy API, first use)  // GoTable (tg_core.h go_lookup), W * H * 32 entries
+  int ro_per_cu = 0;         // k_rollout workgroups resident per CU (occupancy API, first use)
   tg::Soa S{};
   tg_episode* eps = nullptr;
   int32_t* eps_count = nullptr;
@@ -86,6 +86,8 @@ struct tg_batch {
   double* obs_scratch = nullptr;   // tg_rollout without an obs output
   tg::TgOne* one = nullptr;            // tg_step1's row: pinned host memory the kernel writes
   tg::TgOne* one_dev = nullptr;        //   (its device-side address)
+  tg_pystate* py = nullptr;            // tg_step1_py / tg_reset1_py's stream state (pinned)
+  tg_pystate* py_dev = nullptr;
   tg::RenderState* rs = nullptr;   // tg_render_init
 };
 

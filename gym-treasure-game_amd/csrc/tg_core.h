@@ -33,9 +33,13 @@ constexpr int INCR = S / 10;   // x_incr / y_incr (IM/:46-47)
 constexpr int HALFW = S / 4;   // player_width // 2 (IM/:49)
 constexpr int MT_N = 624, MT_M = 397;
 constexpr int TICK_CAP = 1 << 14;  // the reference has no cap (OP/:28-31); observed max 105
-// random() draws one primitive tick can take: a move or jump 1; INTERACT flips <= 2 handles,
-// each 1 draw + <= 2 angle wiggles of the cascade (every object changes once per cascade)
+// random() draws a tick without INTERACT can take (a move or a jump: 1), with margin.  An
+// INTERACT tick can take more: each handle flip is 1 draw plus one wiggle per handle change of
+// its cascade, and since process_trigger clears previously_triggered on return (OB/:76-94) a
+// cascade can change one handle several times.  Its bound depends on the level's trigger
+// table: Level::interact_draws (tg_level.h interact_draw_bound), at most MAX_TICK_DRAWS.
 constexpr uint32_t TICK_DRAWS = 8;
+constexpr uint32_t MAX_TICK_DRAWS = 48;  // what a refilled code window always holds (tg_amd.hip)
 constexpr int PAD = 2;         // WALL cells around the grid in LDS (probes reach <= 60 px out)
 
 // Cell bits in the LDS grid.  A door object's cell carries only its one-hot door bit: its type
@@ -60,6 +64,7 @@ constexpr uint32_t E_BAG = 1u << 25;      // bag overflow (unreachable in the de
 constexpr uint32_t E_ACTION = 1u << 26;   // action outside [-9, 8] (reference: IndexError)
 constexpr uint32_t E_NEARINT = 1u << 27;  // a reset's gauss landed within 1e-9 of an int()
                                           // boundary (device libm vs glibc watch)
+constexpr uint32_t E_WINDOW = 1u << 29;   // a lane drew past its staged code window (a bug)
 constexpr uint32_t E_MASK = 0xFF000000u;
 
 // ---- level (kernel argument; the grid and the trigger table are staged in LDS) -------------
@@ -71,6 +76,7 @@ struct Level {
   int8_t key_cx, key_cy, bolt_cx, bolt_cy, gold_cx, gold_cy;
   uint32_t init_flags;       // door/handle/bolt initial booleans at their F_OBJ bits
   uint32_t trig[6][2];       // trigger lists [object][polarity]: count(4b) + 7 x (target 3b, val 1b)
+  uint32_t interact_draws;   // most random() draws one INTERACT tick can take (>= TICK_DRAWS)
   // go_left / go_right can_run and target per (cell, door state, key home?, gold home?)
   // (GoTable; device global memory, built at tg_create; null: computed directly)
   const uint32_t* gotab;
@@ -217,6 +223,7 @@ struct Rng {
   // draws come straight from the words: nothing to stage (the device's RngCodes stages codes)
   TG_HD void reserve(uint32_t) {}
   TG_HD bool has(uint32_t) const { return true; }
+  TG_HD bool overrun() const { return false; }
   // the state word to store: position, and whether the other half is stale
   TG_HD uint32_t finish() const { return pos | (crossed ? MT_STALE : 0u); }
   // the same when a refill of the half that was stale on entry is already queued
@@ -841,6 +848,46 @@ TG_HD void reset_env(const Level& L, Env& e, R& rng) {
   e.py = L.start_y * S + (int)zy;
 }
 
+// Random.gauss's cached second value (CPython random.py gauss: gauss_next), for an env that
+// draws from a shared Python-level stream (the N=1 drop-in's default, tg_reset1_py)
+struct GaussNext {
+  bool has;
+  double v;
+};
+// z of Random.gauss (the caller applies mu + z * sigma): the cached value if there is one,
+// else a fresh pair (2 draws) whose second value is cached
+template <class R>
+TG_HD double gauss_z(R& rng, GaussNext& g) {
+  if (g.has) {
+    g.has = false;
+    return g.v;
+  }
+  const double x2pi = rng.random() * (2.0 * 3.141592653589793);
+  const double g2rad = sqrt(-2.0 * log(1.0 - rng.random()));
+  g.v = sin(x2pi) * g2rad;
+  g.has = true;
+  return cos(x2pi) * g2rad;
+}
+// reset_env with the stream's gauss_next carried in and out (reset_env assumes it unset, as
+// after random.seed, and leaves it unset: the two gauss calls consume one pair)
+template <class R>
+TG_HD void reset_env_gauss(const Level& L, Env& e, R& rng, GaussNext& g) {
+  e.f = (e.f & E_MASK) | L.init_flags | F_FACING;
+  e.ang0 = ((L.init_flags >> (F_OBJ + 3)) & 1u) ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
+  e.ang1 = ((L.init_flags >> (F_OBJ + 4)) & 1u) ? rng.uniform(0.85, 1.0) : rng.uniform(0, 0.15);
+  e.kx = L.key_cx;
+  e.ky = L.key_cy;
+  e.gx = L.gold_cx;
+  e.gy = L.gold_cy;
+  const double zx = 0.0 + gauss_z(rng, g) * (S / 24.0);
+  const double zy = fabs(0.0 + gauss_z(rng, g) * (S / 36.0));
+  const double fx = fabs(zx) - floor(fabs(zx)), fy = zy - floor(zy);
+  if ((fabs(zx) >= 0.5 && (fx < 1e-9 || fx > 1.0 - 1e-9)) || (zy >= 0.5 && (fy < 1e-9 || fy > 1.0 - 1e-9)))
+    e.f |= E_NEARINT;
+  e.px = L.start_x * S + S / 2 + (int)zx;
+  e.py = L.start_y * S + (int)zy;
+}
+
 // ==========================================================================================
 // One env-step: TreasureGame.step (TG/:91-96) -> _Option.run (OP/:20-36)
 // ==========================================================================================
@@ -1163,7 +1210,7 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
   }
 #endif
   do {
-    rng.reserve(TICK_DRAWS);
+    rng.reserve(K == O_INTERACT ? L.interact_draws : TICK_DRAWS);
     const int prim = policy<K>(L, m, e, o);
     r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
     if (++r.ticks >= TICK_CAP) {

@@ -75,6 +75,37 @@ inline std::vector<std::string> words(const std::string& s) {
   return w;
 }
 
+// random() draws of a cascade, counted (the values do not matter: a cascade's path depends on
+// the objects' booleans only)
+struct CountingRng {
+  uint32_t draws = 0;
+  double uniform(double, double) { ++draws; return 0.5; }
+};
+// The most draws one INTERACT tick (IM/:321-329) can take on this level: handle 0's flip, then
+// handle 1's, then the bolt's unlock (object order), each flip 1 draw plus its cascade's
+// wiggles (or 1 wiggle when it fails, OB/:117-122), over every boolean state of the six
+// interactive objects and every flip outcome.  An upper bound: it does not ask whether the
+// player can be near both handles and the bolt at once.
+inline uint32_t interact_draw_bound(const Level& L) {
+  const uint32_t* trig = &L.trig[0][0];
+  uint32_t most = 0;
+  for (uint32_t s = 0; s < 64; ++s)
+    for (int outcome = 0; outcome < 4; ++outcome)
+      for (int bolt = 0; bolt < 2; ++bolt) {
+        Env e{};
+        e.f = s << F_OBJ;
+        CountingRng r;
+        for (int h = 0; h < 2; ++h) {
+          ++r.draws;  // the flip's uniform(0, 1) <= 0.8
+          if ((outcome >> h) & 1) cascade(trig, e, 3 + h, !((e.f >> (F_OBJ + 3 + h)) & 1u), r);
+          else wiggle(e, h, r);
+        }
+        if (bolt) cascade(trig, e, 5, 0, r);
+        if (r.draws > most) most = r.draws;
+      }
+  return most;
+}
+
 // Returns 0, or -1 with a message in `err`.
 inline int parse_level(const char* dom, const char* objs, const char* inter, Level& L,
                        std::vector<uint8_t>& grid, std::string& err) {
@@ -170,6 +201,12 @@ inline int parse_level(const char* dom, const char* objs, const char* inter, Lev
     if (cnt >= 7) return level_err(err, "level: more than 7 triggers on one object");
     list = (list & ~0xFu) | (cnt + 1) | ((uint32_t)(dst | (val << 3)) << (4 + 4 * cnt));
   }
+  // the option loops stage draws in a per-lane window and reserve a tick's worth before it
+  const uint32_t d = interact_draw_bound(L);
+  if (d > MAX_TICK_DRAWS)
+    return level_err(err, "level: one INTERACT tick can draw %u times (trigger cascades), more "
+                     "than the %u this build stages per tick", d, MAX_TICK_DRAWS);
+  L.interact_draws = d > TICK_DRAWS ? d : TICK_DRAWS;
   return 0;
 }
 

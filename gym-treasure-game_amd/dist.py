@@ -75,12 +75,13 @@ def _sm64(x):
     return x ^ (x >> np.uint64(31))
 
 
-def episode_digest(rows, counts, cap):
+def episode_digest(rows, counts, cap, env_below=None):
     """(records, digest) of gathered episode buffers: ``rows`` int64 [k*cap, 2] raw records
     and ``counts`` [k] valid records per cap-sized segment (any device).  The digest is the
     sum mod 2^64 of sm64(sm64(env) ^ (return | length << 32)) over the valid records, so it
     depends on the set of (env, return, length) only: not on their order, on the ranks that
-    produced them or on the drain interval."""
+    produced them or on the drain interval.  ``env_below``: only the records of global envs
+    [0, env_below) (the bench compares those with the oracle's replay)."""
     r = rows.detach().cpu().numpy().reshape(-1, cap, 2)
     c = counts.detach().cpu().numpy().astype(np.int64).reshape(-1)
     if len(c) != r.shape[0]:
@@ -88,11 +89,14 @@ def episode_digest(rows, counts, cap):
     if np.any(c < 0) or np.any(c > cap):
         raise ValueError("a segment count is outside [0, cap]")
     valid = np.arange(cap)[None, :] < c[:, None]
-    v = r[valid].view(np.uint64)
+    v = r[valid]
+    if env_below is not None:
+        v = v[v[:, 0] < env_below]
+    v = v.view(np.uint64)
     with np.errstate(over="ignore"):
         h = _sm64(_sm64(v[:, 0]) ^ v[:, 1])
         digest = int(np.sum(h, dtype=np.uint64))
-    return int(c.sum()), digest
+    return len(v), digest
 
 
 def records_digest(env, ret, length):
@@ -133,12 +137,14 @@ class EpisodeLog:
         self.records.zero_()
         self.used = 0
 
-    def digest(self):
-        """(records, digest) over every drain added since the last reset (synchronises)."""
+    def digest(self, env_below=None):
+        """(records, digest) over every drain added since the last reset (synchronises);
+        ``env_below``: of the records of global envs [0, env_below) only."""
         if not self.keep:
             return int(self.records.item()), None
         n = self.used
-        return episode_digest(self.rows[:n].reshape(-1, 2), self.counts[:n].reshape(-1), self.cap)
+        return episode_digest(self.rows[:n].reshape(-1, 2), self.counts[:n].reshape(-1), self.cap,
+                              env_below)
 
 
 # ---- the launcher ---------------------------------------------------------------------------

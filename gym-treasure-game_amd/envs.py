@@ -11,6 +11,7 @@ import ctypes
 import operator
 import os
 import random
+import struct
 
 import numpy as np
 import torch
@@ -441,16 +442,19 @@ class TreasureGame:
 
     Same surface and Python types: ``reset() -> list[9]``, ``step(a) -> (list[9], int | None,
     bool, {})``, ``available_mask`` (np int array [9]), ``action_space`` Discrete(9),
-    ``observation_space`` Box(0, 1, (9,), float32), ``option_names``.  ``TreasureGame(seed=s)``
-    equals ``random.seed(s); TreasureGame()`` in a fresh reference process; ``seed=None``
-    draws a seed from Python's global ``random`` (so ``random.seed`` still makes runs
-    reproducible, but not draw-for-draw identical to the reference's shared stream), unless
-    ``share_global_random=True``: then the env draws from Python's global ``random`` itself,
-    as the reference's module-level ``random`` calls do (IM/:2, OB/): its MT state is loaded
-    from ``random.getstate()`` before every call that draws (construction, ``reset``, ``step``,
-    ``option.run``) when the global stream has moved, and stored back after, so user code that
-    interleaves its own ``random`` calls sees the reference's stream draw for draw (one
-    device round trip per call; the global ``gauss_next`` must be unset, as after ``seed``).
+    ``observation_space`` Box(0, 1, (9,), float32), ``option_names``.
+
+    Random numbers, as in the reference, come by default from Python's process-global
+    ``random`` (IM/:2, OB/:9 draw from the module-level ``random``): the constructor's build,
+    ``reset`` and ``step`` (and ``option.run``) each read ``random.getstate()``, draw on the
+    device (tg_step1_py / tg_reset1_py: one launch, one synchronisation) and store the advanced
+    state back with ``random.setstate``, so ``random.seed(s); env = TreasureGame()`` replays
+    the reference env draw for draw, and user code that takes its own ``random`` draws in
+    between (any of them: random(), randrange, gauss, ...) sees and shapes the same shared
+    stream as with the reference.  ``TreasureGame(seed=s)`` instead gives the env a private
+    stream equal to ``random.seed(s); TreasureGame()`` in a fresh reference process, and leaves
+    the global ``random`` untouched (``share_global_random=False`` with ``seed=None`` draws
+    that seed from the global stream).
     ``render(mode='rgb_array')`` returns the frame as a uint8 numpy array [624, 672, 3]
     (TG/:98-105; the sprites are the installed reference's unless ``sprites=`` is given);
     ``mode='human'`` needs gym's image viewer and raises.
@@ -459,8 +463,10 @@ class TreasureGame:
     metadata = {"render.modes": ["human", "rgb_array"]}
 
     def __init__(self, seed=None, device=None, level_dir=None, sprites=None,
-                 share_global_random=False):
+                 share_global_random=None):
         self._sprites = sprites
+        if share_global_random is None:
+            share_global_random = seed is None
         self._shared = bool(share_global_random)
         if self._shared and seed is not None:
             raise ValueError("share_global_random draws from the global random: no seed")
@@ -470,7 +476,6 @@ class TreasureGame:
         if seed >= 2**64:
             raise ValueError("seed must satisfy |seed| < 2**64 (a two-word init_by_array key)")
         self._vec = TreasureGameVec(1, seed=seed, device=device, level_dir=level_dir)
-        self._gstate = None  # the global random state this env last stored
         self.option_list = [GpuOption(self, k) for k in range(_lib.NUM_ACTIONS)]
         self.option_names = list(OPTION_NAMES)
         self.action_space = Discrete(_lib.NUM_ACTIONS)
@@ -478,38 +483,36 @@ class TreasureGame:
         self.viewer = None
         self._h_obs = np.zeros(_lib.OBS_DIM, np.float64)  # tg_step1's host outputs
         self._h_rew, self._h_valid, self._h_done = ctypes.c_int32(), ctypes.c_uint8(), ctypes.c_uint8()
+        if self._shared:
+            self._py = _lib.PyState()
+            # _TreasureGameImpl.__init__'s build draws from the global stream (IM/:31-53)
+            self._reset_py(self._h_obs)
 
-        if self._shared:  # _TreasureGameImpl.__init__'s build draws from the global stream
-            self._load_global(force=True)
-            self._vec.reset()
-            self._store_global()
+    # -- the reference's shared module-level random stream (default) -----------------------------
+    _WORDS = struct.Struct("625I")  # tg_pystate's mt[624] + index
 
-    # -- the reference's shared module-level random stream (share_global_random=True) ----------
-    def _load_global(self, force=False):
+    def _load_global(self):
         st = random.getstate()
-        if not force and st == self._gstate:
-            return  # nobody drew from the global stream since this env stored it
-        if st[2] is not None:
-            raise NotImplementedError("share_global_random: the global random holds a cached "
-                                      "gauss value (random.gauss was called an odd number of times)")
-        snap = self._vec.read_state(mt=True)
-        snap["mt"][0] = np.asarray(st[1][:624], np.uint32)
-        snap["mt_pos"][0] = st[1][624]
-        self._vec.write_state(snap)
+        self._WORDS.pack_into(self._py, 0, *st[1])
+        g = st[2]
+        self._py.has_gauss = g is not None
+        self._py.gauss_next = 0.0 if g is None else g
 
     def _store_global(self):
-        snap = self._vec.read_state(mt=True)
-        st = (3, tuple(int(w) for w in snap["mt"][0]) + (int(snap["mt_pos"][0]),), None)
-        random.setstate(st)
-        self._gstate = st
+        random.setstate((3, self._WORDS.unpack_from(self._py, 0),
+                         self._py.gauss_next if self._py.has_gauss else None))
+
+    def _reset_py(self, obs):
+        self._load_global()
+        check(self._vec._L.tg_reset1_py(self._vec.handle, ctypes.byref(self._py),
+                                        obs.ctypes.data, self._vec._stream()), "tg_reset1_py")
+        self._store_global()
 
     def reset(self):
         if self._shared:
-            self._load_global()
-        obs = self._vec.reset().cpu().numpy()[0].tolist()
-        if self._shared:
-            self._store_global()
-        return obs
+            self._reset_py(self._h_obs)
+            return self._h_obs.tolist()
+        return self._vec.reset().cpu().numpy()[0].tolist()
 
     def _mask_bits(self):
         return int(self._vec.available_mask().cpu().item()) & 0x1FF
@@ -520,17 +523,21 @@ class TreasureGame:
         return np.array([(m >> k) & 1 for k in range(_lib.NUM_ACTIONS)])
 
     def _run(self, a):
-        """option_list[a].run() on the device + get_state + done (TG/:91-96): tg_step1, one
-        launch whose kernel writes the row into pinned host memory, one synchronisation"""
+        """option_list[a].run() on the device + get_state + done (TG/:91-96): tg_step1 (or
+        tg_step1_py over the global stream), one launch whose kernel writes the row into
+        pinned host memory, one synchronisation"""
         v = self._vec
         if self._shared:
             self._load_global()
-        check(v._L.tg_step1(v.handle, int(a), self._h_obs.ctypes.data, ctypes.byref(self._h_rew),
-                            ctypes.byref(self._h_valid), ctypes.byref(self._h_done),
-                            v._stream()), "tg_step1")
-        r = int(self._h_rew.value) if self._h_valid.value else None
-        if self._shared:
+            check(v._L.tg_step1_py(v.handle, int(a), ctypes.byref(self._py), self._h_obs.ctypes.data,
+                                   ctypes.byref(self._h_rew), ctypes.byref(self._h_valid),
+                                   ctypes.byref(self._h_done), v._stream()), "tg_step1_py")
             self._store_global()
+        else:
+            check(v._L.tg_step1(v.handle, int(a), self._h_obs.ctypes.data,
+                                ctypes.byref(self._h_rew), ctypes.byref(self._h_valid),
+                                ctypes.byref(self._h_done), v._stream()), "tg_step1")
+        r = int(self._h_rew.value) if self._h_valid.value else None
         return self._h_obs.tolist(), r, bool(self._h_done.value)
 
     def step(self, action):

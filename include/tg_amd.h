@@ -57,6 +57,7 @@ extern "C" {
 #define TG_ERR_NEARINT (1u << 27)  /* reset gauss within 1e-9 of an int() boundary (libm watch) */
 #define TG_ERR_RENDER (1u << 28)   /* render: a handle shaft end point within 1e-9 of an int()
                                       boundary (libm watch), or a shaft off the screen */
+#define TG_ERR_WINDOW (1u << 29)  /* a lane drew past its staged draw codes (a bound broken: bug) */
 #define TG_ERR_STALL (1u << 31)   /* TG_MODE_ASYNC tg_rollout: a workgroup's queues stopped
                                       making progress (a bookkeeping bug; the launch gave up) */
 
@@ -75,6 +76,16 @@ typedef struct {
   int32_t ret;      /* sum of step rewards since the last reset (None counts 0) */
   int32_t len;      /* env-steps since the last reset */
 } tg_episode;
+
+/* A Python-level random stream's state, as random.getstate() holds it (CPython random.py
+ * getstate: (3, tuple of 624 MT19937 words + index, gauss_next)): the reference's envs all draw
+ * from the process-global `random` (_treasure_game_impl.py:2, _objects.py:9). */
+typedef struct {
+  uint32_t mt[624];   /* the generation CPython's genrand_uint32 reads */
+  uint32_t index;     /* its next word, 0..624 (624: twist before the next word) */
+  uint32_t has_gauss; /* gauss_next is not None */
+  double gauss_next;
+} tg_pystate;
 
 /* Counters accumulated over all tg_step calls since creation / tg_stats_reset. */
 typedef struct {
@@ -125,6 +136,18 @@ int tg_step(tg_batch *h, const int32_t *actions, double *obs, int32_t *reward, u
  * done.  Synchronises `stream`. */
 int tg_step1(tg_batch *h, int32_t action, double *obs, int32_t *reward, uint8_t *valid,
              uint8_t *done, void *stream);
+
+/* The N=1 drop-in drawing from a caller-held Python random stream instead of the env's own
+ * (TreasureGame with the reference's module-global random, IM/:2, OB/:9): `st` (host memory)
+ * is read at the call and written back with the stream advanced by exactly the draws the
+ * reference's call makes, any index (odd ones too) and gauss_next included.  One launch and one
+ * stream synchronisation per call.
+ *   tg_step1_py:  step(action) (TG/:91-96); outputs as tg_step1.
+ *   tg_reset1_py: reset() (TG/:78-81, IM/:55-73: 2 uniform + 2 gauss), also the constructor's
+ *                 build (IM/:31-53); obs f64 [9] host, may be NULL. */
+int tg_step1_py(tg_batch *h, int32_t action, tg_pystate *st, double *obs, int32_t *reward,
+                uint8_t *valid, uint8_t *done, void *stream);
+int tg_reset1_py(tg_batch *h, tg_pystate *st, double *obs, void *stream);
 
 /* K steps in one call with the on-device synthetic policy (TG_POLICY_*): step t0 + s takes
  * the actions tg_policy_actions(action_seed, t0 + s) would give, evaluated inside the step's

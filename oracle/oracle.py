@@ -51,6 +51,8 @@ def lib():
         L.tgo_predicate_table.argtypes = [P, i32, i32, i32, i32, ctypes.c_uint, P]
         L.tgo_run.restype = i32
         L.tgo_run.argtypes = [P, u64, i64, i64, i32, u64, i32, i32, P, P, P, P, P, P, P, P, i32]
+        L.tgo_run_episodes.restype = i32
+        L.tgo_run_episodes.argtypes = [P, u64, i64, i64, i32, u64, i32, i32, P, P, i32]
         L.tgo_rng_words.argtypes = [u64, i32, P]
         L.tgo_rng_random.argtypes = [u64, i32, P]
         L.tgo_rng_uniform5.argtypes = [u64, P]
@@ -178,6 +180,19 @@ def run(seed_base, g0, n, steps, action_seed, policy=0, autoreset=False, full=Tr
     if rc != 0:
         raise RuntimeError("oracle run failed")
     return out
+
+
+def run_episodes(seed_base, g0, n, steps, action_seed, policy=0, t_from=0, nthreads=0,
+                 level_dir=None):
+    """Auto-reset run of envs [g0, g0 + n): (count, digest) of the episodes whose last step
+    index is >= t_from (digest as gym_treasure_game_amd.dist.episode_digest)."""
+    cnt = ctypes.c_int64(0)
+    dig = ctypes.c_uint64(0)
+    rc = lib().tgo_run_episodes(level(level_dir), seed_base, g0, n, steps, action_seed, policy,
+                                t_from, ctypes.byref(cnt), ctypes.byref(dig), nthreads)
+    if rc != 0:
+        raise RuntimeError("oracle run failed")
+    return int(cnt.value), int(dig.value)
 
 
 def rng_words(seed, n):

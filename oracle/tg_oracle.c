@@ -1100,6 +1100,57 @@ int tgo_run(const tgo_level *lv, uint64_t seed_base, int64_t g0, int64_t n, int 
     return err ? -1 : 0;
 }
 
+/* Episodes of an auto-reset run (the step driver above, reset() after a step that returned
+ * done, TG/:91-96 + TG/:78-81): the (env, return, length) record of every episode whose last
+ * step has index >= t_from, reduced to a count and the order-independent digest of
+ * gym-treasure-game_amd/dist.py episode_digest: the sum mod 2^64 of
+ * sm64(sm64(env) ^ (return & 0xFFFFFFFF | length << 32)). */
+int tgo_run_episodes(const tgo_level *lv, uint64_t seed_base, int64_t g0, int64_t n, int steps,
+                     uint64_t action_seed, int policy, int t_from, int64_t *count,
+                     uint64_t *digest, int nthreads) {
+    int err = 0;
+    int64_t cnt = 0;
+    uint64_t dig = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads) reduction(| : err) \
+    reduction(+ : cnt, dig)
+#endif
+    for (int64_t i = 0; i < n; i++) {
+        uint64_t g = (uint64_t)(g0 + i);
+        tgo_env *e = (tgo_env *)malloc(sizeof(tgo_env));
+        if (!e) {
+            err |= 1;
+            continue;
+        }
+        double o[9], fo[9];
+        env_init(e, lv, seed_base + g, o);
+        int64_t ret = 0, len = 0;
+        for (int t = 0; t < steps; t++) {
+            unsigned m = policy ? tgo_mask(e) : 0;
+            int a = tgo_pick_action(action_seed, g, (uint64_t)t, policy, m);
+            int32_t r;
+            uint8_t v, d;
+            if (tgo_step(e, a, fo, &r, &v, &d)) err |= 1;
+            ret += r;
+            len += 1;
+            if (d) {
+                if (t >= t_from) {
+                    const uint64_t packed = ((uint64_t)ret & 0xFFFFFFFFull) | ((uint64_t)len << 32);
+                    dig += tgo_sm64(tgo_sm64(g) ^ packed);
+                    cnt += 1;
+                }
+                tgo_reset(e, o);
+                ret = len = 0;
+            }
+        }
+        free(e);
+    }
+    *count = cnt;
+    *digest = dig;
+    return err ? -1 : 0;
+}
+
 /* ======================================================================================
  * Renderer: TreasureGame.render('rgb_array') (TG/:98-105) -> _TreasureGameDrawer.draw_domain
  * (DR/ = _treasure_game_impl/_treasure_game_drawer.py, DR/:136-163, DR/:238-269).

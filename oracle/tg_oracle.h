@@ -64,6 +64,9 @@ int tgo_run(const tgo_level *lv, uint64_t seed_base, int64_t g0, int64_t n, int 
             int64_t *ticks, int nthreads);
 
 /* action stream + record hash shared with tests/golden/make_golden.py and the device code */
+int tgo_run_episodes(const tgo_level *lv, uint64_t seed_base, int64_t g0, int64_t n, int steps,
+                     uint64_t action_seed, int policy, int t_from, int64_t *count,
+                     uint64_t *digest, int nthreads);
 uint64_t tgo_sm64(uint64_t x);
 uint64_t tgo_action_hash(uint64_t a0, uint64_t g, uint64_t t);
 int tgo_pick_action(uint64_t a0, uint64_t g, uint64_t t, int masked, unsigned mask);

@@ -31,13 +31,14 @@ def main():
     n = int(os.environ.get("N", 1 << 20))
     vec = tg.TreasureGameVec(n, seed=0, autoreset=True)
     vec.reset()
+    pol = os.environ.get("POLICY", "uniform")
     for t in range(int(os.environ.get("STEPS", 30))):
-        vec.step(vec.policy_actions(t))
+        vec.step(vec.policy_actions(t, policy=pol))
     torch.cuda.synchronize()
     nw = n // 64
     buf = np.zeros((nw, 6), np.uint64)
     vec.stats_reset()
-    vec.step(vec.policy_actions(999))
+    vec.step(vec.policy_actions(999, policy=pol))
     torch.cuda.synchronize()
     _lib.check(L.tg_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), nw), "stamps")
     act = buf[:, 3] > 0

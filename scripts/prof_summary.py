@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a gpu_profile.sh session into profiles/<tag>_summary.json (+ traffic_step.json).
+"""Summarise a gpu_profile.sh session into profiles/<tag>_summary.json (+ traffic_step_<policy>.json).
 
     python scripts/prof_summary.py --tag r01 [--out gpurun_out] [--envs 1048576]
 
@@ -117,7 +117,7 @@ def main():
               "burn_in": prof_line.get("burn_in") if prof_line else None,
               "source": "profiles/%s_summary.json (rocprofv3 --pmc passes of bench.py %s)"
                         % (a.tag, "steps=%s" % last)}
-        with open(os.path.join(ROOT, "profiles", "traffic_step.json"), "w") as f:
+        with open(os.path.join(ROOT, "profiles", "traffic_step_%s.json" % a.policy), "w") as f:
             json.dump(tj, f, indent=1)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "%s_summary.json" % a.tag), "w") as f:

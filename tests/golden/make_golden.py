@@ -388,6 +388,41 @@ def make_levels(jobs):
                   jobs, seed0=50, level_dir=d)
 
 
+def make_cascade_level(jobs):
+    """A hand-made level whose trigger table makes one INTERACT tick draw many times: handle
+    0's lists toggle door 0 back and forth, door 0's lists toggle handle 1 back and forth, and
+    process_trigger clears previously_triggered on return (OB/:76-94), so every toggle changes
+    handle 1 again and wiggles it (one draw each): a successful flip of handle 0 draws up to
+    10 times.  The layout is the exit level's, so episodes finish."""
+    d = os.path.join(OUT, "levels", "cascade")
+    os.makedirs(d, exist_ok=True)
+    dom = "////L///////\n/          /\n///////L////\n/       L  /\n////////////\n"
+    objs = ("door 9 3 True\ndoor 2 3 False\ndoor 10 1 False\nhandle 6 3 False\n"
+            "handle 4 3 False\nkey 1 3\nbolt 3 3 True\ngold 7 1\n")
+    inter = ("handle 0 True door 0 False\nhandle 0 True door 0 True\n"
+             "handle 0 True door 0 False\nhandle 0 True handle 1 False\n"
+             "handle 0 False door 0 True\nhandle 0 False door 0 False\n"
+             "handle 0 False handle 1 True\n"
+             "door 0 False handle 1 True\ndoor 0 False handle 1 False\n"
+             "door 0 False handle 1 True\n"
+             "door 0 True handle 1 False\ndoor 0 True handle 1 True\n"
+             "handle 1 True door 1 True\nhandle 1 False door 1 False\n"
+             "bolt 0 True door 2 True\nbolt 0 False door 2 False\n")
+    for f, t in zip(("domain.txt", "domain-objects.txt", "domain-interactions.txt"),
+                    (dom, objs, inter)):
+        with open(os.path.join(d, f), "w") as fh:
+            fh.write(t)
+    with open(os.path.join(d, "README.md"), "w") as fh:
+        fh.write("Hand-made test level (not from the reference): the exit level's layout "
+                 "and a trigger table whose\ncascades change one handle many times, so one "
+                 "INTERACT tick takes more than 8 random() draws.\n"
+                 "traj_level_cascade_*.npz hold the reference's trajectories on it.\n")
+    make_traj("traj_level_cascade_uniform.npz", 16, 400, ACTION_SEED_UNIFORM, False, False,
+              jobs, seed0=0, level_dir=d)
+    make_traj("traj_level_cascade_masked.npz", 16, 600, ACTION_SEED_MASKED, True, True,
+              jobs, seed0=50, level_dir=d)
+
+
 # ----------------------------------------------------------------------------------------
 # F3h rolling hashes
 # ----------------------------------------------------------------------------------------
@@ -487,6 +522,8 @@ def main():
         make_predicates(a.jobs)
     if not only or "levels" in only:
         make_levels(a.jobs)
+    if not only or "cascade" in only:
+        make_cascade_level(a.jobs)
     if not only or "hash" in only:
         make_hash("hash_uniform.npz", 4096, 1000, ACTION_SEED_UNIFORM, False, a.jobs)
         make_hash("hash_masked.npz", 1024, 600, ACTION_SEED_MASKED, True, a.jobs)

@@ -55,6 +55,32 @@ def test_bad_level_is_rejected_before_touching_a_device(tg):
     assert rc == -1
 
 
+def test_cascade_draw_bound_is_checked_at_parse(tg):
+    """One INTERACT tick's random() draws are bounded per level from its trigger table
+    (tg_level.h interact_draw_bound): the cascade level's 10-draw ticks parse (TG_E_NODEV here,
+    no GPU: parsing comes first); a table whose cascades could draw more than the code window
+    stages is rejected with a message, not run past the window."""
+    lib = tg._lib.load()
+    lv = os.path.join(ROOT, "tests", "golden", "levels", "cascade")
+    texts = [open(os.path.join(lv, f), "rb").read()
+             for f in ("domain.txt", "domain-objects.txt", "domain-interactions.txt")]
+    h = ctypes.c_void_p()
+    rc = lib.tg_create(ctypes.byref(h), 4, 0, 0, 0, *texts)
+    assert rc in (0, -4), lib.tg_last_error()
+    if rc == 0:
+        lib.tg_destroy(h)
+    # handle 0 toggles door 0 seven times, door 0 toggles handle 1 seven times per change
+    alt = lambda src, dst: "".join("%s %s %s\n" % (src, dst, ("True", "False")[k % 2])
+                                   for k in range(7))
+    inter = ("".join(alt("handle 0 %s" % p, "door 0") for p in ("True", "False")) +
+             "".join(alt("door 0 %s" % p, "handle 1") for p in ("True", "False")) +
+             "".join(alt("handle 1 %s" % p, "door 1") for p in ("True", "False")) +
+             "".join(alt("door 1 %s" % p, "handle 0") for p in ("True", "False")))
+    rc = lib.tg_create(ctypes.byref(h), 4, 0, 0, 0, texts[0], texts[1], inter.encode())
+    assert rc == -1
+    assert b"INTERACT tick" in lib.tg_last_error()
+
+
 def test_no_device_fails_loudly(tg):
     import torch
     if torch.cuda.is_available():

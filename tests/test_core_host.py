@@ -137,7 +137,7 @@ def test_core_vs_oracle_corridor(hostcheck, oracle, policy, autoreset):
 LEVELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels")
 
 
-@pytest.mark.parametrize("level", ["corridor", "gen1", "gen2", "gen3", "exit"])
+@pytest.mark.parametrize("level", ["corridor", "gen1", "gen2", "gen3", "exit", "cascade"])
 @pytest.mark.parametrize("policy", ["uniform", "masked"])
 def test_core_vs_reference_levels(hostcheck, level, policy):
     """F6: the product core's level loader + physics vs the reference on other levels."""
@@ -150,7 +150,7 @@ def test_core_vs_reference_levels(hostcheck, level, policy):
     np.testing.assert_array_equal(o["draws"], d["draws"][:, -1])
 
 
-@pytest.mark.parametrize("level", [None, "corridor", "gen1", "gen2", "gen3", "exit"])
+@pytest.mark.parametrize("level", [None, "corridor", "gen1", "gen2", "gen3", "exit", "cascade"])
 @pytest.mark.parametrize("policy", [0, 1])
 def test_core_gotable_matches_direct(hostcheck, level, policy):
     """The go options' GoTable (tg_core.h go_lookup, the device's path) against the direct

@@ -173,6 +173,25 @@ def test_bench_gather_digest_independent_of_world(world):
     assert D.records_digest([1], [-5], [3]) != D.records_digest([1], [-5], [4])
 
 
+def test_oracle_episode_digest_matches_the_trajectories():
+    """oracle.run_episodes (the bench's episode parity leg) == dist.records_digest of the
+    episodes read off the oracle's full trajectories, for every start step of the window."""
+    import gym_treasure_game_amd.dist as D
+    import oracle as O
+    n, steps = 192, 1200
+    eps = _oracle_episodes(n, steps, 0x51)
+    for t_from in (0, 500, 1100):
+        sel = [e for e in eps if e[0] - 1 >= t_from]
+        want = D.records_digest([e[1] for e in sel], [e[2] for e in sel], [e[3] for e in sel])
+        assert O.run_episodes(0, 0, n, steps, 0x51, 1, t_from) == want
+    # env_below restricts a digest to the records of envs [0, env_below)
+    sel = [e for e in eps if e[1] < 50]
+    want = D.records_digest([e[1] for e in sel], [e[2] for e in sel], [e[3] for e in sel])
+    rows = torch.tensor([[e[1], (e[2] & 0xFFFFFFFF) | (e[3] << 32)] for e in eps], dtype=torch.int64)
+    assert D.episode_digest(rows, torch.tensor([len(eps)]), len(eps), env_below=50) == want
+    assert O.run_episodes(0, 0, 50, steps, 0x51, 1, 0) == want
+
+
 def test_episode_digest_checks_counts():
     import gym_treasure_game_amd.dist as D
     rows = torch.zeros((8, 2), dtype=torch.int64)

@@ -392,7 +392,7 @@ LEVELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lev
 
 
 @pytest.mark.parametrize("mode", MODES)
-@pytest.mark.parametrize("level", ["corridor", "gen1", "gen2", "gen3", "exit"])
+@pytest.mark.parametrize("level", ["corridor", "gen1", "gen2", "gen3", "exit", "cascade"])
 @pytest.mark.parametrize("policy", ["uniform", "masked"])
 def test_reference_levels(tg, level, policy, mode):
     """F6: the kernels on other levels vs the REFERENCE's trajectories on them (the reference
@@ -571,34 +571,74 @@ def test_vector_env_gymnasium_surface(tg, oracle):
     ve.close()
 
 
-def test_dropin_shares_the_global_random_stream(tg):
-    """TreasureGame(share_global_random=True) draws from Python's global random like the
-    reference's module-level calls: after random.seed(s), construction, reset, step and user
-    code's own random() calls between steps interleave on ONE stream, draw for draw.  The
-    reference side is oracle/pyref.py's Env over one Random(s) that the "user" draws from too."""
+@pytest.mark.parametrize("make", ["default", "make", "explicit"])
+def test_dropin_shares_the_global_random_stream(tg, make):
+    """TreasureGame() -- the default, as gym.make('treasure_game-v0') builds it -- draws from
+    Python's global random like the reference's module-level calls (IM/:2, OB/:9): after
+    random.seed(s), construction, reset, step and the user's own draws between steps
+    interleave on ONE stream, draw for draw.  The user's draws include single 32-bit words
+    (randrange, getrandbits(32): the index goes odd) and a lone gauss (gauss_next stays
+    cached; the reference's next reset consumes it as its first gauss).  The reference side
+    is oracle/pyref.py's Env over one Random(s) that the "user" draws from too."""
     import random
     import pyref  # test infrastructure (oracle/), on sys.path via conftest
     seed = 2024
     saved = random.getstate()
     try:
         random.seed(seed)
-        env = tg.TreasureGame(share_global_random=True)
+        env = {"default": lambda: tg.TreasureGame(),
+               "make": lambda: tg.make("treasure_game-v0"),
+               "explicit": lambda: tg.TreasureGame(share_global_random=True)}[make]()
         ref = pyref.Env(seed)
         assert env.reset() == ref.reset()
         u = random.Random(7)
-        for t in range(150):
+        resets = 0
+        for t in range(400):
             a = u.randrange(9)
-            if t % 10 == 5:  # the user's own draws from the shared stream
+            k = t % 10
+            if k == 1:
                 assert random.random() == ref.rng.random()
+            elif k == 3:
+                assert random.randrange(1000) == ref.rng.randrange(1000)
+            elif k == 5:
+                assert random.gauss(0, 1) == ref.rng.gauss(0, 1)
+            elif k == 7:
+                assert random.getrandbits(32) == ref.rng.getrandbits(32)
             st, r, d, _ = env.step(a)
             rs, rr, rd, _ = ref.step(a)
             assert (st, r, d) == (list(rs), rr, rd), t
-            if d:
+            if d or t % 40 == 6:  # some resets right after a lone gauss (gauss_next cached)
                 assert env.reset() == ref.reset()
+                resets += 1
+            assert random.getstate() == ref.rng.getstate(), t
+        assert resets >= 10
+        for k in range(9):
+            assert env.option_list[k].can_run() == bool(ref.mask() >> k & 1)
+        run = [k for k in range(9) if env.option_list[k].can_run()][0]
+        assert env.option_list[run].run() == ref.step(run)[1]
         assert random.getstate() == ref.rng.getstate()
+        assert env._vec.errors() == 0
         env.close()
     finally:
         random.setstate(saved)
+
+
+def test_dropin_with_seed_leaves_the_global_stream_alone(tg, oracle):
+    """TreasureGame(seed=s) is the private-stream env (random.seed(s); TreasureGame() in a
+    fresh reference process) and never touches Python's global random."""
+    import random
+    random.seed(99)
+    before = random.getstate()
+    env = tg.TreasureGame(seed=5)
+    ref = oracle.OracleEnv(5)
+    assert np.array_equal(np.array(env.reset()).view(np.uint64), ref.obs.view(np.uint64))
+    for t in range(50):
+        a = t % 9
+        st, r, d, _ = env.step(a)
+        rs, rr, rd, _ = ref.step(a)
+        assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)) and (r, d) == (rr, rd)
+    assert random.getstate() == before
+    env.close()
 
 
 def test_step1_rejects_batches_and_bad_outputs(tg):

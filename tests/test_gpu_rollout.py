@@ -79,7 +79,7 @@ def test_async_rollout_after_steps(tg):
     check_pair(run_pair(tg, n, k, "masked", pre_steps=9), n, k)
 
 
-@pytest.mark.parametrize("level", ["corridor", "gen2", "exit"])
+@pytest.mark.parametrize("level", ["corridor", "gen2", "exit", "cascade"])
 def test_async_rollout_levels(tg, level):
     """corridor: go options of ~650 draws (two MT generation crossings inside one step).  Some
     of its envs get stuck against an end wall in an option that never ends (the reference

@@ -80,7 +80,7 @@ def test_golden_coverage():
 
 
 LEVELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels")
-LEVEL_TRAJ = [(lv, pol) for lv in ("corridor", "gen1", "gen2", "gen3", "exit")
+LEVEL_TRAJ = [(lv, pol) for lv in ("corridor", "gen1", "gen2", "gen3", "exit", "cascade")
               for pol in ("uniform", "masked")]
 
 
