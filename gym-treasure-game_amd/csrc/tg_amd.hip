@@ -33,9 +33,9 @@ using namespace tg;
 namespace {
 
 constexpr int BLOCK = 256;
-#ifndef TG_PRIO_SLOW
-#define TG_PRIO_SLOW 3
-#endif
+// issue priority of the option waves whose ticks are slow (ladders, drops, jumps), which share
+// SIMDs with the go waves (0.153 vs 0.156 ms per step)
+constexpr int PRIO_SLOW = 3;
 
 // ------------------------------------------------------------------------------------------
 // SoA pack / unpack
@@ -117,10 +117,7 @@ __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t CODE_CHUNKS = MT_CODES / 16;  // 39
 static_assert(MT_CODES % 16 == 0, "whole 16-B code chunks per env");
-#ifndef TG_WIN_CHUNKS
-#define TG_WIN_CHUNKS 4
-#endif
-constexpr int WIN_CHUNKS = TG_WIN_CHUNKS;
+constexpr int WIN_CHUNKS = 4;  // 7 until r02e (8 instead of 5 workgroups per CU)
 constexpr int WIN_SLOT_BYTES = 64 * 16;
 constexpr int WIN_WAVE_BYTES = WIN_CHUNKS * WIN_SLOT_BYTES;  // 4 KB per wave
 constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
@@ -208,13 +205,11 @@ struct RngCodes {
         stale = NONE;
       }
     }
-#ifndef TG_DIAG_CODEHASH
 #pragma unroll
     for (int j = 0; j < WIN_CHUNKS; ++j) {
       const uint32_t c = c0 + j < CODE_CHUNKS ? c0 + j : c0 + j - CODE_CHUNKS;
       glds16(m0 + j * WIN_SLOT_BYTES, mc + c * 16u);
     }
-#endif
     rd = d & 15u;
     left = (uint32_t)WIN_CHUNKS * 16u - rd;
     loaded = false;
@@ -244,16 +239,50 @@ struct RngCodes {
   }
   // at least k draws staged (no refill: the plain go loop's exit test)
   __device__ __forceinline__ bool has(uint32_t k) const { return left >= k; }
+  // the code dword holding draws 4d .. 4d + 3 of the window (d < WIN_CHUNKS * 4)
+  __device__ __forceinline__ uint32_t dword(uint32_t d) const {
+    return *reinterpret_cast<const lds_u32*>(cell + (d >> 2) * WIN_SLOT_BYTES + (d & 3u) * 4u);
+  }
+  // walk_ticks (tg_core.h) four draws per LDS read: the codes of a dword are applied one by one
+  // (each tick checks the span, the staged draws and the cap at its start, as walk_ticks), so
+  // the result is walk_ticks's; the next dword is read while this one is applied
+  template <int DIR>
+  __device__ __forceinline__ int walk(int& x, const int lim, const int cap) {
+    int taken = 0;
+    if (!((DIR > 0 ? x <= lim : x >= lim) && left >= TICK_DRAWS && cap > 0)) return 0;
+    uint32_t w = dword(rd >> 2);
+    while (true) {
+      const uint32_t wn = dword((rd >> 2) + 1u);  // inside the window: left >= TICK_DRAWS here
+      const int k = (int)(rd & 3u);
+      int moved = 0;
+      bool act = true;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int st = code_step((w >> (8 * i)) & 0xFFu, DIR < 0);
+        act = act && (i >= k ? ((DIR > 0 ? x <= lim : x >= lim) &&
+                                left - (uint32_t)moved >= TICK_DRAWS && taken + moved < cap)
+                             : true);
+        if (i >= k && act) {
+          x += st;
+          ++moved;
+        }
+      }
+      taken += moved;
+      rd += (uint32_t)moved;
+      left -= (uint32_t)moved;
+      n += (uint32_t)moved;
+      draws += (uint32_t)moved;
+      if (moved < 4 - k) break;  // the walk stopped inside this dword
+      if (!((DIR > 0 ? x <= lim : x >= lim) && left >= TICK_DRAWS && taken < cap)) break;
+      w = wn;
+    }
+    nxc = read();  // code() reads one draw ahead
+    return taken;
+  }
   // a draw was taken past the staged window (reserve's bound broken: flagged E_WINDOW)
   __device__ __forceinline__ bool overrun() const { return left > (uint32_t)WIN_CHUNKS * 16u; }
   // one draw, consumed for its outcomes (draw_code); reserve() guarantees it is in the window
   __device__ __forceinline__ uint32_t code() {
-#ifdef TG_DIAG_CODEHASH  // DIAGNOSTIC BUILD ONLY: codes from a register hash (prices the window)
-    uint32_t z = (pos + 2 * n) * 0x9E3779B9u;
-    z ^= z >> 15;
-    ++n; ++draws; --left;
-    return z & 0x3Fu;
-#endif
     const uint32_t c = nxc;
     ++n;
     ++draws;
@@ -290,13 +319,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
   return ((uint64_t)hi << 32) | lo;
 }
-// Regenerate one env's stale half with the whole wave: dst = twist_gen(src), 64 words per round,
-// coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
-// earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart).  src / dst are
-// wave-uniform; must be reached by all 64 lanes of the wave.
-#ifndef TG_TWIST_FENCE
-#define TG_TWIST_FENCE 1  // 0: s_waitcnt lgkmcnt(0) after every round of the twist (A/B builds)
-#endif
+// The whole-wave twist's inputs: 30 dwords per lane, loaded by twist_load, used by twist_store.
 struct TwistIn {
   static constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
   uint32_t a[ROUNDS], b[ROUNDS], c[4];
@@ -325,16 +348,13 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
       scratch[p] = w;
       dst[p] = w;
     }
-#if TG_TWIST_FENCE
     // round r visible to later rounds, whose lanes read what other lanes wrote: a wavefront-scope
     // fence orders the LDS accesses in the compiler (one wave's LDS operations execute in
-    // order), without the hardware wait for the store's completion
+    // order), without the hardware wait for the store's completion (A/B against s_waitcnt
+    // lgkmcnt(0) after every round: 0.1322 vs 0.1340 ms)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#else
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // round r visible to later rounds
-#endif
   }
   // the generation's 312 draw codes, 4 per lane (one 4-B store each)
 #pragma unroll
@@ -350,8 +370,8 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
 }
 // Regenerate one env's stale half with the whole wave: dst = twist_gen(src), 64 words per round,
 // coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
-// earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart; the wait after each
-// round is needed: without it the results differ).  src / dst are wave-uniform; must be reached
+// earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart; twist_store orders
+// the rounds' LDS accesses with wavefront fences).  src / dst are wave-uniform; must be reached
 // by all 64 lanes of the wave.
 __device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
                                            lds_u32* scratch) {
@@ -590,9 +610,6 @@ __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int6
   }
 }
 
-#ifndef TG_CLASSIFY_STAGE_OBS
-#define TG_CLASSIFY_STAGE_OBS 1
-#endif
 // The obs rows of a wave's 64 consecutive envs (4,608 B) through LDS: lane l stores the
 // 8-B words l, l+64, ... of the span, so each store instruction writes 512 contiguous bytes
 // (a lane storing its own 72-B row touches ~36 cache lines per instruction).  Rows of envs
@@ -675,43 +692,54 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
 // ---- two-pass compacted step (TG_MODE_COMPACT) -------------------------------------------
 // Pass 1, k_classify: one lane per env (coalesced).  Evaluates option_list[a].can_run();
 // envs whose option cannot run finish here (reward None, obs/done rows written, state
-// unchanged); the rest are appended to per-option worklists.  Appends are aggregated per
-// workgroup in LDS and the counters are sharded 8 ways (blockIdx % 8) across cache lines, so
-// each counter word sees ~1/72 of the workgroups (one word alone saturates at ~88 atomics/us,
+// unchanged); the rest are appended to per-(option, length class) worklists (buckets;
+// tg_core.h length_class).  Appends are aggregated per workgroup in LDS and the counters are
+// sharded 8 ways (blockIdx % 8) across cache lines (one word alone saturates at ~88 atomics/us,
 // MI355X_MICROARCH.md "dequeue").
-// Pass 2, k_run: wave w runs chunk w (64 envs) of the worklists concatenated in
-// longest-option-first order, so a wavefront holds only envs that tick, mostly of one option
-// (uniform control flow, similar lengths); low chunk ids dispatch first.
+// Pass 2, k_run: wave w runs chunk w (64 envs) of the worklists concatenated in run order:
+// options in kOrder, each option's classes longest first, each class's 8 shards.  Only the
+// options are padded to whole chunks, so every wave holds ONE option (wave-uniform k selects a
+// loop specialised to that option's primitive actions) and lanes of neighbouring classes.
 constexpr int SHARDS = 8;
-constexpr int NSEG = O_COUNT * SHARDS;
+constexpr int kOrderH[O_COUNT] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
+                                  O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
+                                  O_INTERACT};
+struct Buckets {
+  int base[O_COUNT];  // first bucket of option k
+  int count;
+};
+constexpr Buckets make_buckets() {
+  Buckets b{};
+  int acc = 0;
+  for (int j = 0; j < O_COUNT; ++j) {
+    b.base[kOrderH[j]] = acc;
+    acc += nclass(kOrderH[j]);
+  }
+  b.count = acc;
+  return b;
+}
+constexpr Buckets kBuckets = make_buckets();
+constexpr int NBUCKET = kBuckets.count;  // 61
+constexpr int NSEG = NBUCKET * SHARDS;    // segment = bucket * SHARDS + shard, in run order
+static_assert(NSEG <= 2 * BLOCK, "k_run's prefix: two segments per thread");
+constexpr int NCTR = NSEG + 8;  // the worklist counters, then k_run's refill queues (one per XCD)
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
 struct Work {
-  int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = option * SHARDS + shard
+  int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = bucket * SHARDS + shard
   // the listed envs' state, in worklist order (written by k_classify, which has loaded it
   // anyway): k_run reads its chunk's 64 records coalesced, in one round trip with the list
   // entries, instead of a dependent gather of 16 + 16 + 8 scattered bytes per lane
   uint4* __restrict__ wst4;      // [NSEG][shard_cap]
   double2* __restrict__ wang;
   int2* __restrict__ wep;
-  int32_t* __restrict__ ctr;     // [NSEG * CTR_STRIDE], this step's counters
+  int32_t* __restrict__ ctr;     // [NCTR * CTR_STRIDE], this step's counters
   int32_t* __restrict__ ctr_next;  // the other parity's, zeroed here for the next step
   uint32_t* __restrict__ refill;  // [n]: per classify wave w, slots 64w..: env | source half
   uint8_t* __restrict__ nrefill;  // [n / 64]: entries of classify wave w (no atomics)
   int64_t shard_cap;
 };
-#ifndef TG_PRIO_IDLE
-#define TG_PRIO_IDLE 0  // > 0: the idle waves' issue priority while they regenerate (A/B builds)
-#endif
-#ifndef TG_CLS_REFILL
-#define TG_CLS_REFILL 0  // 1: k_classify regenerates the stale halves itself (A/B builds)
-#endif
-#ifndef TG_TWIST_PIPE
-#define TG_TWIST_PIPE 1  // 0: the idle waves' twists one after another (A/B builds)
-#endif
-#ifndef TG_IDLE_WAVES
-#define TG_IDLE_WAVES 0  // > 0: at most this many idle waves regenerate (each loops over more)
-#endif
 constexpr int REFILL_BLOCKS = 64;  // k_run workgroups beyond the padded worklists (>= 256 idle waves)
+constexpr int REFILL_GRAB = 2;     // refill regions a wave takes from its XCD's queue at a time
 // worklist order = the order the chunks' loads reach HBM at the kernel's start (all option
 // waves are resident at once and issue their loads together): the jump waves first, whose
 // ticks are the slowest in wall time (~2,100 cycles each) and which end the kernel, then the
@@ -720,6 +748,9 @@ constexpr int REFILL_BLOCKS = 64;  // k_run workgroups beyond the padded worklis
 __constant__ int kOrder[O_COUNT] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
                                     O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
                                     O_INTERACT};
+__constant__ int kBucketBase[O_COUNT] = {kBuckets.base[0], kBuckets.base[1], kBuckets.base[2],
+                                         kBuckets.base[3], kBuckets.base[4], kBuckets.base[5],
+                                         kBuckets.base[6], kBuckets.base[7], kBuckets.base[8]};
 
 template <bool AUTORESET, bool FINAL, int POL = -1>
 __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
@@ -727,9 +758,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      StepIO io, EpQueue q, Work w, int64_t g0,
                                                      unsigned long long* __restrict__ stats,
                                                      uint32_t* __restrict__ err_or) {
-  __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
-#if TG_CLASSIFY_STAGE_OBS
-  // the obs staging reuses the level's LDS: nothing reads the grid after the first barrier
+  __shared__ int bcnt[NBUCKET], bbase[NBUCKET];
+  // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
   // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
   // keeps 8 waves per SIMD
   __shared__ union {
@@ -739,9 +769,6 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   LdsLevel& lv = lds.lv;
   double* const ostage = lds.ostage;
   double orow[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-#else
-  __shared__ LdsLevel lv;
-#endif
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
   const int lane = threadIdx.x & 63;
@@ -757,8 +784,9 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     a2 = S.ang[i];
     ep = S.ep[i];
   }
-  if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < NSEG) w.ctr_next[threadIdx.x * CTR_STRIDE] = 0;
+  if (threadIdx.x < NBUCKET) bcnt[threadIdx.x] = 0;
+  if (blockIdx.x == 0)
+    for (int c = threadIdx.x; c < NCTR; c += BLOCK) w.ctr_next[c * CTR_STRIDE] = 0;
   stage_level(lv, grid, L);  // includes the barrier
   const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
   int k = -1;
@@ -772,19 +800,12 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
       if (io.actions) io.actions[i] = act;
     }
     k = option_index(act);
-#ifdef TG_DIAG_CLS_NOCANRUN  // DIAGNOSTIC BUILD ONLY: prices can_run (results wrong)
-    runs = k >= 0 && ((sm64((uint64_t)i ^ (uint64_t)io.t) & 7u) < 2u) && k != O_INTERACT;
-#else
     runs = k >= 0 && can_run(L, m, e, k);
-#endif
   }
+  const int bk = runs ? kBucketBase[k] + length_class(L, m, e, k) : -1;  // the env's bucket
   // halves left in the previous step (MT_STALE) go on the refill list; k_run's idle waves
   // regenerate them beside the option loops (a lane that needs one first does it itself)
-#if TG_CLS_REFILL
-  if (false) {
-#else
   {
-#endif
     const bool stale = live && (e.mti & MT_STALE);
     const unsigned long long b = __ballot(stale);
     const int64_t wv = i >> 6;
@@ -793,18 +814,20 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
           (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
     if (lane == 0) w.nrefill[wv] = (uint8_t)__popcll(b);
   }
-  // workgroup-local slots: one LDS atomic per wave and option
+  // workgroup-local slots: one LDS atomic per wave and bucket present in the wave (the
+  // wave's lanes are matched bucket by bucket)
   int slot = 0;
-#pragma unroll
-  for (int kk = 0; kk < O_COUNT; ++kk) {
-    const bool mine = runs && k == kk;
-    const unsigned long long b = __ballot(mine);
-    if (b) {
-      const int first = __ffsll((long long)b) - 1;
+  {
+    unsigned long long pend = __ballot(runs);
+    while (pend) {
+      const int first = __ffsll((long long)pend) - 1;
+      const int b0 = __builtin_amdgcn_readlane(bk, first);
+      const unsigned long long b = __ballot(bk == b0);
       int base = 0;
-      if (lane == first) base = atomicAdd(&bcnt[kk], __popcll(b));
+      if (lane == first) base = atomicAdd(&bcnt[b0], __popcll(b));
       base = __shfl(base, first, 64);
-      if (mine) slot = base + __popcll(b & ((1ull << lane) - 1ull));
+      if (bk == b0) slot = base + __popcll(b & ((1ull << lane) - 1ull));
+      pend &= ~b;
     }
   }
   __syncthreads();
@@ -812,27 +835,11 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   // reward-None envs are finished (their latency overlaps that work)
   const int shard = blockIdx.x % SHARDS;
   int my_base = 0;
-  if (threadIdx.x < O_COUNT) {
+  if (threadIdx.x < NBUCKET) {
     const int c = bcnt[threadIdx.x];
     my_base = c ? atomicAdd(&w.ctr[(threadIdx.x * SHARDS + shard) * CTR_STRIDE], c) : 0;
   }
   uint4 s4w = s4;  // the state the worklist copy carries
-  int cls_regens = 0;
-#if TG_CLS_REFILL
-  // (A/B) the stale halves regenerated here, by this wave (its obs staging area as the twist's
-  // scratch: the grid is no longer read after the barrier above), instead of k_run's idle waves
-  {
-    const unsigned long long need = __ballot(live && (e.mti & MT_STALE));
-    if (lane == 0) w.nrefill[i >> 6] = 0;
-    if (need) {
-      wave_refill(need, S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES, e.mti,
-                  (lds_u32*)(ostage + (threadIdx.x & ~63) * 9));
-      e.mti &= ~MT_STALE;
-      s4w.w &= ~MT_STALE;
-    }
-    cls_regens = __popcll(need);
-  }
-#endif
 
   // envs whose option cannot run: reward None, state unchanged (TG/:91-96, OP/:22-23)
   bool dn = false;
@@ -844,24 +851,14 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     dn = is_done(e);
     Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
     StepResult r{0, 0, (int)dn, 0};
-#if TG_CLASSIFY_STAGE_OBS
-#ifdef TG_DIAG_CLS_NOFINISH  // DIAGNOSTIC BUILD ONLY: prices the invalid envs' finish
-    io.reward[i] = 0; io.valid[i] = 0; io.done[i] = (uint8_t)dn;
-#else
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io, orow);
-#endif
-#else
-    finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
-#endif
     e.mti = rng.finish_queued();  // the stale half, if any, is on the refill list
     draws = rng.draws;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, q, stats);
-#if TG_CLASSIFY_STAGE_OBS
   store_obs_wave(io.obs, i - lane, __ballot(live && !runs), orow,
                  ostage + (threadIdx.x & ~63) * 9);
-#endif
   if (live && !runs) {
     const uint4 s4n = pack(e);
     if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w) {  // reset / flag
@@ -870,17 +867,17 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     }
     S.ep[i] = ep;
   }
-  if (threadIdx.x < O_COUNT) bbase[threadIdx.x] = my_base;
+  if (threadIdx.x < NBUCKET) bbase[threadIdx.x] = my_base;
   __syncthreads();
   if (runs) {
-    const int64_t at = (int64_t)(k * SHARDS + shard) * w.shard_cap + bbase[k] + slot;
+    const int64_t at = (int64_t)(bk * SHARDS + shard) * w.shard_cap + bbase[bk] + slot;
     w.lists[at] = (int32_t)i;
     w.wst4[at] = s4w;
     w.wang[at] = a2;
     w.wep[at] = ep;
   }
   wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
-              AUTORESET ? (live && !runs && dn) : 0, cls_regens);
+              AUTORESET ? (live && !runs && dn) : 0);
 }
 
 #ifdef TG_DIAG_STAMPS
@@ -891,46 +888,69 @@ __device__ unsigned long long g_stamps[(1 << 16) * 6];  // per wave: 4 durations
 #define TG_STAMP(v) (void)0
 #endif
 
-#ifdef TG_RUN_MINW  // waves per SIMD k_run's register budget is sized for (A/B builds)
-#define TG_RUN_BOUNDS __launch_bounds__(BLOCK, TG_RUN_MINW)
-#else
-#define TG_RUN_BOUNDS __launch_bounds__(BLOCK)
-#endif
 template <bool AUTORESET, bool FINAL>
-__global__ TG_RUN_BOUNDS void k_run(Soa S, int64_t n, Level L,
+__global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
                                                 const uint32_t* __restrict__ grid, StepIO io,
                                                 EpQueue q, Work w, int64_t g0,
                                                 unsigned long long* __restrict__ stats,
                                                 uint32_t* __restrict__ err_or) {
-  // segments padded to whole chunks so that every wave holds ONE option (wave-uniform k
-  // selects a loop specialised to that option's primitive actions)
-  __shared__ int pre[NSEG + 1];  // exclusive prefix of the padded segments in run order
+  // the worklists in run order: pre[s] = envs listed before segment s (exclusive prefix of the
+  // counters, two segments per thread), then per option (run order j) its first segment's
+  // prefix and its start in the chunk space, where each option is padded to whole chunks
+  __shared__ int pre[NSEG + 1];
+  __shared__ int wtot[BLOCK / 64];
+  __shared__ int ostart[O_COUNT + 1], oraw[O_COUNT + 1];
+  {
+    const int s0 = 2 * (int)threadIdx.x, ln = threadIdx.x & 63;
+    const int c0 = s0 < NSEG ? w.ctr[s0 * CTR_STRIDE] : 0;
+    const int c1 = s0 + 1 < NSEG ? w.ctr[(s0 + 1) * CTR_STRIDE] : 0;
+    int v = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(v, o, 64);
+      if (ln >= o) v += y;
+    }
+    if (ln == 63) wtot[threadIdx.x >> 6] = v;
+    __syncthreads();
+    for (int wv = 0; wv < (int)(threadIdx.x >> 6); ++wv) v += wtot[wv];
+    const int excl = v - c0 - c1;
+    if (s0 < NSEG) pre[s0] = excl;
+    if (s0 + 1 < NSEG) pre[s0 + 1] = excl + c0;
+    if (threadIdx.x == BLOCK - 1) pre[NSEG] = v;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
-    for (int b = 0; b < O_COUNT; ++b)
-      for (int sh = 0; sh < SHARDS; ++sh) {
-        pre[b * SHARDS + sh] = acc;
-        acc += (w.ctr[(kOrder[b] * SHARDS + sh) * CTR_STRIDE] + 63) & ~63;
-      }
-    pre[NSEG] = acc;
+    for (int j = 0; j < O_COUNT; ++j) {
+      const int kj = kOrder[j];
+      const int sb = kBucketBase[kj] * SHARDS, se = (kBucketBase[kj] + nclass(kj)) * SHARDS;
+      ostart[j] = acc;
+      oraw[j] = pre[sb];
+      acc += (pre[se] - pre[sb] + 63) & ~63;
+    }
+    ostart[O_COUNT] = acc;
+    oraw[O_COUNT] = pre[NSEG];
   }
   __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
   LEVEL_IN_LDS();  // includes the barrier
-  const int total = pre[NSEG];
+  const int total = ostart[O_COUNT];
   const int base = (blockIdx.x * BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
-  int seg = 0;  // pre[seg] <= base < pre[seg + 1] (wave-uniform)
-  if (base < total) {
-    int lo = 0, hi = NSEG;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (pre[mid] <= base) lo = mid; else hi = mid;
+  int oj = 0;  // ostart[oj] <= base < ostart[oj + 1] (wave-uniform)
+  while (oj + 1 < O_COUNT && ostart[oj + 1] <= base) ++oj;
+  oj = __builtin_amdgcn_readfirstlane(oj);
+  const int k = kOrder[oj];
+  // this lane's place in option k's lists (the raw prefix's coordinates), and its segment
+  const int qraw = oraw[oj] + base + (threadIdx.x & 63) - ostart[oj];
+  const bool live = base < total && qraw < oraw[oj + 1];
+  int seg = kBucketBase[k] * SHARDS;
+  if (live) {
+    int hi = (kBucketBase[k] + nclass(k)) * SHARDS;  // pre[seg] <= qraw < pre[hi]
+    while (hi - seg > 1) {
+      const int mid = (seg + hi) >> 1;
+      if (pre[mid] <= qraw) seg = mid; else hi = mid;
     }
-    seg = lo;
   }
-  seg = __builtin_amdgcn_readfirstlane(seg);
-  const int k = kOrder[seg / SHARDS], sh = seg % SHARDS;
-  const int idx = base + (threadIdx.x & 63) - pre[seg];
-  const bool live = base < total && idx < w.ctr[(k * SHARDS + sh) * CTR_STRIDE];
+  const int idx = qraw - pre[seg];
   int64_t i = 0;
   StepResult r{0, 0, 0, 0};
   Env e;
@@ -947,18 +967,14 @@ __global__ TG_RUN_BOUNDS void k_run(Soa S, int64_t n, Level L,
 #endif
   (void)t0; (void)t1; (void)t2; (void)t3;
   if (live) {
-    const int64_t at = (int64_t)(k * SHARDS + sh) * w.shard_cap + idx;
+    const int64_t at = (int64_t)seg * w.shard_cap + idx;
     i = w.lists[at];
     unpack(w.wst4[at], w.wang[at], e);
     ep = w.wep[at];
     RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
     rng.prime();  // issue the code loads now; the first draw comes after the policy setup
     TG_STAMP(t1);
-#if TG_PRIO_SLOW
-    // the options whose ticks are slow (ladders, drops, jumps) end the kernel: give their waves
-    // issue priority over the go waves they share SIMDs with (0.153 vs 0.156 ms per step)
-    if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(TG_PRIO_SLOW);
-#endif
+    if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
     run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform: one specialised loop
     TG_STAMP(t2);
     r.done = is_done(e);
@@ -974,94 +990,51 @@ __global__ TG_RUN_BOUNDS void k_run(Soa S, int64_t n, Level L,
     S.ang[i] = make_double2(e.ang0, e.ang1);
     S.ep[i] = ep;
   }
-#ifdef TG_DIAG_NOIDLE  // DIAGNOSTIC BUILD ONLY: no refills on the idle waves (results wrong)
-  if (false) {
-#else
-  if (base >= total) {
-#endif
-    // an idle wave: regenerate stale MT halves listed by k_classify, beside the option loops
-    // (an env's half may also be regenerated by its own lane if it needs it first; both write
-    // the same generation)
-#if TG_PRIO_IDLE
-    __builtin_amdgcn_s_setprio(TG_PRIO_IDLE);  // (A/B) the refills end the kernel (§3.3)
-#endif
-    const int nidle_all = (int)gridDim.x * (BLOCK / 64) - total / 64;
-#if TG_IDLE_WAVES
-    const int nidle = nidle_all < TG_IDLE_WAVES ? nidle_all : TG_IDLE_WAVES;
-#else
-    const int nidle = nidle_all;
-#endif
+  __builtin_amdgcn_s_setprio(0);
+  // The stale MT halves k_classify listed (per classify wave = region of 64 envs), regenerated
+  // by whichever waves are free: idle waves at once, option waves as soon as their option is
+  // done.  Regions go out REFILL_GRAB at a time from one counter per XCD (blockIdx.x % 8:
+  // regions xcd, xcd + 8, ...), so the twists spread over every wave: with the idle waves alone
+  // a masked step queued its ~130k halves on ~300 waves (~690 us of k_run's ~885, r03a stamps).
+  // An env's half may also be regenerated by its own lane if it needs it first; both write the
+  // same generation.  Every lane of the wave reaches this.
+  {
+    const int xcd = (int)(blockIdx.x & 7u);
     const int nregions = (int)((n + 63) >> 6);  // k_classify's waves
-    const int iw = (base - total) / 64;  // this idle wave; those past nidle have nothing to do
-    for (int rg = iw; iw < nidle && rg < nregions; rg += nidle) {
-      // the stale MT halves k_classify listed for these 64 envs: lane j loads entry j, and the
-      // twists are software-pipelined (twist j + 1's loads are in flight while twist j computes
-      // and stores: A/B in DESIGN.md §3.3)
-      const int cnt = __builtin_amdgcn_readfirstlane((int)w.nrefill[rg]);
-      regens += cnt;
-      if (!cnt) continue;
-      const int lane = threadIdx.x & 63;
-      const uint32_t ent_l = lane < cnt ? w.refill[(int64_t)rg * 64 + lane] : 0u;
-#if TG_TWIST_PIPE == 2
-      // two twists in flight: t0 / t1 hold entries j / j + 1; each is reloaded right after its
-      // twist is stored, while the other one computes (no register copies of pending loads)
-      TwistIn t0, t1;
-      auto src_of = [&](uint32_t en) {
-        return (const glb_u32*)(S.mt + (int64_t)(en & 0x7FFFFFFFu) * MT_WORDS + ((en >> 31) ? MT_N : 0));
-      };
-      auto store_to = [&](const TwistIn& u, uint32_t en) {
-        const int64_t env = (int64_t)(en & 0x7FFFFFFFu);
-        const uint32_t src = (en >> 31) ? (uint32_t)MT_N : 0u;
-        twist_store(u, (glb_u32*)(S.mt + env * MT_WORDS + (MT_N - src)),
-                    S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
-      };
-      uint32_t e0 = __builtin_amdgcn_readfirstlane(ent_l), e1 = 0u;
-      twist_load(src_of(e0), t0);
-      if (cnt > 1) {
-        e1 = __builtin_amdgcn_readlane(ent_l, 1);
-        twist_load(src_of(e1), t1);
-      }
-      for (int j = 0; j < cnt; j += 2) {
-        store_to(t0, e0);
-        if (j + 2 < cnt) {
-          e0 = __builtin_amdgcn_readlane(ent_l, j + 2);
-          twist_load(src_of(e0), t0);
-        }
-        if (j + 1 < cnt) {
-          store_to(t1, e1);
-          if (j + 3 < cnt) {
-            e1 = __builtin_amdgcn_readlane(ent_l, j + 3);
-            twist_load(src_of(e1), t1);
+    const int nmine = (nregions - xcd + 7) >> 3;  // this XCD's regions: xcd + 8 j, j < nmine
+    int32_t* const rq = w.ctr + (NSEG + xcd) * CTR_STRIDE;
+    const int lane = threadIdx.x & 63;
+    while (true) {
+      int j0 = 0;
+      if (lane == 0) j0 = atomicAdd(rq, REFILL_GRAB);
+      j0 = __builtin_amdgcn_readfirstlane(j0);
+      if (j0 >= nmine) break;
+      const int j1 = j0 + REFILL_GRAB < nmine ? j0 + REFILL_GRAB : nmine;
+      for (int j = j0; j < j1; ++j) {
+        const int rg = xcd + 8 * j;
+        // lane e holds entry e; the twists are software-pipelined: twist e + 1's loads are in
+        // flight while twist e computes and stores (A/B in DESIGN.md §3.3)
+        const int cnt = __builtin_amdgcn_readfirstlane((int)w.nrefill[rg]);
+        regens += cnt;
+        if (!cnt) continue;
+        const uint32_t ent_l = lane < cnt ? w.refill[(int64_t)rg * 64 + lane] : 0u;
+        TwistIn t;
+        uint32_t ent = __builtin_amdgcn_readfirstlane(ent_l);
+        twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
+                                    ((ent >> 31) ? MT_N : 0)), t);
+        for (int e2 = 0; e2 < cnt; ++e2) {
+          const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
+          const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
+          TwistIn u = t;
+          if (e2 + 1 < cnt) {
+            ent = __builtin_amdgcn_readlane(ent_l, e2 + 1);
+            twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
+                                        ((ent >> 31) ? MT_N : 0)), t);
           }
+          twist_store(u, (glb_u32*)(S.mt + env * MT_WORDS + (MT_N - src)),
+                      S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
         }
       }
-#elif TG_TWIST_PIPE
-      TwistIn t;
-      uint32_t ent = __builtin_amdgcn_readfirstlane(ent_l);
-      twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
-                                  ((ent >> 31) ? MT_N : 0)), t);
-      for (int j = 0; j < cnt; ++j) {
-        const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
-        const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
-        TwistIn u = t;
-        if (j + 1 < cnt) {
-          ent = __builtin_amdgcn_readlane(ent_l, j + 1);
-          twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
-                                      ((ent >> 31) ? MT_N : 0)), t);
-        }
-        twist_store(u, (glb_u32*)(S.mt + env * MT_WORDS + (MT_N - src)),
-                    S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
-      }
-#else
-      for (int j = 0; j < cnt; ++j) {
-        const uint32_t ent = __builtin_amdgcn_readlane(ent_l, j);
-        const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
-        uint32_t* const env_mt = S.mt + env * MT_WORDS;
-        const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
-        wave_twist((const glb_u32*)(env_mt + src), (glb_u32*)(env_mt + (MT_N - src)),
-                   S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
-      }
-#endif
     }
   }
   wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
@@ -1505,13 +1478,9 @@ __global__ __launch_bounds__(RO_THREADS, TG_RO_MINW) void k_rollout(Soa S, int64
       int t = Q.tstep[j];
       RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
       rng.prime();
-#if TG_PRIO_SLOW
-      if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(TG_PRIO_SLOW);
-#endif
+      if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
       run_option(L, trig, m, e, k, rng, r);
-#if TG_PRIO_SLOW
       __builtin_amdgcn_s_setprio(0);
-#endif
       r.done = is_done(e);
       finish_step<AUTORESET, false>(L, e, rng, i, r, ep, step_io(R, t, n));
       e.mti = rng.finish();
@@ -1686,6 +1655,8 @@ struct PyRng {
   __device__ __forceinline__ void reserve(uint32_t) {}
   __device__ __forceinline__ bool has(uint32_t) const { return true; }
   __device__ __forceinline__ bool overrun() const { return false; }
+  template <int DIR>
+  __device__ __forceinline__ int walk(int& x, int lim, int cap) { return walk_ticks<DIR>(*this, x, lim, cap); }
 };
 // dst = twist_gen(src) with the 64 lanes of the (only) wave, both in LDS
 __device__ __forceinline__ void lds_twist64(const uint32_t* src, uint32_t* dst) {
@@ -1772,8 +1743,9 @@ __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4,
 
 namespace {
 int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
-// k_run needs one wave per 64-lane chunk of the padded worklists: at most n/64 + NSEG chunks
-int run_grid_for(int64_t n) { return grid_for(n) + (NSEG * 64 + BLOCK - 1) / BLOCK + REFILL_BLOCKS; }
+// k_run needs one wave per 64-lane chunk of the worklists, each option padded to whole chunks:
+// at most n/64 + O_COUNT chunks
+int run_grid_for(int64_t n) { return grid_for(n) + (O_COUNT * 64 + BLOCK - 1) / BLOCK + REFILL_BLOCKS; }
 // per-block launch-counter slots cover the largest step grid
 // one counter slot per workgroup of the widest step launch: k_run, or k_rollout (>= 64 envs
 // per workgroup)
@@ -1870,7 +1842,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->wst4, sizeof(uint4) * NSEG * (size_t)h->shard_cap);
   ALLOC(h->wang, sizeof(double2) * NSEG * (size_t)h->shard_cap);
   ALLOC(h->wep, sizeof(int2) * NSEG * (size_t)h->shard_cap);
-  ALLOC(h->wctr, sizeof(int32_t) * 2 * NSEG * CTR_STRIDE);
+  ALLOC(h->wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
   ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63));
   ALLOC(h->nrefill, (size_t)((n + 63) >> 6));
 #undef ALLOC
@@ -1878,7 +1850,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->gotab, gotab.data(), sizeof(uint32_t) * gotab.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
-      hipMemset(h->wctr, 0, sizeof(int32_t) * 2 * NSEG * CTR_STRIDE) != hipSuccess ||
+      hipMemset(h->wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE) != hipSuccess ||
       hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)) != hipSuccess ||
       hipMemset(h->err, 0, sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail(TG_E_HIP, "tg_create: upload failed"));
@@ -1953,8 +1925,8 @@ int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
   } else {
     // counters double-buffered by step parity: k_classify zeroes the next step's set (the
     // previous k_run, which read it, has finished), so no memset launch per step
-    int32_t* const cur = h->wctr + (h->parity ? NSEG * CTR_STRIDE : 0);
-    int32_t* const nxt = h->wctr + (h->parity ? 0 : NSEG * CTR_STRIDE);
+    int32_t* const cur = h->wctr + (h->parity ? NCTR * CTR_STRIDE : 0);
+    int32_t* const nxt = h->wctr + (h->parity ? 0 : NCTR * CTR_STRIDE);
     h->parity ^= 1;
     const Work w{h->wl, h->wst4, h->wang, h->wep, cur, nxt, h->refill, h->nrefill, h->shard_cap};
     decltype(&k_classify<true, true>) kc;

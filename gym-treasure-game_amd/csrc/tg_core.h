@@ -187,6 +187,21 @@ TG_HD void gen_codes(const uint32_t* words, uint8_t* c) {
   for (int k = 0; k < MT_N / 2; ++k) c[k] = (uint8_t)draw_code(mt_double(words[2 * k], words[2 * k + 1]));
 }
 
+// Plain ticks of a walk along one axis (the go / ladder loops' plain phases, run_option_k):
+// while the coordinate x is inside its span (x <= lim moving in +, x >= lim moving in -), at
+// least TICK_DRAWS draws are staged (rng.has) and fewer than `cap` ticks were taken, one draw
+// moves x by its noisy step (IM/:361-366: +2..+4 or -4..-2).  Returns the ticks taken.  The
+// device's RngCodes takes them four draws per LDS read (RngCodes::walk), with the same result.
+template <int DIR, class R>
+TG_HD int walk_ticks(R& rng, int& x, int lim, int cap) {
+  int t = 0;
+  while ((DIR > 0 ? x <= lim : x >= lim) && rng.has(TICK_DRAWS) && t < cap) {
+    x += code_step(rng.code(), DIR < 0);
+    ++t;
+  }
+  return t;
+}
+
 // Direct-load consumer (few draws per launch: create/reset/classify, and the host checks).
 struct Rng {
   uint32_t* mt;    // this env's MT_WORDS words
@@ -224,6 +239,8 @@ struct Rng {
   TG_HD void reserve(uint32_t) {}
   TG_HD bool has(uint32_t) const { return true; }
   TG_HD bool overrun() const { return false; }
+  template <int DIR>
+  TG_HD int walk(int& x, int lim, int cap) { return walk_ticks<DIR>(*this, x, lim, cap); }
   // the state word to store: position, and whether the other half is stale
   TG_HD uint32_t finish() const { return pos | (crossed ? MT_STALE : 0u); }
   // the same when a refill of the half that was stale on entry is already queued
@@ -725,6 +742,73 @@ TG_HD uint32_t available_mask(const Level& L, const Map& m, const Env& e) {  // 
   return r;
 }
 
+// ---- length classes: how long an option that can run will take, predicted at can_run time -----
+// The compacted step (tg_amd.hip k_classify / k_run) lists the envs of each (option, class) apart
+// and runs a wave's 64 envs together, so that a wave runs to its longest lane's length with its
+// lanes of similar lengths.  Classes never change a result, only which envs share a wave; class
+// 0 is the longest of its option (the run order goes longest first).
+//   go_left / go_right (MO/:69-85): the walk to the target column's centre, |T - px| px at 2-4 px
+//     per tick: 16 classes of 32 px;
+//   up_ladder / down_ladder (MO/:160-189): the ladder cells above / below the player in its
+//     column (the climb ends where the ladder predicates fail): 8 classes of 32 px;
+//   down_left / down_right (MO/:211-244): the open cells below the next column (the fall): 4;
+//   jump_left / jump_right (MO/:269-314): the landing 1 or 2 columns away: 2;
+//   interact: 1 tick.
+TG_HD constexpr int nclass(int k) {
+  return k == O_GO_LEFT || k == O_GO_RIGHT ? 16 : k == O_UP_LADDER || k == O_DOWN_LADDER ? 8
+       : k == O_INTERACT ? 1 : k == O_DOWN_LEFT || k == O_DOWN_RIGHT ? 4 : 2;
+}
+TG_HD int length_class(const Level& L, const Map& m, const Env& e, int k) {
+  int xc, yc;
+  player_cell(e, xc, yc);
+  const uint32_t dc = Map::dc_of(e.f);
+  int d = 0;  // predicted length, larger = longer
+  switch (k) {
+    case O_GO_LEFT:
+    case O_GO_RIGHT: {
+      const int dir = k == O_GO_LEFT ? -1 : 1;
+      int tx = xc + dir;
+      uint32_t gt;
+      if (go_lookup(L, e, xc, yc, gt)) tx = (int)((gt >> (dir < 0 ? 8 : 16)) & 0xFFu) - 1;
+      else go_target(L, m, e, dir, xc, yc, tx);
+      const int D = tx * S + S / 2 - e.px;
+      d = (D < 0 ? -D : D) >> 5;
+      break;
+    }
+    case O_UP_LADDER: {  // ladder cells from the row of the player's feet up
+      int y = m.rowy(e.py + S - INCR);
+      while (y >= 0 && Map::is_ladder(m.cellb(xc, y))) --y;
+      d = (e.py - (y + 1) * S + S) >> 5;
+      break;
+    }
+    case O_DOWN_LADDER: {
+      int y = m.rowy(e.py);
+      while (y < L.H && Map::is_ladder(m.cellb(xc, y))) ++y;
+      d = (y * S - e.py) >> 5;
+      break;
+    }
+    case O_DOWN_LEFT:
+    case O_DOWN_RIGHT: {
+      const int cx = xc + (k == O_DOWN_LEFT ? -1 : 1);
+      int y = yc + 1;
+      while (y < L.H && m.open_cell(dc, cx, y)) ++y;
+      d = y - yc - 1;
+      break;
+    }
+    case O_JUMP_LEFT:
+    case O_JUMP_RIGHT: {
+      const int dir = k == O_JUMP_LEFT ? -1 : 1;
+      d = landing(m, e, xc + dir, yc - 1) ? 0 : 1;
+      break;
+    }
+    default:
+      return 0;
+  }
+  const int n = nclass(k);
+  d = d < 0 ? 0 : (d >= n ? n - 1 : d);
+  return n - 1 - d;
+}
+
 // option-local state (start_cell / target_cell are None between steps, MO/:80-83 etc.)
 struct Opt {
   int tx;      // target cell x
@@ -1130,28 +1214,22 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
     // it leaves it (the loop body is just the plain tick).  Full phase: then no lane of the wave is in a span, and each takes one full
     // tick, which may open a new span.  Each lane's own tick sequence is the reference's; only
     // the interleaving across lanes differs, and the full tick's code runs once per round.
-    bool capped = false;
     do {
       // a lane leaves when its span ends; the wave when all have (a per-lane loop: a
       // ballot-driven one, with the idle lanes kept inside, made the compiler copy ~26
       // loop-carried registers per iteration and was slower)
       // (the plain phase also ends when the staged draws run low: the full tick restocks them
       // in rng.reserve, so the plain loop's body holds no refill code)
-      while ((DIR > 0 ? e.px <= lim : e.px >= lim) && rng.has(TICK_DRAWS)) {  // a plain tick
-#if defined(__HIP_DEVICE_COMPILE__) && defined(TG_DIAG_MARK)
-        asm volatile("; PLAIN_TICK_BEGIN");
-#endif
-        e.px += code_step(rng.code(), DIR < 0);
+      if (const int t = rng.template walk<DIR>(e.px, lim, TICK_CAP - r.ticks)) {  // plain ticks
         e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
-        r.reward += -1;
+        r.reward -= t;
+        r.ticks += t;
         if (DIR > 0 ? e.px > lim : e.px < lim) pickups(L, e);  // left the span: as the full tick
-        if (++r.ticks >= TICK_CAP) {
+        if (r.ticks >= TICK_CAP) {
           e.f |= E_TICKCAP;
-          capped = true;
-          lim = DIR > 0 ? -0x40000000 : 0x40000000;  // out of the plain phase
+          break;
         }
       }
-      if (capped) break;
       rng.reserve(TICK_DRAWS);
       const int prim = policy<K>(L, m, e, o);
       r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
@@ -1166,20 +1244,17 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
   if constexpr (K == O_UP_LADDER || K == O_DOWN_LADDER) {
     constexpr int DIR = K == O_UP_LADDER ? -1 : 1;
     int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
-    bool capped = false;
     do {
       // plain phase (ladder_plain_limit), then one full tick: as the go loops
-      while ((DIR > 0 ? e.py <= lim : e.py >= lim) && rng.has(TICK_DRAWS)) {
-        e.py += code_step(rng.code(), DIR < 0);
-        r.reward += -1;
+      if (const int t = rng.template walk<DIR>(e.py, lim, TICK_CAP - r.ticks)) {  // plain ticks
+        r.reward -= t;
+        r.ticks += t;
         if (DIR > 0 ? e.py > lim : e.py < lim) pickups(L, e);  // left the span: as the full tick
-        if (++r.ticks >= TICK_CAP) {
+        if (r.ticks >= TICK_CAP) {
           e.f |= E_TICKCAP;
-          capped = true;
-          lim = DIR > 0 ? -0x40000000 : 0x40000000;
+          break;
         }
       }
-      if (capped) break;
       rng.reserve(TICK_DRAWS);
       const int prim = policy<K>(L, m, e, o);
       r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);

@@ -497,16 +497,31 @@ class TreasureGame:
         g = st[2]
         self._py.has_gauss = g is not None
         self._py.gauss_next = 0.0 if g is None else g
+        return st
 
     def _store_global(self):
         random.setstate((3, self._WORDS.unpack_from(self._py, 0),
                          self._py.gauss_next if self._py.has_gauss else None))
 
     def _reset_py(self, obs):
-        self._load_global()
+        st = self._load_global()
         check(self._vec._L.tg_reset1_py(self._vec.handle, ctypes.byref(self._py),
                                         obs.ctypes.data, self._vec._stream()), "tg_reset1_py")
-        self._store_global()
+        # The reset's draws (IM/:55-73): two uniform(), then gauss twice.  Their stream position
+        # is the device's; gauss_next, the cached half of a gauss pair, is left in the global
+        # state where user code can read it, so it must be CPython's own sin(x2pi) * g2rad
+        # (glibc), not the device's (OCML; they may differ in the last ulp): the same calls are
+        # replayed on a private Random from the state the reset started from.
+        r = random.Random()
+        r.setstate(st)
+        r.random()
+        r.random()
+        r.gauss(0.0, 1.0)
+        r.gauss(0.0, 1.0)
+        out = r.getstate()
+        if out[1] != self._WORDS.unpack_from(self._py, 0):
+            raise TgError("tg_reset1_py: the device's stream position differs from CPython's")
+        random.setstate(out)
 
     def reset(self):
         if self._shared:
