@@ -109,6 +109,8 @@ def load():
         "tg_version": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("TG_AB_LIB") and not hasattr(L, name):
+            continue  # scripts/ab.py times earlier builds, which may lack newer entry points
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

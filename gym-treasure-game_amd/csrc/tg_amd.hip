@@ -356,15 +356,15 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  // the generation's 312 draw codes, 4 per lane (one 4-B store each)
+  // the generation's 312 draw codes, draw d = r * 64 + lane per round: its two words are one
+  // 8-B LDS read at an 8-B lane stride (conflict-free; four draws per lane at a 32-B stride
+  // were 2-way conflicts), its code one byte of a coalesced 64-B store
 #pragma unroll
-  for (int r = 0; r < (MT_N / 8 + 63) / 64; ++r) {
-    const int k = r * 64 + lane;
-    if (k < MT_N / 8) {
-      const lds_u32* w = scratch + 8 * k;
-      const uint32_t v = draw_code(mt_double(w[0], w[1])) | draw_code(mt_double(w[2], w[3])) << 8 |
-                         draw_code(mt_double(w[4], w[5])) << 16 | draw_code(mt_double(w[6], w[7])) << 24;
-      reinterpret_cast<uint32_t*>(dst_c)[k] = v;
+  for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
+    const int d = r * 64 + lane;
+    if (d < MT_N / 2) {
+      const uint2 w = *reinterpret_cast<const __attribute__((address_space(3))) uint2*>(scratch + 2 * d);
+      dst_c[d] = (uint8_t)draw_code(mt_double(w.x, w.y));
     }
   }
 }

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""A/B timing of step libraries on one GPU (diagnostics; not the bench).
+
+    VARIANTS="base=gym-treasure-game_amd/libtg_amd_r02.so,new=gym-treasure-game_amd/libtg_amd.so" \\
+    POLICIES=uniform,masked BURN=3000 STEPS=50 ROUNDS=3 python scripts/ab.py
+
+Each variant is a prebuilt libtg_amd.so (an earlier commit's build, or the product's sources
+with -D flags); per policy and round, every variant runs the bench's workload (1,048,576 envs,
+seed 0, auto-reset, the bench's action stream) from construction through BURN untimed steps,
+then STEPS steps timed with HIP events (tg_step's kernels) and the wall clock.  Variants are
+interleaved and the best round is reported, so that box-to-box spread cancels."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["TG_AB_LIB"] = "1"
+import gym_treasure_game_amd as tg  # noqa: E402
+from gym_treasure_game_amd import _lib  # noqa: E402
+
+ACTION_SEED = 0x5EED0001
+
+
+def time_one(path, policy, n, burn, steps):
+    _lib._lib = None
+    _lib.LIB_PATH = path
+    vec = tg.TreasureGameVec(n, seed=0, autoreset=True)
+    vec.reset()
+    rec = torch.empty((1 << 16, 2), dtype=torch.int64, device=vec.device)
+    cnt = torch.zeros(1, dtype=torch.int32, device=vec.device)
+    for t in range(burn):
+        vec.step(vec.policy_actions(t, ACTION_SEED, policy))
+        if t % 10 == 9:
+            vec.drain_episodes(rec, cnt)
+    acts = None
+    if policy == "uniform":  # inputs resident before timing, as the bench
+        acts = [vec.policy_actions(burn + j, ACTION_SEED, policy).clone() for j in range(steps)]
+    torch.cuda.synchronize()
+    vec.stats_reset()
+    vec.set_timing(True)
+    t0 = time.perf_counter()
+    for j in range(steps):
+        vec.step(acts[j] if acts is not None else vec.policy_actions(burn + j, ACTION_SEED, policy))
+        if j % 10 == 9:
+            vec.drain_episodes(rec, cnt)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = vec.stats()
+    vec.close()
+    return {"ms_step": dt / steps * 1e3, "kernel_ms": st["kernel_ms"] / steps,
+            "lane_eff": st["ticks"] / max(64 * st["wave_ticks"], 1)}
+
+
+def main():
+    variants = [v.split("=", 1) for v in os.environ["VARIANTS"].split(",")]
+    policies = os.environ.get("POLICIES", "uniform,masked").split(",")
+    n = int(os.environ.get("N", 1 << 20))
+    steps = int(os.environ.get("STEPS", 50))
+    rounds = int(os.environ.get("ROUNDS", 3))
+    out = {}
+    for pol in policies:
+        burn = int(os.environ.get("BURN", 3000 if pol == "uniform" else 1500))
+        for r in range(rounds):
+            for name, path in variants:
+                res = time_one(os.path.join(ROOT, path), pol, n, burn, steps)
+                key = "%s/%s" % (pol, name)
+                print(key, "round", r, json.dumps(res), flush=True)
+                best = out.get(key)
+                if best is None or res["kernel_ms"] < best["kernel_ms"]:
+                    out[key] = res
+    print(json.dumps({"best": out, "n": n, "steps": steps}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
