@@ -132,22 +132,32 @@ def parse(argv=None):
 
 # ---- CPU legs (the oracle is loaded here only: bench's cpu_baseline leg) ------------------
 def dropin_latency(tg, steps=300, seed=0):
-    """The N=1 drop-in's own hot call: TreasureGame.step(a) (TG/:91-96) from Python, one env
-    on the GPU (tg_step1: one launch, the row written into pinned host memory, one sync),
-    uniform random actions from a host RNG, resetting when done.  Mean µs per call."""
+    """The N=1 drop-in's own hot call: TreasureGame.step(a) (TG/:91-96) from Python, one env on
+    the GPU, uniform random actions from a host RNG, resetting when done; mean µs per call.
+    Both construction modes: TreasureGame() draws from Python's global random as the reference
+    does (tg_step1_py: the stream state goes in and out with the launch), TreasureGame(seed=s)
+    from the env's own stream (tg_step1); each is one launch and one synchronisation."""
     import random
-    env = tg.TreasureGame(seed=seed)
-    env.reset()
-    r = random.Random(seed)
-    for _ in range(20):
-        env.step(r.randrange(9))
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        if env.step(r.randrange(9))[2]:
+    out = {"steps": steps, "api": "TreasureGame.step, host RNG actions, synchronous"}
+    saved = random.getstate()
+    try:
+        for mode in ("shared_global_random", "private_stream"):
+            random.seed(seed)
+            env = tg.TreasureGame() if mode == "shared_global_random" else tg.TreasureGame(seed=seed)
             env.reset()
-    dt = time.perf_counter() - t0
-    return {"step_us": dt / steps * 1e6, "steps": steps,
-            "api": "TreasureGame.step (tg_step1), host RNG actions, synchronous"}
+            r = random.Random(seed)
+            for _ in range(20):
+                env.step(r.randrange(9))
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                if env.step(r.randrange(9))[2]:
+                    env.reset()
+            out[mode + "_step_us"] = (time.perf_counter() - t0) / steps * 1e6
+            env.close()
+    finally:
+        random.setstate(saved)
+    out["step_us"] = out["shared_global_random_step_us"]  # the default TreasureGame()
+    return out
 
 
 def cpu_baseline(seconds, policy, parity_envs=0):

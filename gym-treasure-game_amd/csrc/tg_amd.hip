@@ -279,6 +279,21 @@ struct RngCodes {
     nxc = read();  // code() reads one draw ahead
     return taken;
   }
+#ifdef TG_DIAG_STAMPS
+  // DIAGNOSTIC BUILD ONLY: s_memtime per phase of the option loops (tg_core.h run_option_k):
+  // ph[k] sums the time of the segments ending at stamp k (1 plain walk, 2 window refill,
+  // 3 full tick); rounds counts stamp 0
+  unsigned long long ph[4] = {0, 0, 0, 0}, last = 0;
+  uint32_t rounds = 0;
+  __device__ __forceinline__ void phase(int k) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    if (last) ph[k] += now - last;
+    last = now;
+    rounds += k == 0;
+  }
+#else
+  __device__ __forceinline__ void phase(int) {}
+#endif
   // a draw was taken past the staged window (reserve's bound broken: flagged E_WINDOW)
   __device__ __forceinline__ bool overrun() const { return left > (uint32_t)WIN_CHUNKS * 16u; }
   // one draw, consumed for its outcomes (draw_code); reserve() guarantees it is in the window
@@ -363,8 +378,8 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
   for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
     const int d = r * 64 + lane;
     if (d < MT_N / 2) {
-      const uint2 w = *reinterpret_cast<const __attribute__((address_space(3))) uint2*>(scratch + 2 * d);
-      dst_c[d] = (uint8_t)draw_code(mt_double(w.x, w.y));
+      const lds_u32* w = scratch + 2 * d;
+      dst_c[d] = (uint8_t)draw_code(mt_double(w[0], w[1]));
     }
   }
 }
@@ -882,7 +897,10 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
 
 #ifdef TG_DIAG_STAMPS
 // DIAGNOSTIC BUILD ONLY (scripts/diag_stamps.py): per-wave s_memtime stamps of k_run
-__device__ unsigned long long g_stamps[(1 << 16) * 6];  // per wave: 4 durations/counts + 100 MHz start, end
+constexpr int NSTAMP = 10;
+// per wave: 4 durations/counts, 100 MHz start and end, the option loop's phases (walk, refill,
+// full tick: lane 0's sums) and rounds
+__device__ unsigned long long g_stamps[(1 << 16) * NSTAMP];
 #define TG_STAMP(v) v = __builtin_amdgcn_s_memtime()
 #else
 #define TG_STAMP(v) (void)0
@@ -966,6 +984,10 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   (void)t0; (void)t1; (void)t2; (void)t3;
+#ifdef TG_DIAG_STAMPS
+  unsigned long long ph1 = 0, ph2 = 0, ph3 = 0;
+  uint32_t prounds = 0;
+#endif
   if (live) {
     const int64_t at = (int64_t)seg * w.shard_cap + idx;
     i = w.lists[at];
@@ -977,6 +999,9 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
     run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform: one specialised loop
     TG_STAMP(t2);
+#ifdef TG_DIAG_STAMPS
+    ph1 = rng.ph[1], ph2 = rng.ph[2], ph3 = rng.ph[3], prounds = rng.rounds;
+#endif
     r.done = is_done(e);
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
     e.mti = rng.finish_queued();  // MT_STALE if a half was left: the next step refills it
@@ -1051,14 +1076,21 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     const unsigned long long a2 = __shfl(t2, src, 64);
     const int wv = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
     const unsigned long long rt3 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long p1 = __shfl(ph1, src, 64), p2 = __shfl(ph2, src, 64),
+                             p3 = __shfl(ph3, src, 64);
+    const uint32_t pr = __shfl(prounds, src, 64);
     if ((threadIdx.x & 63) == 0 && bl && wv < (1 << 16)) {
-      g_stamps[wv * 6 + 0] = a1 - t0;
-      g_stamps[wv * 6 + 1] = a2 - a1;
-      g_stamps[wv * 6 + 2] = t3 - a2;
-      g_stamps[wv * 6 + 3] = (unsigned long long)mx | ((unsigned long long)sum << 32) |
-                             ((unsigned long long)k << 56);
-      g_stamps[wv * 6 + 4] = rt0;
-      g_stamps[wv * 6 + 5] = rt3;
+      unsigned long long* const g = g_stamps + (size_t)wv * NSTAMP;
+      g[0] = a1 - t0;
+      g[1] = a2 - a1;
+      g[2] = t3 - a2;
+      g[3] = (unsigned long long)mx | ((unsigned long long)sum << 32) | ((unsigned long long)k << 56);
+      g[4] = rt0;
+      g[5] = rt3;
+      g[6] = p1;
+      g[7] = p2;
+      g[8] = p3;
+      g[9] = pr;
     }
   }
 #endif
@@ -1655,6 +1687,7 @@ struct PyRng {
   __device__ __forceinline__ void reserve(uint32_t) {}
   __device__ __forceinline__ bool has(uint32_t) const { return true; }
   __device__ __forceinline__ bool overrun() const { return false; }
+  __device__ __forceinline__ void phase(int) {}
   template <int DIR>
   __device__ __forceinline__ int walk(int& x, int lim, int cap) { return walk_ticks<DIR>(*this, x, lim, cap); }
 };
@@ -2364,7 +2397,7 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
 int tg_diag_stamps(unsigned long long* out, int n_waves) {
   if (n_waves > (1 << 16)) n_waves = 1 << 16;
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 6 * n_waves));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * NSTAMP * n_waves));
   return TG_OK;
 }
 #endif

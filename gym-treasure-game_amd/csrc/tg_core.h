@@ -239,6 +239,7 @@ struct Rng {
   TG_HD void reserve(uint32_t) {}
   TG_HD bool has(uint32_t) const { return true; }
   TG_HD bool overrun() const { return false; }
+  TG_HD void phase(int) {}  // per-phase timing hook of the diagnostic build (tg_amd.hip RngCodes)
   template <int DIR>
   TG_HD int walk(int& x, int lim, int cap) { return walk_ticks<DIR>(*this, x, lim, cap); }
   // the state word to store: position, and whether the other half is stale
@@ -1220,6 +1221,7 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
       // loop-carried registers per iteration and was slower)
       // (the plain phase also ends when the staged draws run low: the full tick restocks them
       // in rng.reserve, so the plain loop's body holds no refill code)
+      rng.phase(0);
       if (const int t = rng.template walk<DIR>(e.px, lim, TICK_CAP - r.ticks)) {  // plain ticks
         e.f = DIR > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
         r.reward -= t;
@@ -1230,10 +1232,13 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
           break;
         }
       }
+      rng.phase(1);
       rng.reserve(TICK_DRAWS);
+      rng.phase(2);
       const int prim = policy<K>(L, m, e, o);
       r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
       if (!o.done) lim = go_plain_limit<DIR>(m, e, o.tx);
+      rng.phase(3);
       if (++r.ticks >= TICK_CAP) {
         e.f |= E_TICKCAP;
         break;
@@ -1248,6 +1253,7 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
       // plain phase (ladder_plain_limit), then one full tick: as the go loops
       // per tick (a batched walk here, RngCodes::walk, took k_run from 82 to 98 VGPRs: 4
       // instead of 5 waves per SIMD)
+      rng.phase(0);
       bool capped = false;
       while ((DIR > 0 ? e.py <= lim : e.py >= lim) && rng.has(TICK_DRAWS)) {
         e.py += code_step(rng.code(), DIR < 0);
@@ -1260,10 +1266,13 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
         }
       }
       if (capped) break;
+      rng.phase(1);
       rng.reserve(TICK_DRAWS);
+      rng.phase(2);
       const int prim = policy<K>(L, m, e, o);
       r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
       if (!o.done) lim = ladder_plain_limit<DIR>(m, e);
+      rng.phase(3);
       if (++r.ticks >= TICK_CAP) {
         e.f |= E_TICKCAP;
         break;
@@ -1274,13 +1283,17 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
   if constexpr (K == O_JUMP_LEFT || K == O_JUMP_RIGHT || K == O_DOWN_LEFT || K == O_DOWN_RIGHT) {
     AirCells ac{0u, 0u, -0x40000000, 0, 0, 0u};  // holds nothing: built on the first air tick
     do {
+      rng.phase(0);
+      rng.phase(1);
       rng.reserve(TICK_DRAWS);
+      rng.phase(2);
       if (o.init) {
         r.reward += air_tick<K>(L, m, e, o, rng, ac);
       } else {  // the first tick (the jump itself; the drop's target)
         const int prim = policy<K>(L, m, e, o);
         r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
       }
+      rng.phase(3);
       if (++r.ticks >= TICK_CAP) {
         e.f |= E_TICKCAP;
         break;

@@ -653,7 +653,9 @@ class TreasureGameVectorEnv:
         old = getattr(self, "env", None)
         if old is not None:
             old.close()
-        self.env = TreasureGameVec(self.num_envs, seed=seed, autoreset=True, **self._kw)
+        # copy=True: every returned tensor is the caller's own (gymnasium loops keep obs across
+        # steps: obs_t must not change when the next step writes the library's buffers)
+        self.env = TreasureGameVec(self.num_envs, seed=seed, autoreset=True, copy=True, **self._kw)
         self.device = self.env.device
         self._len = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
 

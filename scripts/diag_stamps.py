@@ -36,7 +36,7 @@ def main():
         vec.step(vec.policy_actions(t, policy=pol))
     torch.cuda.synchronize()
     nw = n // 64
-    buf = np.zeros((nw, 6), np.uint64)
+    buf = np.zeros((nw, 10), np.uint64)
     vec.stats_reset()
     vec.step(vec.policy_actions(999, policy=pol))
     torch.cuda.synchronize()
@@ -75,8 +75,11 @@ def main():
         sel = kk == k
         if sel.any():
             print("  %-11s waves %5d end max %6.1f us p90 %6.1f  iters max %4d mean %5.1f  cyc/iter %6.0f"
+                  "  | loop %7.0f = walk %7.0f + refill %7.0f + full ticks %7.0f, rounds %5.1f"
                   % (names[k], sel.sum(), en_us[sel].max(), np.percentile(en_us[sel], 90),
-                     mx[sel].max(), mx[sel].mean(), (b[sel, 1] / np.maximum(mx[sel], 1)).mean()))
+                     mx[sel].max(), mx[sel].mean(), (b[sel, 1] / np.maximum(mx[sel], 1)).mean(),
+                     b[sel, 1].mean(), b[sel, 6].mean(), b[sel, 7].mean(), b[sel, 8].mean(),
+                     b[sel, 9].mean()))
     top = np.argsort(-en_us)[:10]
     for j in top:
         print("  last: start %.1f end %.1f us iters %d loop cyc/iter %.0f" % (

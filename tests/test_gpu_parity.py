@@ -571,6 +571,24 @@ def test_vector_env_gymnasium_surface(tg, oracle):
     ve.close()
 
 
+def test_vector_env_outputs_are_not_overwritten(tg):
+    """A gymnasium loop keeps obs_t while it steps to obs_t+1: the vector env's outputs (obs,
+    info['final_obs'], info['valid'], reward, flags) are the caller's own tensors, not the
+    library's buffers that the next step rewrites."""
+    ve = tg.make_vec("treasure_game-v0", num_envs=256, seed=3)
+    obs0, _ = ve.reset()
+    keep0 = obs0.clone()
+    obs1, r1, te1, tr1, info1 = ve.step(ve.env.policy_actions(0, policy="masked").clone())
+    keep1 = [x.clone() for x in (obs1, r1, info1["final_obs"], info1["valid"])]
+    for t in range(1, 6):
+        ve.step(ve.env.policy_actions(t, policy="masked").clone())
+    assert torch.equal(obs0, keep0)
+    for x, k in zip((obs1, r1, info1["final_obs"], info1["valid"]), keep1):
+        assert torch.equal(x, k)
+    assert not torch.equal(obs0, obs1)  # the step moved something
+    ve.close()
+
+
 @pytest.mark.parametrize("make", ["default", "make", "explicit"])
 def test_dropin_shares_the_global_random_stream(tg, make):
     """TreasureGame() -- the default, as gym.make('treasure_game-v0') builds it -- draws from
