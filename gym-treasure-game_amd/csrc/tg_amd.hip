@@ -707,40 +707,34 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
 // ---- two-pass compacted step (TG_MODE_COMPACT) -------------------------------------------
 // Pass 1, k_classify: one lane per env (coalesced).  Evaluates option_list[a].can_run();
 // envs whose option cannot run finish here (reward None, obs/done rows written, state
-// unchanged); the rest are appended to per-(option, length class) worklists (buckets;
-// tg_core.h length_class).  Appends are aggregated per workgroup in LDS and the counters are
-// sharded 8 ways (blockIdx % 8) across cache lines (one word alone saturates at ~88 atomics/us,
-// MI355X_MICROARCH.md "dequeue").
-// Pass 2, k_run: wave w runs chunk w (64 envs) of the worklists concatenated in run order:
-// options in kOrder, each option's classes longest first, each class's 8 shards.  Only the
-// options are padded to whole chunks, so every wave holds ONE option (wave-uniform k selects a
-// loop specialised to that option's primitive actions) and lanes of neighbouring classes.
+// unchanged); the rest are appended to per-option worklists.  Appends are aggregated per
+// workgroup in LDS and the counters are sharded 8 ways (blockIdx % 8) across cache lines (one
+// word alone saturates at ~88 atomics/us, MI355X_MICROARCH.md "dequeue").
+// Pass 2, k_run: wave w runs chunk w (64 envs) of the worklists concatenated in run order
+// (options in kOrder, each option's 8 shards).  Only the options are padded to whole chunks
+// (round 2 padded every shard), so every wave holds ONE option: a wave-uniform k selects a loop
+// specialised to that option's primitive actions.  (Round 3 also tried worklists per (option,
+// predicted length class), which raised lane efficiency from 0.53 to 0.84 but ran 2-5 % slower:
+// DESIGN.md §3.1.)
 constexpr int SHARDS = 8;
 constexpr int kOrderH[O_COUNT] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
                                   O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
                                   O_INTERACT};
-struct Buckets {
-  int base[O_COUNT];  // first bucket of option k
-  int count;
+struct RunPos {
+  int of[O_COUNT];  // run position of option k (kOrder's inverse)
 };
-constexpr Buckets make_buckets() {
-  Buckets b{};
-  int acc = 0;
-  for (int j = 0; j < O_COUNT; ++j) {
-    b.base[kOrderH[j]] = acc;
-    acc += nclass(kOrderH[j]);
-  }
-  b.count = acc;
-  return b;
+constexpr RunPos make_runpos() {
+  RunPos r{};
+  for (int j = 0; j < O_COUNT; ++j) r.of[kOrderH[j]] = j;
+  return r;
 }
-constexpr Buckets kBuckets = make_buckets();
-constexpr int NBUCKET = kBuckets.count;  // 61
-constexpr int NSEG = NBUCKET * SHARDS;    // segment = bucket * SHARDS + shard, in run order
+constexpr RunPos kRunPos = make_runpos();
+constexpr int NSEG = O_COUNT * SHARDS;  // segment = run position * SHARDS + shard
 static_assert(NSEG <= 2 * BLOCK, "k_run's prefix: two segments per thread");
 constexpr int NCTR = NSEG + 8;  // the worklist counters, then k_run's refill queues (one per XCD)
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
 struct Work {
-  int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = bucket * SHARDS + shard
+  int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = run position * SHARDS + shard
   // the listed envs' state, in worklist order (written by k_classify, which has loaded it
   // anyway): k_run reads its chunk's 64 records coalesced, in one round trip with the list
   // entries, instead of a dependent gather of 16 + 16 + 8 scattered bytes per lane
@@ -763,9 +757,11 @@ constexpr int REFILL_GRAB = 2;     // refill regions a wave takes from its XCD's
 __constant__ int kOrder[O_COUNT] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
                                     O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
                                     O_INTERACT};
-__constant__ int kBucketBase[O_COUNT] = {kBuckets.base[0], kBuckets.base[1], kBuckets.base[2],
-                                         kBuckets.base[3], kBuckets.base[4], kBuckets.base[5],
-                                         kBuckets.base[6], kBuckets.base[7], kBuckets.base[8]};
+__constant__ int kSegBase[O_COUNT] = {kRunPos.of[0] * SHARDS, kRunPos.of[1] * SHARDS,
+                                      kRunPos.of[2] * SHARDS, kRunPos.of[3] * SHARDS,
+                                      kRunPos.of[4] * SHARDS, kRunPos.of[5] * SHARDS,
+                                      kRunPos.of[6] * SHARDS, kRunPos.of[7] * SHARDS,
+                                      kRunPos.of[8] * SHARDS};
 
 template <bool AUTORESET, bool FINAL, int POL = -1>
 __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
@@ -773,7 +769,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      StepIO io, EpQueue q, Work w, int64_t g0,
                                                      unsigned long long* __restrict__ stats,
                                                      uint32_t* __restrict__ err_or) {
-  __shared__ int bcnt[NBUCKET], bbase[NBUCKET];
+  __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
   // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
   // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
   // keeps 8 waves per SIMD
@@ -799,7 +795,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     a2 = S.ang[i];
     ep = S.ep[i];
   }
-  if (threadIdx.x < NBUCKET) bcnt[threadIdx.x] = 0;
+  if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
   if (blockIdx.x == 0)
     for (int c = threadIdx.x; c < NCTR; c += BLOCK) w.ctr_next[c * CTR_STRIDE] = 0;
   stage_level(lv, grid, L);  // includes the barrier
@@ -817,8 +813,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     k = option_index(act);
     runs = k >= 0 && can_run(L, m, e, k);
   }
-  const int bk = runs ? kBucketBase[k] + length_class(L, m, e, k) : -1;  // the env's bucket
-  // halves left in the previous step (MT_STALE) go on the refill list; k_run's idle waves
+  const int bk = runs ? k : -1;  // the env's worklist  // halves left in the previous step (MT_STALE) go on the refill list; k_run's idle waves
   // regenerate them beside the option loops (a lane that needs one first does it itself)
   {
     const bool stale = live && (e.mti & MT_STALE);
@@ -829,8 +824,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
           (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
     if (lane == 0) w.nrefill[wv] = (uint8_t)__popcll(b);
   }
-  // workgroup-local slots: one LDS atomic per wave and bucket present in the wave (the
-  // wave's lanes are matched bucket by bucket)
+  // workgroup-local slots: one LDS atomic per wave and option present in the wave (the
+  // wave's lanes are matched option by option)
   int slot = 0;
   {
     unsigned long long pend = __ballot(runs);
@@ -850,9 +845,9 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   // reward-None envs are finished (their latency overlaps that work)
   const int shard = blockIdx.x % SHARDS;
   int my_base = 0;
-  if (threadIdx.x < NBUCKET) {
+  if (threadIdx.x < O_COUNT) {
     const int c = bcnt[threadIdx.x];
-    my_base = c ? atomicAdd(&w.ctr[(threadIdx.x * SHARDS + shard) * CTR_STRIDE], c) : 0;
+    my_base = c ? atomicAdd(&w.ctr[(kSegBase[threadIdx.x] + shard) * CTR_STRIDE], c) : 0;
   }
   uint4 s4w = s4;  // the state the worklist copy carries
 
@@ -882,10 +877,10 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     }
     S.ep[i] = ep;
   }
-  if (threadIdx.x < NBUCKET) bbase[threadIdx.x] = my_base;
+  if (threadIdx.x < O_COUNT) bbase[threadIdx.x] = my_base;
   __syncthreads();
   if (runs) {
-    const int64_t at = (int64_t)(bk * SHARDS + shard) * w.shard_cap + bbase[bk] + slot;
+    const int64_t at = (int64_t)(kSegBase[k] + shard) * w.shard_cap + bbase[k] + slot;
     w.lists[at] = (int32_t)i;
     w.wst4[at] = s4w;
     w.wang[at] = a2;
@@ -940,8 +935,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   if (threadIdx.x == 0) {
     int acc = 0;
     for (int j = 0; j < O_COUNT; ++j) {
-      const int kj = kOrder[j];
-      const int sb = kBucketBase[kj] * SHARDS, se = (kBucketBase[kj] + nclass(kj)) * SHARDS;
+      const int sb = j * SHARDS, se = sb + SHARDS;
       ostart[j] = acc;
       oraw[j] = pre[sb];
       acc += (pre[se] - pre[sb] + 63) & ~63;
@@ -960,9 +954,9 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   // this lane's place in option k's lists (the raw prefix's coordinates), and its segment
   const int qraw = oraw[oj] + base + (threadIdx.x & 63) - ostart[oj];
   const bool live = base < total && qraw < oraw[oj + 1];
-  int seg = kBucketBase[k] * SHARDS;
+  int seg = oj * SHARDS;
   if (live) {
-    int hi = (kBucketBase[k] + nclass(k)) * SHARDS;  // pre[seg] <= qraw < pre[hi]
+    int hi = seg + SHARDS;  // pre[seg] <= qraw < pre[hi]
     while (hi - seg > 1) {
       const int mid = (seg + hi) >> 1;
       if (pre[mid] <= qraw) seg = mid; else hi = mid;
@@ -1076,9 +1070,16 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     const unsigned long long a2 = __shfl(t2, src, 64);
     const int wv = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
     const unsigned long long rt3 = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long p1 = __shfl(ph1, src, 64), p2 = __shfl(ph2, src, 64),
-                             p3 = __shfl(ph3, src, 64);
-    const uint32_t pr = __shfl(prounds, src, 64);
+    // the phases of the lane whose option loop ran longest (the wave's own time)
+    int lmax = src;
+    unsigned long long best = 0;
+    for (int l = 0; l < 64; ++l) {
+      const unsigned long long tl = __shfl(ph1 + ph2 + ph3, l, 64);
+      if (((bl >> l) & 1ull) && tl > best) best = tl, lmax = l;
+    }
+    const unsigned long long p1 = __shfl(ph1, lmax, 64), p2 = __shfl(ph2, lmax, 64),
+                             p3 = __shfl(ph3, lmax, 64);
+    const uint32_t pr = __shfl(prounds, lmax, 64);
     if ((threadIdx.x & 63) == 0 && bl && wv < (1 << 16)) {
       unsigned long long* const g = g_stamps + (size_t)wv * NSTAMP;
       g[0] = a1 - t0;
@@ -1777,7 +1778,9 @@ __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4,
 namespace {
 int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 // k_run needs one wave per 64-lane chunk of the worklists, each option padded to whole chunks:
-// at most n/64 + O_COUNT chunks
+// at most n/64 + O_COUNT chunks (idle blocks interleaved among the option blocks, so that MT
+// regenerations start at once, measured no faster for the masked policy and slower for the
+// uniform one: DESIGN.md §3.3)
 int run_grid_for(int64_t n) { return grid_for(n) + (O_COUNT * 64 + BLOCK - 1) / BLOCK + REFILL_BLOCKS; }
 // per-block launch-counter slots cover the largest step grid
 // one counter slot per workgroup of the widest step launch: k_run, or k_rollout (>= 64 envs

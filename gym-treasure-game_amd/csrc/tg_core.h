@@ -743,73 +743,6 @@ TG_HD uint32_t available_mask(const Level& L, const Map& m, const Env& e) {  // 
   return r;
 }
 
-// ---- length classes: how long an option that can run will take, predicted at can_run time -----
-// The compacted step (tg_amd.hip k_classify / k_run) lists the envs of each (option, class) apart
-// and runs a wave's 64 envs together, so that a wave runs to its longest lane's length with its
-// lanes of similar lengths.  Classes never change a result, only which envs share a wave; class
-// 0 is the longest of its option (the run order goes longest first).
-//   go_left / go_right (MO/:69-85): the walk to the target column's centre, |T - px| px at 2-4 px
-//     per tick: 16 classes of 32 px;
-//   up_ladder / down_ladder (MO/:160-189): the ladder cells above / below the player in its
-//     column (the climb ends where the ladder predicates fail): 8 classes of 32 px;
-//   down_left / down_right (MO/:211-244): the open cells below the next column (the fall): 4;
-//   jump_left / jump_right (MO/:269-314): the landing 1 or 2 columns away: 2;
-//   interact: 1 tick.
-TG_HD constexpr int nclass(int k) {
-  return k == O_GO_LEFT || k == O_GO_RIGHT ? 16 : k == O_UP_LADDER || k == O_DOWN_LADDER ? 8
-       : k == O_INTERACT ? 1 : k == O_DOWN_LEFT || k == O_DOWN_RIGHT ? 4 : 2;
-}
-TG_HD int length_class(const Level& L, const Map& m, const Env& e, int k) {
-  int xc, yc;
-  player_cell(e, xc, yc);
-  const uint32_t dc = Map::dc_of(e.f);
-  int d = 0;  // predicted length, larger = longer
-  switch (k) {
-    case O_GO_LEFT:
-    case O_GO_RIGHT: {
-      const int dir = k == O_GO_LEFT ? -1 : 1;
-      int tx = xc + dir;
-      uint32_t gt;
-      if (go_lookup(L, e, xc, yc, gt)) tx = (int)((gt >> (dir < 0 ? 8 : 16)) & 0xFFu) - 1;
-      else go_target(L, m, e, dir, xc, yc, tx);
-      const int D = tx * S + S / 2 - e.px;
-      d = (D < 0 ? -D : D) >> 5;
-      break;
-    }
-    case O_UP_LADDER: {  // ladder cells from the row of the player's feet up
-      int y = m.rowy(e.py + S - INCR);
-      while (y >= 0 && Map::is_ladder(m.cellb(xc, y))) --y;
-      d = (e.py - (y + 1) * S + S) >> 5;
-      break;
-    }
-    case O_DOWN_LADDER: {
-      int y = m.rowy(e.py);
-      while (y < L.H && Map::is_ladder(m.cellb(xc, y))) ++y;
-      d = (y * S - e.py) >> 5;
-      break;
-    }
-    case O_DOWN_LEFT:
-    case O_DOWN_RIGHT: {
-      const int cx = xc + (k == O_DOWN_LEFT ? -1 : 1);
-      int y = yc + 1;
-      while (y < L.H && m.open_cell(dc, cx, y)) ++y;
-      d = y - yc - 1;
-      break;
-    }
-    case O_JUMP_LEFT:
-    case O_JUMP_RIGHT: {
-      const int dir = k == O_JUMP_LEFT ? -1 : 1;
-      d = landing(m, e, xc + dir, yc - 1) ? 0 : 1;
-      break;
-    }
-    default:
-      return 0;
-  }
-  const int n = nclass(k);
-  d = d < 0 ? 0 : (d >= n ? n - 1 : d);
-  return n - 1 - d;
-}
-
 // option-local state (start_cell / target_cell are None between steps, MO/:80-83 etc.)
 struct Opt {
   int tx;      // target cell x
