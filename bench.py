@@ -57,13 +57,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ACTION_SEED = 0x5EED0001
 PREGEN_BYTES = 8 << 30  # pre-generated action rows for the timed steps, at most this much HBM
 EP_CAP = 4096          # episode records gathered per rank per step of a drain interval (padded)
-# algorithmic bytes of one tg_step for THIS data layout, per launch:
-#   every env: action 4 + state word 16 read (classify)
-#   reward-None env: angles 16 + episode 8 read; episode 8 + obs 72 + reward/valid/done 6 written
-#   valid env: worklist index 4 + 4, state 16 + 16, angles 16 + 16, episode 8 + 8, obs 72, rows 6
-#   random() draw: its 1-B code (tg_core.h draw_code; the option loops read codes, not doubles)
-#   MT regeneration: 624 words read, 624 words + 312 codes written
-BYTES_ENV, BYTES_INVALID, BYTES_VALID, BYTES_DRAW, BYTES_REGEN = 20, 110, 166, 1, 5304
+# algorithmic bytes of one tg_step for THIS data layout, per kernel:
+#   k_classify, every env: action 4 + state word 16 + angles 16 + episode 8 read (44)
+#     reward-None env: episode 8 + obs 72 + reward/valid/done 6 written (86)
+#     valid env: worklist index 4 + state 16 + angles 16 + episode 8 written (44)
+#     stale MT half: its refill-list entry 4 written
+#   k_run, valid env: the worklist row 44 read; state 16 + angles 16 + episode 8 + obs 72 +
+#     rows 6 written (118); random() draw: its 1-B code (tg_core.h draw_code); MT regeneration:
+#     the refill entry 4 + 624 words read, 624 words + 312 codes written
+#   k_step (direct mode): one kernel, the same without the worklist round trip
+CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 86, 44, 4
+RUN_VALID, RUN_DRAW, RUN_REGEN = 162, 1, 5308
+DIRECT_ENV, DIRECT_INVALID, DIRECT_VALID, DIRECT_REGEN = 44, 86, 118, 5304
+BYTES_DRAW = RUN_DRAW
 # SURVEY.md §8(d)'s layout-independent count per env-step: action 4 + obs 72 + reward 4 +
 # valid 1 + done 1 + state read/write 2 x 40 = 162, plus 24 per random() draw (8 B of MT words
 # read + 16 B amortised twist read/write)
@@ -74,10 +80,18 @@ BYTES_RENDER_STATE = 32
 MT_DRAWS_PER_GEN = 312  # random() values per MT19937 generation
 
 
-def alg_bytes(st):
+def alg_bytes(st, mode="compact"):
+    """algorithmic bytes of the counted steps per kernel: (first, second) = (k_classify, k_run),
+    or (0, k_step) in the direct mode"""
     inval = st["steps"] - st["valid_steps"]
-    return (BYTES_ENV * st["steps"] + BYTES_INVALID * inval + BYTES_VALID * st["valid_steps"] +
-            BYTES_DRAW * st["draws"] + BYTES_REGEN * st["regens"])
+    if mode == "direct":
+        return 0, (DIRECT_ENV * st["steps"] + DIRECT_INVALID * inval +
+                   DIRECT_VALID * st["valid_steps"] + BYTES_DRAW * st["draws"] +
+                   DIRECT_REGEN * st["regens"])
+    cls = (CLS_ENV * st["steps"] + CLS_INVALID * inval + CLS_VALID * st["valid_steps"] +
+           CLS_REGEN * st["regens"])
+    run = RUN_VALID * st["valid_steps"] + RUN_DRAW * st["draws"] + RUN_REGEN * st["regens"]
+    return cls, run
 
 
 def survey_bytes(st):
@@ -116,6 +130,9 @@ def parse(argv=None):
                     help="per-step API: drain and gather the completed episodes every G steps "
                          "(SURVEY §8e: batched gather; 1 = every step); --rollout K drains "
                          "every K steps")
+    ap.add_argument("--timing-every", type=int, default=8,
+                    help="HIP-event timing of every k-th timed step (its kernels' durations for "
+                         "the roofline); an event record between kernels costs the stream ~5 us")
     ap.add_argument("--secondary-steps", type=int, default=30,
                     help="N = 1, c3: steps of the masked-policy line (0 disables it)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -318,7 +335,7 @@ class Runner:
                 raise SystemExit("--rollout K: c3 only, with --steps and --warmup multiples of K")
             self.roll = [torch.empty((self.K, count), dtype=d, device=dev)
                          for d in (torch.int32, torch.uint8, torch.uint8)]
-        self.frames, self.rev, self.timing = None, [], False
+        self.frames, self.rev, self.timing, self.render_on = None, [], False, True
         if args.workload == "c5":  # ObservationWrapper.step: render every env after its step
             vec.render_init(tg.synthetic_sprites(seed=1))
             self.frames = torch.empty((count,) + vec.frame_shape, dtype=torch.uint8, device=dev)
@@ -361,7 +378,7 @@ class Runner:
             chk(L.tg_step(*self.args_step), "tg_step")
         if (t + 1) % self.G == 0 or K:
             self.drain()
-        if self.frames is not None:
+        if self.frames is not None and self.render_on:
             if self.timing:  # k_render alone, on the stream it is launched on
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
@@ -374,9 +391,11 @@ class Runner:
         """warm-up + burn-in (untimed), then EXACTLY ``steps`` timed steps between barriers;
         returns the max-over-ranks wall time and this rank's stats."""
         t = 0
-        for _ in range(warmup + burn_in):
+        for j in range(warmup + burn_in):
+            self.render_on = j < warmup  # c5: the burn-in only advances the envs
             self.step(t)
             t += 1
+        self.render_on = True
         if self.pre is not None:  # the timed steps' inputs, resident before timing
             self.pre_t0 = t
             for j in range(steps):
@@ -388,7 +407,7 @@ class Runner:
         self.log.reset()
         vec = self.vec
         vec.stats_reset()
-        vec.set_timing(True)
+        vec.set_timing(self.args.timing_every)
         self.timing = True
         if self.world > 1:
             dist.barrier()
@@ -402,7 +421,7 @@ class Runner:
             dist.barrier()
         dt = time.perf_counter() - t0
         self.timing = False
-        vec.set_timing(False)
+        vec.set_timing(0)
         st = vec.stats()
         self.drain_all(log=True)  # records of the timed steps still queued (untimed)
         if self.world > 1:
@@ -448,38 +467,62 @@ def load_pmc(path, envs, policy, mode, regens_per_step, burn_in):
 
 
 def step_line(args, runner, dt, st, node, world, total):
-    """the bench line's roofline / counters for the c3 step measurement"""
+    """the bench line's roofline / counters for the c3 step measurement: the dominant kernel
+    (k_run; k_step in the direct mode) over its own HIP-event time, the step's kernels beside"""
     env_steps = total * args.steps
     assert node["steps"] == env_steps, (node, env_steps)
     launches = max(st["launches"], 1)
-    kern_s = st["kernel_ms"] / 1e3 / launches
-    alg = alg_bytes(st) / launches
+    timed = max(st["timed_launches"], 1)
+    step_s = st["kernel_ms"] / 1e3 / timed      # k_classify + k_run of a timed launch
+    run_s = st["run_ms"] / 1e3 / timed          # k_run alone
+    cls_s = step_s - run_s
+    cls_b, run_b = (b / launches for b in alg_bytes(st, args.mode))
     surv = survey_bytes(st) / launches
-    achieved = alg / kern_s / 1e9
     d = node["draws"] / max(node["steps"], 1)
     regens = st["regens"] / launches
     regens_expected = runner.count * d / MT_DRAWS_PER_GEN
     lane_eff = node["ticks"] / max(64 * node["wave_ticks"], 1)
     pmc = load_pmc(args.traffic_json, args.envs, args.policy_used, args.mode, regens,
                    args.burn_in_used)
-    roof = {"bound": "hbm",
-            "kernel": ("tg_step = k_classify + k_run" if args.mode == "compact"
-                       else "tg_step = k_step"),
-            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+    run_name = "k_run" if args.mode == "compact" else "k_step"
+    kp = pmc.get("kernels", {}) if pmc else {}
+    run_pmc = next((v for k, v in kp.items() if k.split("<")[0] == run_name), None)
+    cls_pmc = next((v for k, v in kp.items() if k.split("<")[0] == "k_classify"), None)
+
+    def kern(name, alg, sec, pm):
+        ach = alg / sec / 1e9 if sec > 0 else None
+        out = {"kernel": name, "alg_bytes_per_launch": alg, "kernel_ms": sec * 1e3,
+               "achieved": ach, "frac": ach / HBM_PEAK_GBS if ach else None,
+               "traffic": pm["hbm_bytes"] if pm else None}
+        if pm:
+            out.update({"traffic_gbs": pm["hbm_bytes"] / sec / 1e9 if sec > 0 else None,
+                        "valu_util": pm.get("valu_util"), "wait_frac": pm.get("wait_frac"),
+                        "limiter": pm.get("limiter")})
+        return out
+
+    run_k = kern(run_name, run_b, run_s, run_pmc)
+    roof = {"bound": "hbm", "kernel": run_name + " (the step's dominant kernel)",
+            "achieved": run_k["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": run_k["frac"], "traffic": run_k["traffic"],
             "traffic_source": pmc["source"] if pmc else None,
-            "kernel_ms": kern_s * 1e3,
-            "alg_bytes_per_launch": alg,
-            "alg_bytes_per_launch_survey": surv,
-            "achieved_survey": surv / kern_s / 1e9,
-            "frac_survey": surv / kern_s / 1e9 / HBM_PEAK_GBS,
-            # what ends the kernels (DESIGN.md §3.5): the go waves' dependent per-tick chains,
-            # not HBM bandwidth; the counters below are the evidence
-            "limiter": ("latency: k_run ends on its idle waves' MT refills (latency-bound twists, "
-                        "DESIGN.md §3.3) and the option tick loops (lane_efficiency, valu_util)"),
-            "valu_util": pmc.get("valu_util") if pmc else None,
-            "lane_efficiency": lane_eff}
+            "kernel_ms": run_s * 1e3, "alg_bytes_per_launch": run_b,
+            "timed_launches": st["timed_launches"],
+            "timing": "HIP events around every %d-th step on the step's stream (start, "
+                      "between the kernels, end)" % args.timing_every,
+            "limiter": run_k.get("limiter"), "valu_util": run_k.get("valu_util"),
+            "wait_frac": run_k.get("wait_frac"), "lane_efficiency": lane_eff}
+    kernels = {"run": run_k}
+    if args.mode == "compact":
+        kernels["classify"] = kern("k_classify", cls_b, cls_s, cls_pmc)
+    roof["step"] = {"kernel": "tg_step = " + (" + ".join(
+                        ["k_classify", "k_run"] if args.mode == "compact" else ["k_step"])),
+                    "alg_bytes_per_launch": cls_b + run_b, "kernel_ms": step_s * 1e3,
+                    "achieved": (cls_b + run_b) / step_s / 1e9,
+                    "frac": (cls_b + run_b) / step_s / 1e9 / HBM_PEAK_GBS,
+                    "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                    "alg_bytes_per_launch_survey": surv,
+                    "frac_survey": surv / step_s / 1e9 / HBM_PEAK_GBS,
+                    "kernels": kernels}
     return {
         "ticks_per_s": node["ticks"] / dt,
         # SURVEY §8d: ticks executed / lane-ticks issued by the tick loops' wavefronts

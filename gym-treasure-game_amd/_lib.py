@@ -58,7 +58,8 @@ class Stats(ctypes.Structure):
                 ("episodes", ctypes.c_int64), ("episodes_dropped", ctypes.c_int64),
                 ("launches", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("regens", ctypes.c_int64),
-                ("wave_ticks", ctypes.c_int64)]
+                ("wave_ticks", ctypes.c_int64), ("timed_launches", ctypes.c_int64),
+                ("run_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

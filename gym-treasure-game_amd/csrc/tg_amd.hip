@@ -1791,13 +1791,39 @@ int stat_slots(int64_t n) {
 }
 
 int flush_timing(tg_batch* h) {
-  for (size_t k = 0; k + 1 < h->ev_used; k += 2) {
-    HIP_TRY(hipEventSynchronize(h->ev[k + 1]));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]));
-    h->kernel_ms_done += ms;
+  for (size_t k = 0; k + 3 <= h->ev_used; k += 3) {
+    HIP_TRY(hipEventSynchronize(h->ev[k + 2]));
+    float all = 0.f, second = 0.f;
+    HIP_TRY(hipEventElapsedTime(&all, h->ev[k], h->ev[k + 2]));
+    HIP_TRY(hipEventElapsedTime(&second, h->ev[k + 1], h->ev[k + 2]));
+    h->kernel_ms_done += all;
+    h->run_ms_done += second;
+    ++h->timed_launches;
   }
   h->ev_used = 0;
+  return TG_OK;
+}
+// timing of one step launch (tg_set_timing): whether this launch is sampled, and its events
+bool timing_begin(tg_batch* h, hipStream_t st, int& rc) {
+  rc = TG_OK;
+  if (!h->timing_every || (h->timing_calls++ % (uint64_t)h->timing_every) != 0) return false;
+  while (h->ev.size() < h->ev_used + 3) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) {
+      rc = fail(TG_E_HIP, "hipEventCreate");
+      return false;
+    }
+    h->ev.push_back(ev);
+  }
+  if (hipEventRecord(h->ev[h->ev_used], st) != hipSuccess) rc = fail(TG_E_HIP, "hipEventRecord");
+  return rc == TG_OK;
+}
+int timing_mark(tg_batch* h, hipStream_t st, int k) {  // k = 1: after the first kernel, 2: end
+  HIP_TRY(hipEventRecord(h->ev[h->ev_used + k], st));
+  if (k == 2) {
+    h->ev_used += 3;
+    if (h->ev_used >= 4095) return flush_timing(h);
+  }
   return TG_OK;
 }
 }  // namespace
@@ -1935,14 +1961,9 @@ namespace {
 // one step's kernels on `st`, timed with HIP events when enabled
 int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
   const bool fo = io.final_obs != nullptr;
-  if (h->timing) {
-    while (h->ev.size() < h->ev_used + 2) {
-      hipEvent_t ev;
-      HIP_TRY(hipEventCreate(&ev));
-      h->ev.push_back(ev);
-    }
-    HIP_TRY(hipEventRecord(h->ev[h->ev_used], st));
-  }
+  int rc;
+  const bool timed = timing_begin(h, st, rc);
+  if (rc) return rc;
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   const dim3 grid(grid_for(h->n)), block(BLOCK);
   if (h->mode == TG_MODE_DIRECT) {
@@ -1956,6 +1977,7 @@ int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
     else
       kern = ar ? (fo ? k_step<true, true> : k_step<true, false>)
                 : (fo ? k_step<false, true> : k_step<false, false>);
+    if (timed && (rc = timing_mark(h, st, 1))) return rc;
     hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, h->g0,
                        h->stats, h->err);
   } else {
@@ -1980,16 +2002,12 @@ int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
     hipLaunchKernelGGL(kc, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, w, h->g0,
                        h->stats, h->err);
     HIP_TRY(hipGetLastError());
+    if (timed && (rc = timing_mark(h, st, 1))) return rc;
     hipLaunchKernelGGL(kr, dim3(run_grid_for(h->n)), block, 0, st, h->S, h->n, h->L, h->grid, io,
                        q, w, h->g0, h->stats, h->err);
   }
   HIP_TRY(hipGetLastError());
-  if (h->timing) {
-    HIP_TRY(hipEventRecord(h->ev[h->ev_used + 1], st));
-    h->ev_used += 2;
-    if (h->ev_used >= 4096) return flush_timing(h);
-  }
-  return TG_OK;
+  return timed ? timing_mark(h, st, 2) : TG_OK;
 }
 
 // envs per k_rollout workgroup: one round of workgroups fills every CU's resident slots
@@ -2000,14 +2018,9 @@ int32_t ro_envs_per_block(int64_t n, int slots) {
 }
 
 int launch_rollout(tg_batch* h, const RollIO& R, bool ar, hipStream_t st) {
-  if (h->timing) {
-    while (h->ev.size() < h->ev_used + 2) {
-      hipEvent_t ev;
-      HIP_TRY(hipEventCreate(&ev));
-      h->ev.push_back(ev);
-    }
-    HIP_TRY(hipEventRecord(h->ev[h->ev_used], st));
-  }
+  int rc;
+  const bool timed = timing_begin(h, st, rc);
+  if (rc) return rc;
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   decltype(&k_rollout<true, 0>) kern;
   if (R.io.policy == TG_POLICY_UNIFORM)
@@ -2025,15 +2038,11 @@ int launch_rollout(tg_batch* h, const RollIO& R, bool ar, hipStream_t st) {
   if ((int64_t)grid.x > (int64_t)stat_slots(h->n))
     return fail(TG_E_INVAL, "k_rollout: %u workgroups exceed the %d counter slots", grid.x,
                 stat_slots(h->n));
+  if (timed && (rc = timing_mark(h, st, 1))) return rc;
   hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, R, q, h->g0, E,
                      h->stats, h->err);
   HIP_TRY(hipGetLastError());
-  if (h->timing) {
-    HIP_TRY(hipEventRecord(h->ev[h->ev_used + 1], st));
-    h->ev_used += 2;
-    if (h->ev_used >= 4096) return flush_timing(h);
-  }
-  return TG_OK;
+  return timed ? timing_mark(h, st, 2) : TG_OK;
 }
 }  // namespace
 
@@ -2224,9 +2233,11 @@ int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
   return TG_OK;
 }
 
-int tg_set_timing(tg_batch* h, int enable) {
+int tg_set_timing(tg_batch* h, int every) {
   BIND(h);
-  h->timing = enable != 0;
+  if (every < 0) return fail(TG_E_INVAL, "tg_set_timing: every %d < 0", every);
+  h->timing_every = every;
+  h->timing_calls = 0;
   return TG_OK;
 }
 
@@ -2279,6 +2290,8 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   out->kernel_ms = h->kernel_ms_done;
   out->regens = (int64_t)s[ST_REGENS];
   out->wave_ticks = (int64_t)s[ST_WTICKS];
+  out->timed_launches = h->timed_launches;
+  out->run_ms = h->run_ms_done;
   return TG_OK;
 }
 
@@ -2288,6 +2301,8 @@ int tg_stats_reset(tg_batch* h) {
   HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(h->n)));
   h->ev_used = 0;
   h->kernel_ms_done = 0.0;
+  h->run_ms_done = 0.0;
+  h->timed_launches = 0;
   return TG_OK;
 }
 

@@ -78,10 +78,13 @@ struct tg_batch {
   uint8_t* nrefill = nullptr;
   int parity = 0;  // which half of wctr this compact step counts in
   int64_t shard_cap = 0;
-  bool timing = false;
-  std::vector<hipEvent_t> ev;  // (start, stop) pairs
+  int timing_every = 0;        // HIP-event timing of every k-th step launch (0: off)
+  uint64_t timing_calls = 0;   // step launches since timing was enabled
+  std::vector<hipEvent_t> ev;  // (start, after the first kernel, stop) triples
   size_t ev_used = 0;
-  double kernel_ms_done = 0.0;
+  double kernel_ms_done = 0.0;  // the timed launches' step kernels
+  double run_ms_done = 0.0;     //   of which the second (k_run), or the single kernel
+  int64_t timed_launches = 0;
   std::string domain;              // domain.txt text (the renderer's cell sprites)
   double* obs_scratch = nullptr;   // tg_rollout without an obs output
   tg::TgOne* one = nullptr;            // tg_step1's row: pinned host memory the kernel writes

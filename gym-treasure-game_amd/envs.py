@@ -312,8 +312,10 @@ class TreasureGameVec:
                                          self._stream()), "tg_predicate_table")
         return out
 
-    def set_timing(self, enable=True):
-        check(self._L.tg_set_timing(self.handle, int(bool(enable))), "tg_set_timing")
+    def set_timing(self, every=1):
+        """HIP-event timing of every ``every``-th step launch (0 / False: off; True: every
+        launch).  stats() then holds kernel_ms / run_ms summed over timed_launches."""
+        check(self._L.tg_set_timing(self.handle, int(every)), "tg_set_timing")
 
     def stats(self):
         s = _lib.Stats()

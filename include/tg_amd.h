@@ -96,12 +96,15 @@ typedef struct {
   int64_t episodes;     /* completed episodes (auto-reset) */
   int64_t episodes_dropped; /* records lost because the queue (max(4N, 65536)) was full */
   int64_t launches;     /* step-kernel launches */
-  double kernel_ms;     /* summed step-kernel time measured with HIP events (if enabled) */
+  double kernel_ms;     /* summed step-kernel time of the timed launches (tg_set_timing) */
   int64_t regens;       /* MT19937 generations regenerated by the step kernels (624 words +
                            312 random() values each) */
   int64_t wave_ticks;   /* sum over the tick loops' wavefronts of their longest lane's ticks:
                            lane efficiency = ticks / (64 * wave_ticks) (an upper bound for the
                            go loops, whose lanes may also wait for the others' plain ticks) */
+  int64_t timed_launches; /* launches timed with HIP events (tg_set_timing) */
+  double run_ms;        /* of kernel_ms, the second kernel's time (k_run in the compact mode; the
+                           single kernel of the direct / async launches) */
 } tg_stats;
 
 /* Create N envs on `device`: env i is `random.seed(seed_base + global_offset + i);
@@ -194,9 +197,11 @@ int tg_errors(tg_batch *h, uint32_t *or_of_flags, void *stream);
 #define TG_MODE_ASYNC 2
 int tg_set_mode(tg_batch *h, int mode, int run_blocks);
 
-/* Enable HIP-event timing of every tg_step (adds two event records per step; the measured
- * interval covers all of the step's kernels). */
-int tg_set_timing(tg_batch *h, int enable);
+/* HIP-event timing of every `every`-th step launch (tg_step, tg_rollout's launches; 0 = off):
+ * three event records around a timed launch (start, after the first kernel, end), accumulated
+ * into tg_stats.kernel_ms / run_ms / timed_launches.  An event record between two kernels costs
+ * the stream a gap of several microseconds, so a benchmark samples (e.g. every 8th step). */
+int tg_set_timing(tg_batch *h, int every);
 /* Capacity of the completed-episode queue (default max(4N, 65536) records).  Records that
  * arrive while it is full are dropped and counted (tg_stats.episodes_dropped); the count is
  * clamped so that an undrained queue never overflows.  Reallocates the queue and discards

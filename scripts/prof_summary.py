@@ -5,10 +5,18 @@
 
 Reads the rocprofv3 kernel-trace stats (same command as bench.py) and the separate PMC passes
 (FETCH_SIZE, WRITE_SIZE, SQ_*).  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE /
-WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts a wide coalesced 128-B read request as 64 B,
-so it is calibrated here on k_errors, which reads exactly 16 B per env (one uint4) in fully
-coalesced 16-B lanes and nothing else.  The calibration factor is applied to k_step's
-FETCH_SIZE and reported beside the raw value.
+WRITE_SIZE are in KiB.  FETCH_SIZE is calibrated per access pattern by scripts/calib/
+calib_fetch.hip (profiles/r03/fetch_calibration.json): a coalesced stream (dword or 16-B lanes)
+is reported at HALF its bytes; a scattered 8-B / 16-B load or 16-B LDS-DMA (one env per lane)
+is reported as 64-66 B, one 64-B HBM read each; WRITE_SIZE is 1:1 for coalesced stores and 32 B
+per scattered 8- or 16-B store (the write granule).  So each step kernel's HBM read bytes are
+its coalesced reads (known from the step's counters: the bench line of the profiled run) plus
+the rest of FETCH_SIZE at face value:
+    hbm_read = coalesced + (FETCH_SIZE - coalesced / 2)
+k_classify's reads are all coalesced (env-order loads); k_run's coalesced reads are the
+worklist rows (44 B per valid env) and the twist sources (2,496 B + a 4-B list entry per
+regenerated half); its scattered reads are the code-window LDS-DMA fills.  The k_errors factor
+(the round-2 method, 2.0 for its coalesced 16-B reads) is kept beside it as a cross-check.
 """
 import argparse
 import csv
@@ -75,7 +83,9 @@ def main():
     res["kernel_trace"] = ks
     pm = {}
     meta = {}
-    prof_line = bench_line(os.path.join(a.out, "pmc_fetch.log"))
+    prof_line = bench_line(os.path.join(a.out, "pmc_fetch_%s.log" % a.policy))
+    if prof_line is None:
+        prof_line = bench_line(os.path.join(a.out, "pmc_fetch.log"))
     last = prof_line["steps"] if prof_line else None
     for p in ("fetch", "write", "sq1", "sq2"):
         path = os.path.join(a.out, "pmc_%s_%s" % (p, a.tag), "run_counter_collection.csv")
@@ -93,17 +103,58 @@ def main():
         known = 16.0 * a.envs  # k_errors: one 16-B uint4 per env, 16 B per lane
         raw_err = pm["k_errors"]["FETCH_SIZE"] * 1024.0
         cal = known / raw_err if raw_err > 0 else None
+        valid = (prof_line or {}).get("valid_step_frac", 0.0) * a.envs
+        regens = (prof_line or {}).get("regens_per_step", 0.0)
         per = {}
         for k in step_k:
             fr = pm[k]["FETCH_SIZE"] * 1024.0
             wr = pm[k].get("WRITE_SIZE", 0.0) * 1024.0
-            per[k] = {"fetch_bytes_raw": fr, "fetch_bytes": fr * (cal or 1.0), "write_bytes": wr}
-        tot = sum(v["fetch_bytes"] + v["write_bytes"] for v in per.values())
-        res["hbm"] = {"kernels": per, "fetch_calibration": cal, "hbm_bytes_per_launch": tot,
-                      "calibration_note": "FETCH_SIZE x (16 B/env read by k_errors / its FETCH_SIZE); "
-                                          "k_errors reads %d B, FETCH_SIZE reported %.0f B "
-                                          "(MI355X_MICROARCH.md: wide reads tallied at half)" %
-                                          (known, raw_err)}
+            base = k.split("<")[0]
+            if base == "k_classify":
+                coal = 44.0 * a.envs
+            elif base == "k_run":
+                coal = 44.0 * valid + 2500.0 * regens
+            else:  # k_step: env-order state loads + the refills' sources
+                coal = 44.0 * a.envs + 2496.0 * regens
+            scat = max(fr - coal / 2.0, 0.0)
+            rd = coal + scat
+            kn = ks.get(k, {}).get("avg_ns")
+            cyc = pm[k].get("SQ_WAVE_CYCLES")
+            ent = {"fetch_bytes_raw": fr, "coalesced_read_bytes": coal,
+                   "scattered_read_bytes": scat, "read_bytes": rd, "write_bytes": wr,
+                   "hbm_bytes": rd + wr, "fetch_bytes_kerrors_factor": fr * (cal or 1.0),
+                   "avg_ns": kn}
+            if kn:
+                ent["hbm_gbs"] = (rd + wr) / kn
+                v = pm[k].get("SQ_INSTS_VALU")
+                # VALU issue utilisation: wave64 VALU instructions x 2 cycles (SIMD-32) over the
+                # SIMD-cycles of the kernel's duration at the 2.4 GHz nominal clock
+                ent["valu_util"] = v * 2.0 / (1024 * kn * 2.4) if v else None
+            if cyc:
+                ent["wait_frac"] = pm[k].get("SQ_WAIT_ANY", 0.0) / cyc
+                ent["lds_bank_conflict_frac"] = (pm[k].get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                                                 max(pm[k].get("SQ_ACTIVE_INST_LDS", 1.0), 1.0))
+            # what bounds the kernel, from the counters: HBM when its traffic runs at >= 60 %
+            # of the 8 TB/s peak, VALU when issue is >= 60 % busy, else latency
+            g, vu, wf = ent.get("hbm_gbs"), ent.get("valu_util"), ent.get("wait_frac")
+            if g is not None and g >= 0.6 * 8000:
+                ent["limiter"] = "hbm (%.0f GB/s)" % g
+            elif vu is not None and vu >= 0.6:
+                ent["limiter"] = "valu (issue %.0f %%)" % (100 * vu)
+            elif g is not None:
+                ent["limiter"] = ("latency: HBM %.0f GB/s (%.0f %% of peak), VALU issue %s, waves "
+                                  "waiting %s of their cycles" %
+                                  (g, g / 80.0, "%.0f %%" % (100 * vu) if vu is not None else "?",
+                                   "%.0f %%" % (100 * wf) if wf is not None else "?"))
+            per[k] = ent
+        tot = sum(v["hbm_bytes"] for v in per.values())
+        res["hbm"] = {"kernels": per, "hbm_bytes_per_launch": tot,
+                      "calibration": "per access pattern (profiles/r03/fetch_calibration.json): "
+                                     "coalesced reads reported at 1/2, scattered 8/16-B loads "
+                                     "and LDS-DMA at one 64-B read each, writes 1:1",
+                      "fetch_calibration_kerrors": cal,
+                      "kerrors_note": "k_errors reads %d B, FETCH_SIZE reported %.0f B" %
+                                      (known, raw_err)}
         ns = sum(ks[k]["avg_ns"] for k in ks if k.split("<")[0] in names)
         res["step_kernels_avg_ns"] = ns
         # VALU issue utilisation of the step kernels: wave64 VALU instructions x 2 cycles
@@ -111,7 +162,12 @@ def main():
         valu = sum(pm[k].get("SQ_INSTS_VALU", 0.0) for k in step_k)
         valu_util = valu * 2.0 / (1024 * ns * 2.4) if valu and ns else None
         res["valu_util"] = valu_util
-        tj = {"envs": a.envs, "policy": a.policy, "mode": a.mode, "kernels": sorted(step_k),
+        tj = {"envs": a.envs, "policy": a.policy, "mode": a.mode,
+              "kernels": {k: {f: v[f] for f in ("hbm_bytes", "read_bytes", "write_bytes",
+                                                 "coalesced_read_bytes", "scattered_read_bytes",
+                                                 "avg_ns", "hbm_gbs", "valu_util", "wait_frac",
+                                                 "lds_bank_conflict_frac", "limiter")
+                              if f in v} for k, v in per.items()},
               "hbm_bytes_per_launch": tot, "step_kernels_avg_ns": ns, "valu_util": valu_util,
               "regens_per_step": prof_line.get("regens_per_step") if prof_line else None,
               "burn_in": prof_line.get("burn_in") if prof_line else None,
