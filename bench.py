@@ -61,14 +61,19 @@ EP_CAP = 4096          # episode records gathered per rank per step of a drain i
 #   k_classify, every env: action 4 + state word 16 + angles 16 + episode 8 read (44)
 #     reward-None env: episode 8 + obs 72 + reward/valid/done 6 written (86)
 #     valid env: worklist index 4 + state 16 + angles 16 + episode 8 written (44)
-#     stale MT half: its refill-list entry 4 written
+#     stale MT half: its refill-list entry 4 written (1 per generation: a half is 4)
 #   k_run, valid env: the worklist row 44 read; state 16 + angles 16 + episode 8 + obs 72 +
-#     rows 6 written (118); random() draw: its 1-B code (tg_core.h draw_code); MT regeneration:
-#     the refill entry 4 + 624 words read, 624 words + 312 codes written
+#     rows 6 written (118); random() draw: its 1-B code (tg_core.h draw_code); MT generation
+#     regenerated (tg_core.h: halves of MT_HALF_GENS = 4 generations, chained in LDS): 624
+#     words + 312 codes written, a quarter of the source generation's 624 words and of the
+#     4-B refill entry read
 #   k_step (direct mode): one kernel, the same without the worklist round trip
-CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 86, 44, 4
-RUN_VALID, RUN_DRAW, RUN_REGEN = 162, 1, 5308
-DIRECT_ENV, DIRECT_INVALID, DIRECT_VALID, DIRECT_REGEN = 44, 86, 118, 5304
+MT_HALF_GENS = 4
+CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 86, 44, 4 / MT_HALF_GENS
+RUN_VALID, RUN_DRAW = 162, 1
+RUN_REGEN = 2496 + 312 + (2496 + 4) / MT_HALF_GENS
+DIRECT_ENV, DIRECT_INVALID, DIRECT_VALID = 44, 86, 118
+DIRECT_REGEN = 2496 + 312 + 2496 / MT_HALF_GENS
 BYTES_DRAW = RUN_DRAW
 # SURVEY.md §8(d)'s layout-independent count per env-step: action 4 + obs 72 + reward 4 +
 # valid 1 + done 1 + state read/write 2 x 40 = 162, plus 24 per random() draw (8 B of MT words

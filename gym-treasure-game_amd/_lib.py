@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtg_amd.so")
+# TG_LIB_PATH: an A/B variant build (scripts/build_variant.py) in place of the product library
+LIB_PATH = os.environ.get("TG_LIB_PATH") or os.path.join(HERE, "libtg_amd.so")
 
 TG_OK = 0
 TG_STEP_AUTORESET = 1

@@ -115,27 +115,38 @@ __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o
 //   Draws that need the double (handle angles in a flip cascade, an auto-reset's uniform and
 //   gauss) consume the code and read the position's two words (one 8-B load).
 // ------------------------------------------------------------------------------------------
-constexpr uint32_t CODE_CHUNKS = MT_CODES / 16;  // 39
-static_assert(MT_CODES % 16 == 0, "whole 16-B code chunks per env");
-constexpr int WIN_CHUNKS = 4;  // 7 until r02e (8 instead of 5 workgroups per CU)
-constexpr int WIN_SLOT_BYTES = 64 * 16;
-constexpr int WIN_WAVE_BYTES = WIN_CHUNKS * WIN_SLOT_BYTES;  // 4 KB per wave
+#ifndef TG_WIN_UNIT
+#define TG_WIN_UNIT 16
+#endif
+constexpr int WIN_UNIT = TG_WIN_UNIT;  // code bytes per lane per LDS-DMA (16: dwordx4, 4: dword)
+static_assert(WIN_UNIT == 16 || WIN_UNIT == 4, "global_load_lds_dwordx4 or _dword");
+constexpr int WIN_DRAWS = 64;                       // codes per lane in the window
+constexpr int WIN_SLOTS = WIN_DRAWS / WIN_UNIT;     // DMA instructions per fill
+constexpr int WIN_SLOT_BYTES = 64 * WIN_UNIT;       // one slot: every lane's unit
+constexpr uint32_t CODE_UNITS = MT_CODES / WIN_UNIT;
+static_assert(MT_CODES % WIN_UNIT == 0, "whole DMA units of codes per env");
+constexpr int WIN_WAVE_BYTES = WIN_SLOTS * WIN_SLOT_BYTES;  // 4 KB per wave
 constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
 static_assert(WIN_WAVE_BYTES >= WAVE_SCRATCH, "wave_refill reuses the window as scratch");
-static_assert(WIN_CHUNKS * 16 - 15 >= (int)MAX_TICK_DRAWS, "a refilled window holds a tick's draws");
+static_assert(WIN_DRAWS - WIN_UNIT + 1 >= (int)MAX_TICK_DRAWS, "a refilled window holds a tick's draws");
 
 typedef __attribute__((address_space(1))) uint32_t glb_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-// LDS-DMA of one 16-B chunk per active lane into LDS [m0 + lane * 16]; M0 is saved/restored
-__device__ __forceinline__ void glds16(uint32_t m0, const void* gptr) {
+// LDS-DMA of one WIN_UNIT-byte unit per active lane into LDS [m0 + lane * WIN_UNIT]; M0 is
+// saved/restored
+__device__ __forceinline__ void glds_unit(uint32_t m0, const void* gptr) {
   uint32_t save;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"
+#if TG_WIN_UNIT == 16
       "global_load_lds_dwordx4 %2, off\n\t"
+#else
+      "global_load_lds_dword %2, off\n\t"
+#endif
       "s_mov_b32 m0, %0"
       : "=&s"(save)
       : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
@@ -144,8 +155,7 @@ __device__ __forceinline__ void glds16(uint32_t m0, const void* gptr) {
 
 // the rare second crossing (RngCodes::fill), out of line so that the draw sites stay small
 __device__ __noinline__ void regen_half(uint32_t* mt, uint8_t* mc, uint32_t h) {
-  twist_gen(mt + (MT_N - h), mt + h);
-  gen_codes(mt + h, mc + h / 2);
+  twist_half(mt, h, mc);
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
 }
 
@@ -153,7 +163,7 @@ struct RngCodes {
   static constexpr uint32_t NONE = 0xFFFFFFFFu;
   uint32_t* mt;      // this env's MT_WORDS words (HBM)
   uint8_t* mc;       // this env's MT_CODES code bytes (HBM)
-  lds_u8* cell;      // this lane's 16-B cell in slot 0 of the wave's window
+  lds_u8* cell;      // this lane's unit in slot 0 of the wave's window
   uint32_t m0;       // LDS address of slot 0 of the wave's window (wave-uniform)
   uint32_t pos;      // word position of the window's first draw (even)
   uint32_t n;        // draws taken since then
@@ -166,20 +176,20 @@ struct RngCodes {
   bool primed, loaded, entered;  // entered: a half was entered in this launch (as tg::Rng)
 
   __device__ __forceinline__ RngCodes(uint32_t* m, uint8_t* c, uint32_t state, lds_u8* wave_win)
-      : mt(m), mc(c), cell(wave_win + (threadIdx.x & 63) * 16),
+      : mt(m), mc(c), cell(wave_win + (threadIdx.x & 63) * WIN_UNIT),
         m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_win)),
         pos(state & MT_POS_MASK), n(0u), rd(0u), left(0u), nxc(0u),
-        stale((state & MT_STALE) ? (uint32_t)MT_N - mt_half(state & MT_POS_MASK) : NONE),
+        stale((state & MT_STALE) ? (uint32_t)MT_HALF - mt_half(state & MT_POS_MASK) : NONE),
         draws(0u), regens(0u), primed(false), loaded(false), entered(false) {}
 
-  // fold the draws taken since the window start into pos (a window is < 312 draws, so at
-  // most one half boundary lies in between).  Entering a half that is stale (possible only
+  // fold the draws taken since the window start into pos (a window is < MT_HALF / 2 draws, so
+  // at most one half boundary lies in between).  Entering a half that is stale (possible only
   // when the window ended exactly at the boundary, so nothing of it was read) regenerates it
   // first, from the half being left, which then becomes the stale one.
   __device__ __forceinline__ void sync() {
     const uint32_t d = pos >> 1, e = d + n;
-    if (e / (MT_N / 2) != d / (MT_N / 2)) {
-      const uint32_t left_half = mt_half(pos), entered_half = (uint32_t)MT_N - left_half;
+    if (e / (MT_HALF / 2) != d / (MT_HALF / 2)) {
+      const uint32_t left_half = mt_half(pos), entered_half = (uint32_t)MT_HALF - left_half;
       if (stale == entered_half) {
         regen_half(mt, mc, entered_half);
         ++regens;
@@ -187,18 +197,18 @@ struct RngCodes {
       stale = left_half;
       entered = true;
     }
-    pos = 2u * (e >= (uint32_t)MT_N ? e - (uint32_t)MT_N : e);
+    pos = 2u * (e >= (uint32_t)MT_CODES ? e - (uint32_t)MT_CODES : e);
     n = 0u;
   }
   // DMA the window starting at pos (all lanes reaching it start at slot 0: one DMA per slot)
   __device__ __forceinline__ void fill() {
-    const uint32_t d = pos >> 1, c0 = d >> 4;
+    const uint32_t d = pos >> 1, c0 = d / (uint32_t)WIN_UNIT;
     if (stale != NONE) {
-      // the draws the window serves are words [pos, pos + 2 * left) (mod 1248; the bytes of
+      // the draws the window serves are words [pos, pos + 2 * left) (mod MT_WORDS; the bytes of
       // its first and last chunks outside that range are never read): regenerate the stale
       // half first if they overlap it
-      const uint32_t w0 = pos, w1 = pos + 2u * ((uint32_t)WIN_CHUNKS * 16u - (d & 15u));
-      if ((w0 < stale + (uint32_t)MT_N && stale < w1) ||
+      const uint32_t w0 = pos, w1 = pos + 2u * ((uint32_t)WIN_DRAWS - d % (uint32_t)WIN_UNIT);
+      if ((w0 < stale + (uint32_t)MT_HALF && stale < w1) ||
           (w1 > (uint32_t)MT_WORDS && stale < w1 - (uint32_t)MT_WORDS)) {
         regen_half(mt, mc, stale);
         ++regens;
@@ -206,17 +216,17 @@ struct RngCodes {
       }
     }
 #pragma unroll
-    for (int j = 0; j < WIN_CHUNKS; ++j) {
-      const uint32_t c = c0 + j < CODE_CHUNKS ? c0 + j : c0 + j - CODE_CHUNKS;
-      glds16(m0 + j * WIN_SLOT_BYTES, mc + c * 16u);
+    for (int j = 0; j < WIN_SLOTS; ++j) {
+      const uint32_t c = c0 + j < CODE_UNITS ? c0 + j : c0 + j - CODE_UNITS;
+      glds_unit(m0 + j * WIN_SLOT_BYTES, mc + c * (uint32_t)WIN_UNIT);
     }
-    rd = d & 15u;
-    left = (uint32_t)WIN_CHUNKS * 16u - rd;
+    rd = d % (uint32_t)WIN_UNIT;
+    left = (uint32_t)WIN_DRAWS - rd;
     loaded = false;
   }
   __device__ __forceinline__ uint32_t read() const {
-    const uint32_t r = rd < (uint32_t)WIN_CHUNKS * 16u ? rd : 0u;  // stay inside the window
-    return cell[(r >> 4) * WIN_SLOT_BYTES + (r & 15u)];
+    const uint32_t r = rd < (uint32_t)WIN_DRAWS ? rd : 0u;  // stay inside the window
+    return cell[(r / WIN_UNIT) * WIN_SLOT_BYTES + r % WIN_UNIT];
   }
   __device__ __forceinline__ void prime() {
     fill();
@@ -239,9 +249,10 @@ struct RngCodes {
   }
   // at least k draws staged (no refill: the plain go loop's exit test)
   __device__ __forceinline__ bool has(uint32_t k) const { return left >= k; }
-  // the code dword holding draws 4d .. 4d + 3 of the window (d < WIN_CHUNKS * 4)
+  // the code dword holding draws 4d .. 4d + 3 of the window (d < WIN_DRAWS / 4)
   __device__ __forceinline__ uint32_t dword(uint32_t d) const {
-    return *reinterpret_cast<const lds_u32*>(cell + (d >> 2) * WIN_SLOT_BYTES + (d & 3u) * 4u);
+    return *reinterpret_cast<const lds_u32*>(cell + (4u * d / WIN_UNIT) * WIN_SLOT_BYTES +
+                                             (4u * d) % WIN_UNIT);
   }
   // walk_ticks (tg_core.h) four draws per LDS read: the codes of a dword are applied one by one
   // (each tick checks the span, the staged draws and the cap at its start, as walk_ticks), so
@@ -295,7 +306,7 @@ struct RngCodes {
   __device__ __forceinline__ void phase(int) {}
 #endif
   // a draw was taken past the staged window (reserve's bound broken: flagged E_WINDOW)
-  __device__ __forceinline__ bool overrun() const { return left > (uint32_t)WIN_CHUNKS * 16u; }
+  __device__ __forceinline__ bool overrun() const { return left > (uint32_t)WIN_DRAWS; }
   // one draw, consumed for its outcomes (draw_code); reserve() guarantees it is in the window
   __device__ __forceinline__ uint32_t code() {
     const uint32_t c = nxc;
@@ -309,7 +320,7 @@ struct RngCodes {
   // one draw as its double (rare): the code is consumed too, the value built from the words
   __device__ __forceinline__ double random() {
     uint32_t p = (pos >> 1) + n;
-    p = 2u * (p >= (uint32_t)MT_N ? p - (uint32_t)MT_N : p);
+    p = 2u * (p >= (uint32_t)MT_CODES ? p - (uint32_t)MT_CODES : p);
     (void)code();
     const uint2 w = *reinterpret_cast<const uint2*>(mt + p);
     return mt_double(w.x, w.y);
@@ -333,6 +344,22 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
   const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
   return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// a generation's 312 draw codes from its words in LDS, draw d = r * 64 + lane per round: its
+// two words are one 8-B LDS read at an 8-B lane stride (conflict-free; four draws per lane at a
+// 32-B stride were 2-way conflicts), its code one byte of a coalesced 64-B store
+__device__ __forceinline__ void codes_from_lds(const lds_u32* w, uint8_t* dst_c) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
+    const int d = r * 64 + lane;
+    if (d < MT_N / 2) dst_c[d] = (uint8_t)draw_code(mt_double(w[2 * d], w[2 * d + 1]));
+  }
 }
 // The whole-wave twist's inputs: 30 dwords per lane, loaded by twist_load, used by twist_store.
 struct TwistIn {
@@ -367,48 +394,64 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
     // fence orders the LDS accesses in the compiler (one wave's LDS operations execute in
     // order), without the hardware wait for the store's completion (A/B against s_waitcnt
     // lgkmcnt(0) after every round: 0.1322 vs 0.1340 ms)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_fence();
   }
-  // the generation's 312 draw codes, draw d = r * 64 + lane per round: its two words are one
-  // 8-B LDS read at an 8-B lane stride (conflict-free; four draws per lane at a 32-B stride
-  // were 2-way conflicts), its code one byte of a coalesced 64-B store
-#pragma unroll
-  for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
-    const int d = r * 64 + lane;
-    if (d < MT_N / 2) {
-      const lds_u32* w = scratch + 2 * d;
-      dst_c[d] = (uint8_t)draw_code(mt_double(w[0], w[1]));
-    }
-  }
+  codes_from_lds(scratch, dst_c);
 }
-// Regenerate one env's stale half with the whole wave: dst = twist_gen(src), 64 words per round,
-// coalesced.  Words p < 227 read the old generation only; p >= 227 need new[p - 227], which an
-// earlier round wrote into the wave's LDS scratch (rounds are >= 3 apart; twist_store orders
-// the rounds' LDS accesses with wavefront fences).  src / dst are wave-uniform; must be reached
-// by all 64 lanes of the wave.
-__device__ __forceinline__ void wave_twist(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
-                                           lds_u32* scratch) {
+// The next generation in place in LDS (s: a generation -> its successor), stored to dst with
+// its codes.  Round r reads words p + 1 (old: written by round r + 1's lanes) and p + 397 (old
+// for p < 227: rounds >= 6 write them) or p - 227 (new: >= 3 rounds earlier) and then writes
+// p; a lane's store depends on its three reads, and the wave's reads of a round precede its
+// writes (one wave's LDS operations execute in order).  Must be reached by all 64 lanes.
+__device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst_c) {
+  const int lane = threadIdx.x & 63;
+  wave_fence();  // the previous codes pass's reads of s before this twist's writes
+#pragma unroll
+  for (int r = 0; r < TwistIn::ROUNDS; ++r) {
+    const int p = r * 64 + lane;
+    if (p < MT_N) {
+      const uint32_t a = s[p];
+      const uint32_t b = s[p + 1 < MT_N ? p + 1 : 0];
+      const uint32_t c = s[p < MT_N - MT_M ? p + MT_M : p - (MT_N - MT_M)];
+      const uint32_t w = mt_twist(a, b, c);
+      s[p] = w;
+      dst[p] = w;
+    }
+    wave_fence();
+  }
+  codes_from_lds(s, dst_c);
+}
+// `gens` generations in sequence after src (a generation in HBM) into dst, dst + MT_N, ...
+// (words) and dst_c, dst_c + MT_N / 2, ... (codes): the first twisted from registers, the rest
+// chained in the wave's LDS scratch, so a half's regeneration reads one generation from HBM.
+// src / dst are wave-uniform; must be reached by all 64 lanes.
+__device__ __forceinline__ void twist_chain(const TwistIn& t, glb_u32* dst, uint8_t* dst_c, int gens,
+                                            lds_u32* scratch) {
+  twist_store(t, dst, dst_c, scratch);
+  for (int g = 1; g < gens; ++g) twist_lds(scratch, dst + g * MT_N, dst_c + g * (MT_N / 2));
+}
+__device__ __forceinline__ void wave_twist_gens(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
+                                                int gens, lds_u32* scratch) {
   TwistIn t;
   twist_load(src, t);
-  twist_store(t, dst, dst_c, scratch);
+  twist_chain(t, dst, dst_c, gens, scratch);
 }
 // For every lane in `need`: regenerate the stale half of its env (the one not holding the
-// position in its state word), one env at a time.  Must be reached by all 64 lanes.
+// position in its state word), one env at a time, with the whole wave (wave_twist_gens: its
+// MT_HALF_GENS generations from the other half's last).  Must be reached by all 64 lanes.
 __device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* env_mt, uint8_t* env_mc,
                                             uint32_t state, lds_u32* scratch) {
   const uint32_t pos = state & MT_POS_MASK;
-  const uint32_t dst = MT_N - mt_half(pos);
-  const uint64_t src_l = (uint64_t)(uintptr_t)(env_mt + mt_half(pos));
+  const uint32_t dst = (uint32_t)MT_HALF - mt_half(pos);
+  const uint64_t src_l = (uint64_t)(uintptr_t)(env_mt + mt_prev_gen(dst));
   const uint64_t dst_l = (uint64_t)(uintptr_t)(env_mt + dst);
   const uint64_t dc_l = (uint64_t)(uintptr_t)(env_mc + dst / 2);
   while (need) {
     const int L = __ffsll((long long)need) - 1;
     need &= need - 1;
-    wave_twist((const glb_u32*)(uintptr_t)readlane64(src_l, L),
-               (glb_u32*)(uintptr_t)readlane64(dst_l, L),
-               (uint8_t*)(uintptr_t)readlane64(dc_l, L), scratch);
+    wave_twist_gens((const glb_u32*)(uintptr_t)readlane64(src_l, L),
+                    (glb_u32*)(uintptr_t)readlane64(dst_l, L),
+                    (uint8_t*)(uintptr_t)readlane64(dc_l, L), MT_HALF_GENS, scratch);
   }
 }
 
@@ -432,30 +475,39 @@ __device__ __forceinline__ int wave_max(int v) {
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
-// random.seed(seed0 + i): init_by_array into the second half of the env's MT buffer; two
-// k_gen_twist launches then make generations 1 and 2, and k_reset (mask NULL) performs the
-// constructor's game build (_TreasureGameImpl.__init__, IM/:31-53: 4 draws) — tg_create.
+// random.seed(seed0 + i): init_by_array into the ring's last generation slot (tg_core.h
+// init_mt); k_gen_twist then makes generations 1 .. 2 x MT_HALF_GENS, and k_reset (mask NULL)
+// performs the constructor's game build (_TreasureGameImpl.__init__, IM/:31-53: 4 draws) —
+// tg_create.
 __global__ __launch_bounds__(BLOCK) void k_create(Soa S, int64_t n, uint64_t seed0,
                                                    const uint32_t* __restrict__ genrand) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
-  seed_mt(S.mt + i * MT_WORDS + MT_N, genrand, seed0 + (uint64_t)i);
+  seed_mt(S.mt + i * MT_WORDS + (MT_WORDS - MT_N), genrand, seed0 + (uint64_t)i);
   Env e{};
   e.mti = 0u;
   S.st4[i] = pack(e);
   S.ang[i] = make_double2(0.0, 0.0);
   S.ep[i] = make_int2(0, 0);
 }
-// one generation for every env: the half at from_pos -> the other half
-__global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t from_pos) {
+// `gens` generations for every env, in sequence after the one at word offset src, into word
+// offsets dst, dst + MT_N, ... (words and codes; tg_create, tg_write_state)
+__global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t src, uint32_t dst,
+                                                     int gens) {
   __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const bool live = i < n;
-  wave_refill(__ballot(live), S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES, from_pos,
-              (lds_u32*)scratch[threadIdx.x >> 6]);
+  unsigned long long need = __ballot(i < n);
+  const int64_t i0 = i - (threadIdx.x & 63);
+  while (need) {
+    const int L = __ffsll((long long)need) - 1;
+    need &= need - 1;
+    const int64_t e = i0 + L;
+    wave_twist_gens((const glb_u32*)(S.mt + e * MT_WORDS + src), (glb_u32*)(S.mt + e * MT_WORDS + dst),
+                    S.mc + e * MT_CODES + dst / 2, gens, (lds_u32*)scratch[threadIdx.x >> 6]);
+  }
 }
 
-// the draw codes of the first half (words [0, 624)) of every env (tg_write_state)
+// the draw codes of the ring's first generation (words [0, 624)) of every env (tg_write_state)
 __global__ __launch_bounds__(BLOCK) void k_gen_codes(Soa S, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i < n) gen_codes(S.mt + i * MT_WORDS, S.mc + i * MT_CODES);
@@ -1037,21 +1089,24 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
         regens += cnt;
         if (!cnt) continue;
         const uint32_t ent_l = lane < cnt ? w.refill[(int64_t)rg * 64 + lane] : 0u;
+        // entry: env | (the half holding its position) << 31; the other half is regenerated
+        // from the last generation of that one
         TwistIn t;
         uint32_t ent = __builtin_amdgcn_readfirstlane(ent_l);
+        auto dst_of = [](uint32_t en) { return (en >> 31) ? 0u : (uint32_t)MT_HALF; };
         twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
-                                    ((ent >> 31) ? MT_N : 0)), t);
+                                    mt_prev_gen(dst_of(ent))), t);
         for (int e2 = 0; e2 < cnt; ++e2) {
           const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
-          const uint32_t src = (ent >> 31) ? (uint32_t)MT_N : 0u;
+          const uint32_t dst = dst_of(ent);
           TwistIn u = t;
           if (e2 + 1 < cnt) {
             ent = __builtin_amdgcn_readlane(ent_l, e2 + 1);
             twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
-                                        ((ent >> 31) ? MT_N : 0)), t);
+                                        mt_prev_gen(dst_of(ent))), t);
           }
-          twist_store(u, (glb_u32*)(S.mt + env * MT_WORDS + (MT_N - src)),
-                      S.mc + env * MT_CODES + (MT_N - src) / 2, (lds_u32*)wscr);
+          twist_chain(u, (glb_u32*)(S.mt + env * MT_WORDS + dst), S.mc + env * MT_CODES + dst / 2,
+                      MT_HALF_GENS, (lds_u32*)wscr);
         }
       }
     }
@@ -1651,8 +1706,8 @@ __global__ __launch_bounds__(BLOCK) void k_gather_mt(Soa S, int64_t first, int64
   const int64_t k = t / Q;
   const int q = (int)(t - k * Q);
   const int64_t i = first + k;
-  const uint32_t half = mt_half(S.st4[i].w & MT_POS_MASK);
-  const uint4* src = reinterpret_cast<const uint4*>(S.mt + i * MT_WORDS + half);
+  const uint32_t pos = S.st4[i].w & MT_POS_MASK;
+  const uint4* src = reinterpret_cast<const uint4*>(S.mt + i * MT_WORDS + (pos - pos % MT_N));
   reinterpret_cast<uint4*>(dst)[t] = src[q];
 }
 
@@ -1919,8 +1974,8 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   // seed -> generation 1 (first half) -> generation 2 (second half) -> the constructor's draws
   hipLaunchKernelGGL(k_create, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n,
                      seed_base + (uint64_t)global_offset, h->genrand);
-  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, (uint32_t)MT_N);
-  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, 0u);
+  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n,
+                     (uint32_t)(MT_WORDS - MT_N), 0u, 2 * MT_HALF_GENS);
   hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, h->L,
                      (const uint8_t*)nullptr, (double*)nullptr);
   hipError_t e = hipGetLastError();
@@ -2288,7 +2343,7 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   out->episodes_dropped = (int64_t)s[ST_EP_OVERFLOW];
   out->launches = out->steps / (h->n ? h->n : 1);
   out->kernel_ms = h->kernel_ms_done;
-  out->regens = (int64_t)s[ST_REGENS];
+  out->regens = (int64_t)s[ST_REGENS] * MT_HALF_GENS;  // halves -> generations
   out->wave_ticks = (int64_t)s[ST_WTICKS];
   out->timed_launches = h->timed_launches;
   out->run_ms = h->run_ms_done;
@@ -2335,7 +2390,7 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
   if (ang) HIP_TRY(hipMemcpy(ang, h->S.ang, sizeof(double2) * n, hipMemcpyDeviceToHost));
   if (ep) HIP_TRY(hipMemcpy(ep, h->S.ep, sizeof(int2) * n, hipMemcpyDeviceToHost));
   if (mt_pos) {
-    // CPython's index into the generation holding the position (MT_STALE: the OTHER half)
+    // CPython's index into the generation holding the position
     for (int64_t i = 0; i < n; ++i) mt_pos[i] = (st[(size_t)i].w & MT_POS_MASK) % MT_N;
   }
   if (mt) {
@@ -2386,8 +2441,8 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
     e.px = pos[2 * i], e.py = pos[2 * i + 1];
     e.f = flags[i];
     e.kx = objs[4 * i], e.ky = objs[4 * i + 1], e.gx = objs[4 * i + 2], e.gy = objs[4 * i + 3];
-    // the given generation goes to half 0, its successor to half 1 (fresh); index 624 is the
-    // start of the successor (CPython twists before its next draw)
+    // the given generation goes to the ring's first slot, its successors to the others
+    // (fresh); index 624 is the start of the successor (CPython twists before its next draw)
     e.mti = p;
     uint4 w;
     w.x = ((uint32_t)e.px & 0xFFFFu) | ((uint32_t)e.py << 16);
@@ -2405,7 +2460,8 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
   HIP_TRY(hipMemcpy2D(h->S.mt, sizeof(uint32_t) * MT_WORDS, mt, sizeof(uint32_t) * MT_N,
                       sizeof(uint32_t) * MT_N, (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_gen_codes, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n);
-  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, 0u);
+  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, 0u, (uint32_t)MT_N,
+                     2 * MT_HALF_GENS - 1);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipDeviceSynchronize());
   return TG_OK;

@@ -35,7 +35,7 @@ struct Soa {
   double2* ang;
   int2* ep;
   uint32_t* mt;   // [N][MT_WORDS]
-  uint8_t* mc;    // [N][MT_CODES]: the draw codes of both generations (tg_core.h draw_code)
+  uint8_t* mc;    // [N][MT_CODES]: the draw codes of the ring's generations (tg_core.h draw_code)
 };
 
 // tg_step1's result row (one env)

@@ -88,7 +88,7 @@ struct Env {
   uint32_t f;            // flags above
   int kx, ky, gx, gy;    // key / goldcoin cell (OB/:34-38)
   double ang0, ang1;     // handle angles (OB/:111-114)
-  uint32_t mti;          // MT state word: position (0..1246, even) | MT_STALE (see Rng)
+  uint32_t mti;          // MT state word: position ([0, MT_WORDS), even) | MT_STALE (see Rng)
 };
 
 TG_HD int floordiv(int a, int b) {  // Python // for b > 0
@@ -114,23 +114,35 @@ TG_HD int div48(int v) { return (int)(mul24((uint32_t)v, 21846u) >> 20); }  // 0
 TG_HD int floordiv48(int a) { return div48(a + 16 * S) - 16; }              // -768 <= a < 31,900
 
 // ==========================================================================================
-// CPython random over two pre-twisted generations.
+// CPython random over a ring of pre-twisted generations.
 //   CPython (_randommodule.c genrand_uint32) regenerates all 624 words at once ("twist")
 //   whenever its index reaches 624, then tempers one word per call; random() takes two.
-//   Here each env keeps TWO consecutive generations, words [0, 624) and [624, 1248), and a
-//   position pos in [0, 1248) (always even: random() is the only consumer).  Consumption only
-//   reads: the half holding pos is CPython's mt[] with index pos % 624, and the other half is
-//   always the NEXT generation, so crossing 624 / 1248 continues the stream without a twist.
-//   The half a lane has left is stale (two generations behind) until it is regenerated
-//   (twist_gen of the one the lane is in); the env's state word carries MT_STALE meanwhile.
-//   The kernels regenerate it later, a whole wavefront per env, coalesced (tg_amd.hip
-//   wave_refill: the next step's classify pass, or after the launch).  A launch that would
-//   enter a stale half (> 312 draws since the refill) regenerates it first, per lane.
-//   Seeding (init_by_array) fills one half; two twists then give generations 1 and 2, pos 0.
+//   Here each env keeps a ring of 2 x MT_HALF_GENS consecutive generations, two halves of
+//   MT_HALF_GENS generations each (words [0, MT_HALF) and [MT_HALF, MT_WORDS)), and a position
+//   pos in [0, MT_WORDS) (always even: random() is the only consumer).  Consumption only
+//   reads: the generation holding pos is CPython's mt[] with index pos % 624, and the ring
+//   always holds the NEXT generations after it, so crossing a generation or half boundary
+//   continues the stream without a twist.
+//   The half a lane has left is stale (2 x MT_HALF_GENS generations behind) until it is
+//   regenerated: MT_HALF_GENS twists in sequence from the last generation of the half the
+//   lane is in (twist_half); the env's state word carries MT_STALE meanwhile.  The kernels
+//   regenerate it later, a whole wavefront per env, coalesced, the chained twists in LDS
+//   (tg_amd.hip wave_twist_gens: k_run's refill queue, k_reset, k_rollout).  A launch that
+//   would enter a stale half (> MT_HALF draws since the refill) regenerates it first, per
+//   lane.  Seeding (init_by_array) fills the ring's last generation; 2 x MT_HALF_GENS twists
+//   then give generations 1 .. 2 x MT_HALF_GENS, pos 0 (init_mt).
+//   Why a ring of 4 + 4: a half's regeneration reads one generation (its
+//   source) and writes MT_HALF_GENS of them, 3,432 B per generation instead of the 5,304 of
+//   a two-generation ring whose every twist re-reads its source from HBM
+//   (scripts/calib/twist_bench.hip: 1,013-1,050 vs 827-881 generations per us), and the
+//   refill list is a quarter as long.  20 KB of words + 2.5 KB of codes per env.
 // ==========================================================================================
-constexpr int MT_WORDS = 2 * MT_N;  // per env
+constexpr int MT_HALF_GENS = 4;                // generations per half
+constexpr int MT_HALF = MT_HALF_GENS * MT_N;   // words per half
+constexpr int MT_WORDS = 2 * MT_HALF;          // per env
 constexpr uint32_t MT_STALE = 1u << 31;   // state word: the half not holding pos is stale
 constexpr uint32_t MT_POS_MASK = 0xFFFFu;
+static_assert(MT_WORDS <= (int)MT_POS_MASK, "positions fit the state word");
 constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu;
 
 TG_HD uint32_t mt_twist(uint32_t a, uint32_t b, uint32_t c) {
@@ -156,7 +168,10 @@ TG_HD void twist_gen(const uint32_t* src, uint32_t* dst) {
     dst[p] = mt_twist(src[p], src[p + 1], dst[p - (MT_N - MT_M)]);
   dst[MT_N - 1] = mt_twist(src[MT_N - 1], dst[0], dst[MT_M - 1]);
 }
-TG_HD uint32_t mt_half(uint32_t pos) { return pos >= (uint32_t)MT_N ? (uint32_t)MT_N : 0u; }
+// word offset of the half holding word position pos
+TG_HD uint32_t mt_half(uint32_t pos) { return pos >= (uint32_t)MT_HALF ? (uint32_t)MT_HALF : 0u; }
+// word offset of the generation before the one at word offset g (ring order)
+TG_HD uint32_t mt_prev_gen(uint32_t g) { return (g == 0u ? (uint32_t)MT_WORDS : g) - (uint32_t)MT_N; }
 
 // ---- draw codes ------------------------------------------------------------------------------
 // Every random() value the option loops consume decides one of four things, each a comparison
@@ -167,9 +182,10 @@ TG_HD uint32_t mt_half(uint32_t pos) { return pos >= (uint32_t)MT_N ? (uint32_t)
 //   handle.flip (OB/:117-122):     uniform(0, 1) <= 0.8  (== r exactly)
 // so each generation is stored twice: its 624 words (for the next twist and for the rare
 // draws that need the double itself: handle angles, the reset's gauss) and one code byte per
-// draw (MT_CODES per env, half h at h / 2) holding those four outcomes.  Whoever regenerates
-// a half writes both.  Tick loops read bytes (16 draws per 16-B load) and do no f64 work.
-constexpr int MT_CODES = MT_N;  // 2 x 312 draws
+// draw (MT_CODES per env, the generation at word offset g at g / 2) holding those four
+// outcomes.  Whoever regenerates a half writes both.  Tick loops read bytes (16 draws per 16-B
+// load) and do no f64 work.
+constexpr int MT_CODES = MT_WORDS / 2;  // one per random() draw of the ring
 constexpr uint32_t CODE_POS = 3u;        // rint(2 + 2r) - 2
 constexpr uint32_t CODE_NEG_SHIFT = 2;   // rint(-4 + 2r) + 4, bits 2-3
 constexpr uint32_t CODE_JUMP = 1u << 4;  // r > 0.25
@@ -185,6 +201,15 @@ TG_HD int code_step(uint32_t c, bool neg) {
 }
 TG_HD void gen_codes(const uint32_t* words, uint8_t* c) {
   for (int k = 0; k < MT_N / 2; ++k) c[k] = (uint8_t)draw_code(mt_double(words[2 * k], words[2 * k + 1]));
+}
+// regenerate half h (word offset 0 / MT_HALF): its generations in sequence from the one before
+// it (the other half's last), words and, with mc, codes (per-lane form of wave_twist_gens)
+TG_HD void twist_half(uint32_t* mt, uint32_t h, uint8_t* mc = nullptr) {
+  for (int g = 0; g < MT_HALF_GENS; ++g) {
+    const uint32_t dst = h + (uint32_t)(g * MT_N);
+    twist_gen(mt + mt_prev_gen(dst), mt + dst);
+    if (mc) gen_codes(mt + dst, mc + dst / 2);
+  }
 }
 
 // Plain ticks of a walk along one axis (the go / ladder loops' plain phases, run_option_k):
@@ -219,13 +244,10 @@ struct Rng {
     const uint32_t w0 = mt[pos], w1 = mt[pos + 1];
     pos += 2;
     if (pos == (uint32_t)MT_WORDS) pos = 0u;
-    if (pos == 0u || pos == (uint32_t)MT_N) {
-      // entering the other half; a second crossing in one launch finds it stale (two
-      // generations behind): regenerate it from the half just left before reading it
-      if (crossed) {
-        twist_gen(mt + (MT_N - pos), mt + pos);
-        if (mc) gen_codes(mt + pos, mc + pos / 2);
-      }
+    if (pos == 0u || pos == (uint32_t)MT_HALF) {
+      // entering the other half; a second crossing in one launch finds it stale (a whole ring
+      // behind): regenerate it from the half just left before reading it
+      if (crossed) twist_half(mt, pos, mc);
       crossed = entered = true;
     }
     ++draws;
@@ -250,11 +272,7 @@ struct Rng {
 // regenerate the stale half (per-lane form of wave_refill); returns the clean state word
 TG_HD uint32_t refill_after(uint32_t* mt, uint32_t state, uint8_t* mc = nullptr) {
   const uint32_t pos = state & MT_POS_MASK;
-  if (state & MT_STALE) {
-    const uint32_t dst = MT_N - mt_half(pos);
-    twist_gen(mt + mt_half(pos), mt + dst);
-    if (mc) gen_codes(mt + dst, mc + dst / 2);
-  }
+  if (state & MT_STALE) twist_half(mt, (uint32_t)MT_HALF - mt_half(pos), mc);
   return pos;
 }
 
@@ -289,6 +307,14 @@ TG_HD void seed_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed)
     if (i >= (uint32_t)MT_N) { mt[0] = mt[MT_N - 1]; prev = mt[0]; i = 1; }
   }
   mt[0] = 0x80000000u;
+}
+// random.seed(seed) into an env's ring (per-lane form of tg_create: k_create + k_gen_twist):
+// the seeded words in the last generation's slot, then the ring's generations, pos 0
+TG_HD void init_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed,
+                   uint8_t* mc = nullptr) {
+  seed_mt(mt + MT_WORDS - MT_N, genrand19650218, seed);
+  twist_half(mt, 0u, mc);
+  twist_half(mt, (uint32_t)MT_HALF, mc);
 }
 
 // ==========================================================================================

@@ -12,6 +12,8 @@
 //   F  E writing every generation's words (a ring of 2G generations per env: no reconstruction
 //      for the draws that need the double), HBM bytes (2,496 / G + 2,496 + 312) per generation
 //   G  F with the draw codes from integer thresholds on the 53-bit draw (no f64 work)
+//   H  E with the integer codes
+//   I  C with the integer codes (one twist per source load, as k_run's refill queue)
 // Prints one JSON line: twists per microsecond and the HBM bytes rate (5,304 B per twist).
 #include <hip/hip_runtime.h>
 
@@ -81,6 +83,27 @@ __device__ __forceinline__ void store_regs(const Regs& t, uint32_t* dst, uint8_t
   }
   codes_out(nw, dst_c);
 }
+struct Thr {
+  uint64_t p1, p2, n1, n2, j, f;
+};
+__constant__ Thr kThr;
+__device__ __forceinline__ uint32_t code_int(uint32_t w0, uint32_t w1) {
+  const uint64_t k = ((uint64_t)(mt_temper(w0) >> 5) << 26) | (mt_temper(w1) >> 6);
+  const uint32_t pos = (uint32_t)(k >= kThr.p1) + (uint32_t)(k >= kThr.p2);
+  const uint32_t neg = (uint32_t)(k >= kThr.n1) + (uint32_t)(k >= kThr.n2);
+  return pos | (neg << CODE_NEG_SHIFT) | (k >= kThr.j ? CODE_JUMP : 0u) | (k < kThr.f ? CODE_FLIP : 0u);
+}
+__device__ __forceinline__ void codes_int(lds_u32* nw, uint8_t* dst_c) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
+    const int d = r * 64 + lane;
+    if (d < MT_N / 2) {
+      const lds_u32* w = nw + 2 * d;
+      dst_c[d] = (uint8_t)code_int(w[0], w[1]);
+    }
+  }
+}
 // the source generation into LDS: 156 x 16 B chunks, lane l takes chunks l, l + 64, l + 128
 __device__ __forceinline__ void dma_src(const uint32_t* src, lds_u32* s) {
   const int lane = threadIdx.x & 63;
@@ -103,6 +126,7 @@ __device__ __forceinline__ void dma_src(const uint32_t* src, lds_u32* s) {
     }
   }
 }
+template <bool INT = false>
 __device__ __forceinline__ void store_lds(const lds_u32* s, uint32_t* dst, uint8_t* dst_c, lds_u32* nw) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -118,30 +142,9 @@ __device__ __forceinline__ void store_lds(const lds_u32* s, uint32_t* dst, uint8
     }
     wave_fence();
   }
-  codes_out(nw, dst_c);
+  if (INT) codes_int(nw, dst_c); else codes_out(nw, dst_c);
 }
 
-struct Thr {
-  uint64_t p1, p2, n1, n2, j, f;
-};
-__constant__ Thr kThr;
-__device__ __forceinline__ uint32_t code_int(uint32_t w0, uint32_t w1) {
-  const uint64_t k = ((uint64_t)(mt_temper(w0) >> 5) << 26) | (mt_temper(w1) >> 6);
-  const uint32_t pos = (uint32_t)(k >= kThr.p1) + (uint32_t)(k >= kThr.p2);
-  const uint32_t neg = (uint32_t)(k >= kThr.n1) + (uint32_t)(k >= kThr.n2);
-  return pos | (neg << CODE_NEG_SHIFT) | (k >= kThr.j ? CODE_JUMP : 0u) | (k < kThr.f ? CODE_FLIP : 0u);
-}
-__device__ __forceinline__ void codes_int(lds_u32* nw, uint8_t* dst_c) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
-    const int d = r * 64 + lane;
-    if (d < MT_N / 2) {
-      const lds_u32* w = nw + 2 * d;
-      dst_c[d] = (uint8_t)code_int(w[0], w[1]);
-    }
-  }
-}
 // G twists chained in LDS from the source in s: codes of every generation, words of the last
 // only (ALL = false) or of every generation (ALL: dst + g * MT_N)
 template <int G, bool ALL = false, bool INT = false>
@@ -236,6 +239,22 @@ __global__ __launch_bounds__(BLOCK) void k_twist(Job J) {
       dma_src(src, base);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       chain_lds<4>(base, base + MT_N, dst, J.mc4 + (uint64_t)(J.ent[j] & 0x7FFFFFFFu) * (4 * MT_N / 2));
+    }
+  } else if constexpr (V == 7) {
+    for (int j = w; j < J.n; j += nw) {
+      job_ptrs(J, J.ent[j], src, dst, dc);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      dma_src(src, base);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      chain_lds<4, false, true>(base, base + MT_N, dst, J.mc4 + (uint64_t)(J.ent[j] & 0x7FFFFFFFu) * (4 * MT_N / 2));
+    }
+  } else if constexpr (V == 8) {
+    for (int j = w; j < J.n; j += nw) {
+      job_ptrs(J, J.ent[j], src, dst, dc);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      dma_src(src, base);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_lds<true>(base, dst, dc, base + MT_N);
     }
   } else if constexpr (V == 5 || V == 6) {
     for (int j = w; j < J.n; j += nw) {
@@ -342,7 +361,7 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreate(&b));
   std::vector<uint32_t> ref_w, ref_c, ref4_w, ref4_c;
   printf("{\"jobs\": %d, \"grid\": %d, \"variants\": {", njobs, grid);
-  for (int v = 0; v < 7; ++v) {
+  for (int v = 0; v < 9; ++v) {
     float best = 1e30f;
     for (int rep = 0; rep < 5; ++rep) {
       // jobs name distinct envs and read one half, write the other: every run sees the same input
@@ -354,6 +373,8 @@ int main(int argc, char** argv) {
       if (v == 4) hipLaunchKernelGGL(k_twist<4>, dim3(grid), dim3(BLOCK), 0, 0, J);
       if (v == 5) hipLaunchKernelGGL(k_twist<5>, dim3(grid), dim3(BLOCK), 0, 0, J);
       if (v == 6) hipLaunchKernelGGL(k_twist<6>, dim3(grid), dim3(BLOCK), 0, 0, J);
+      if (v == 7) hipLaunchKernelGGL(k_twist<7>, dim3(grid), dim3(BLOCK), 0, 0, J);
+      if (v == 8) hipLaunchKernelGGL(k_twist<8>, dim3(grid), dim3(BLOCK), 0, 0, J);
       CHECK(hipEventRecord(b));
       CHECK(hipEventSynchronize(b));
       float ms = 0;
@@ -366,20 +387,21 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(c.data(), mc, c.size() * 4, hipMemcpyDeviceToHost));
     bool same = true;
     if (v == 0) ref_w = w, ref_c = c;
-    else if (v < 4) same = (w == ref_w) && (c == ref_c);
+    else if (v < 4 || v == 8) same = (w == ref_w) && (c == ref_c);
     std::vector<uint32_t> w4(envs * 4 * MT_N / 64), c4(envs * 4 * MT_N / 2 / 64 / 4);
-    if (v >= 5) {
+    if (v >= 5 && v <= 6) {
       CHECK(hipMemcpy(w4.data(), mt4, w4.size() * 4, hipMemcpyDeviceToHost));
       CHECK(hipMemcpy(c4.data(), mc4, c4.size() * 4, hipMemcpyDeviceToHost));
       if (v == 5) ref4_w = w4, ref4_c = c4;
       else same = (w4 == ref4_w) && (c4 == ref4_c);
     }
     const double us = best * 1e3;
-    const int gens = v >= 4 ? 4 : 1;
-    const double bytes = v == 4 ? 2 * 2496.0 + 4 * 312.0 : v >= 5 ? 5 * 2496.0 + 4 * 312.0 : 5304.0;
+    const int gens = v >= 4 && v <= 7 ? 4 : 1;
+    const double bytes = v == 4 || v == 7 ? 2 * 2496.0 + 4 * 312.0
+                         : v == 5 || v == 6 ? 5 * 2496.0 + 4 * 312.0 : 5304.0;
     printf("%s\"%c\": {\"ms\": %.4f, \"twists_per_us\": %.1f, \"GBps\": %.0f, \"same_as_A\": %s}",
            v ? ", " : "", 'A' + v, best, njobs * gens / us, njobs * bytes / us / 1e3,
-           v == 4 || v == 5 ? "null" : same ? "true" : "false");
+           v == 4 || v == 5 || v == 7 ? "null" : same ? "true" : "false");
   }
   printf("}}\n");
   return 0;

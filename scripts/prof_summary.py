@@ -15,7 +15,7 @@ the rest of FETCH_SIZE at face value:
     hbm_read = coalesced + (FETCH_SIZE - coalesced / 2)
 k_classify's reads are all coalesced (env-order loads); k_run's coalesced reads are the
 worklist rows (44 B per valid env) and the twist sources (2,496 B + a 4-B list entry per
-regenerated half); its scattered reads are the code-window LDS-DMA fills.  The k_errors factor
+regenerated half of 4 generations); its scattered reads are the code-window LDS-DMA fills.  The k_errors factor
 (the round-2 method, 2.0 for its coalesced 16-B reads) is kept beside it as a cross-check.
 """
 import argparse
@@ -112,10 +112,10 @@ def main():
             base = k.split("<")[0]
             if base == "k_classify":
                 coal = 44.0 * a.envs
-            elif base == "k_run":
-                coal = 44.0 * valid + 2500.0 * regens
+            elif base == "k_run":  # regens: generations; one source read per half of G = 4
+                coal = 44.0 * valid + 2500.0 / 4 * regens
             else:  # k_step: env-order state loads + the refills' sources
-                coal = 44.0 * a.envs + 2496.0 * regens
+                coal = 44.0 * a.envs + 2496.0 / 4 * regens
             scat = max(fr - coal / 2.0, 0.0)
             rd = coal + scat
             kn = ks.get(k, {}).get("avg_ns")

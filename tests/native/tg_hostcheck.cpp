@@ -75,9 +75,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
   std::vector<uint32_t> mt(MT_WORDS);
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t g = (uint64_t)(g0 + i);
-    seed_mt(mt.data() + MT_N, gen, seed_base + g);  // k_create, then k_gen_twist x2
-    twist_gen(mt.data() + MT_N, mt.data());
-    twist_gen(mt.data(), mt.data() + MT_N);
+    init_mt(mt.data(), gen, seed_base + g);  // k_create + k_gen_twist
     Env e{};
     int64_t ndraws = 0;
     {  // construct + reset, each a separate launch on the device (k_reset)
@@ -146,9 +144,7 @@ int hc_rng_stream(uint64_t seed, const int32_t* launches, int nl, int defer, dou
   gen[0] = 19650218u;
   for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
   std::vector<uint32_t> mt(MT_WORDS);
-  seed_mt(mt.data() + MT_N, gen, seed);
-  twist_gen(mt.data() + MT_N, mt.data());
-  twist_gen(mt.data(), mt.data() + MT_N);
+  init_mt(mt.data(), gen, seed);
   uint32_t state = 0;
   int64_t k = 0;
   for (int j = 0; j < nl; ++j) {
@@ -225,9 +221,7 @@ int hc_render_run(const char* dom, const char* objs, const char* inter, uint64_t
   const size_t fb = (size_t)A.Hpx * A.Wpx * 3;
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t g = (uint64_t)envs[i];
-    seed_mt(mt.data() + MT_N, gen, seed_base + g);
-    twist_gen(mt.data() + MT_N, mt.data());
-    twist_gen(mt.data(), mt.data() + MT_N);
+    init_mt(mt.data(), gen, seed_base + g);
     Env e{};
     for (int r = 0; r < 2; ++r) {  // construct + reset
       Rng rng(mt.data(), e.mti);
