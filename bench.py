@@ -61,14 +61,14 @@ EP_CAP = 4096          # episode records gathered per rank per step of a drain i
 #   k_classify, every env: action 4 + state word 16 + angles 16 + episode 8 read (44)
 #     reward-None env: episode 8 + obs 72 + reward/valid/done 6 written (86)
 #     valid env: worklist index 4 + state 16 + angles 16 + episode 8 written (44)
-#     stale MT half: its refill-list entry 4 written (1 per generation: a half is 4)
+#     stale MT half: its refill-list entry 4 written (a half is MT_HALF_GENS generations)
 #   k_run, valid env: the worklist row 44 read; state 16 + angles 16 + episode 8 + obs 72 +
 #     rows 6 written (118); random() draw: its 1-B code (tg_core.h draw_code); MT generation
-#     regenerated (tg_core.h: halves of MT_HALF_GENS = 4 generations, chained in LDS): 624
-#     words + 312 codes written, a quarter of the source generation's 624 words and of the
+#     regenerated (tg_core.h: halves of MT_HALF_GENS = 8 generations, chained in LDS): 624
+#     words + 312 codes written, an eighth of the source generation's 624 words and of the
 #     4-B refill entry read
 #   k_step (direct mode): one kernel, the same without the worklist round trip
-MT_HALF_GENS = 4
+MT_HALF_GENS = 8
 CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 86, 44, 4 / MT_HALF_GENS
 RUN_VALID, RUN_DRAW = 162, 1
 RUN_REGEN = 2496 + 312 + (2496 + 4) / MT_HALF_GENS
@@ -135,6 +135,8 @@ def parse(argv=None):
                     help="per-step API: drain and gather the completed episodes every G steps "
                          "(SURVEY §8e: batched gather; 1 = every step); --rollout K drains "
                          "every K steps")
+    ap.add_argument("--progress", action="store_true",
+                    help="a line on stderr every 500 untimed steps (profiler runs)")
     ap.add_argument("--timing-every", type=int, default=8,
                     help="HIP-event timing of every k-th timed step (its kernels' durations for "
                          "the roofline); an event record between kernels costs the stream ~5 us")
@@ -400,6 +402,9 @@ class Runner:
             self.render_on = j < warmup  # c5: the burn-in only advances the envs
             self.step(t)
             t += 1
+            if self.args.progress and j % 500 == 499:
+                print("untimed step %d of %d" % (j + 1, warmup + burn_in), file=sys.stderr,
+                      flush=True)
         self.render_on = True
         if self.pre is not None:  # the timed steps' inputs, resident before timing
             self.pre_t0 = t

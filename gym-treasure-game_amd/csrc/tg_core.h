@@ -131,13 +131,14 @@ TG_HD int floordiv48(int a) { return div48(a + 16 * S) - 16; }              // -
 //   would enter a stale half (> MT_HALF draws since the refill) regenerates it first, per
 //   lane.  Seeding (init_by_array) fills the ring's last generation; 2 x MT_HALF_GENS twists
 //   then give generations 1 .. 2 x MT_HALF_GENS, pos 0 (init_mt).
-//   Why a ring of 4 + 4: a half's regeneration reads one generation (its
-//   source) and writes MT_HALF_GENS of them, 3,432 B per generation instead of the 5,304 of
-//   a two-generation ring whose every twist re-reads its source from HBM
-//   (scripts/calib/twist_bench.hip: 1,013-1,050 vs 827-881 generations per us), and the
-//   refill list is a quarter as long.  20 KB of words + 2.5 KB of codes per env.
+//   Why a ring of 8 + 8: a half's regeneration reads one generation (its
+//   source) and writes MT_HALF_GENS of them, 3,120 B per generation instead of the 5,304 of
+//   a two-generation ring whose every twist re-reads its source from HBM, and the refill
+//   list is an eighth as long (A/B, 1M envs: 2 + 2 / 4 + 4 / 8 + 8 per half: uniform 0.172 /
+//   0.168 / 0.164 ms, masked 0.399 / 0.391 / 0.368 ms per step; 1 + 1: 0.176 / 0.483).
+//   40 KB of words + 5 KB of codes per env.
 // ==========================================================================================
-constexpr int MT_HALF_GENS = 4;                // generations per half
+constexpr int MT_HALF_GENS = 8;                // generations per half
 constexpr int MT_HALF = MT_HALF_GENS * MT_N;   // words per half
 constexpr int MT_WORDS = 2 * MT_HALF;          // per env
 constexpr uint32_t MT_STALE = 1u << 31;   // state word: the half not holding pos is stale

@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# r03j: generations per ring half: 2 / 4 (product) / 8
+set -u
+OUT=gpurun_out
+mkdir -p $OUT
+cd "$GRAFT_REPO_ROOT"
+run() {
+  local name=$1 lim=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 3 "$OUT/$name.log" | cut -c1-300
+  if [ $rc -ne 0 ]; then echo "stop ($name rc=$rc)"; exit $rc; fi
+}
+export TG_LIB_PATH=$GRAFT_REPO_ROOT/gym-treasure-game_amd/libtg_amd_g8.so
+run pytest_g8 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py -m gpu
+unset TG_LIB_PATH
+VARIANTS="g2=gym-treasure-game_amd/libtg_amd_g2.so,g4=gym-treasure-game_amd/libtg_amd_ring.so,g8=gym-treasure-game_amd/libtg_amd_g8.so" ROUNDS=3 STEPS=50 run ab_g 900 python scripts/ab.py
+echo "== all done"

@@ -15,7 +15,8 @@ the rest of FETCH_SIZE at face value:
     hbm_read = coalesced + (FETCH_SIZE - coalesced / 2)
 k_classify's reads are all coalesced (env-order loads); k_run's coalesced reads are the
 worklist rows (44 B per valid env) and the twist sources (2,496 B + a 4-B list entry per
-regenerated half of 4 generations); its scattered reads are the code-window LDS-DMA fills.  The k_errors factor
+regenerated half of MT_HALF_GENS generations); its scattered reads are the code-window
+LDS-DMA fills.  The k_errors factor
 (the round-2 method, 2.0 for its coalesced 16-B reads) is kept beside it as a cross-check.
 """
 import argparse
@@ -26,6 +27,7 @@ import re
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MT_HALF_GENS = 8  # tg_core.h: generations per half of an env's MT ring
 
 
 def short(name):
@@ -73,6 +75,9 @@ def main():
     ap.add_argument("--envs", type=int, default=1 << 20)
     ap.add_argument("--policy", default="uniform")
     ap.add_argument("--mode", default="compact")
+    ap.add_argument("--dest", default=os.path.join(ROOT, "profiles"),
+                    help="where the summaries go (on a GPU box: under gpurun_out/, which is what "
+                         "comes back)")
     ap.add_argument("--render", action="store_true",
                     help="the C5 passes (<tag>c5): k_render -> profiles/traffic_render.json")
     a = ap.parse_args()
@@ -99,9 +104,9 @@ def main():
     # the step's kernels: k_classify + k_run (compact) or k_step (direct)
     names = (("k_classify", "k_run") if a.mode == "compact" else ("k_step",))
     step_k = [k for k in pm if k.split("<")[0] in names]
-    if step_k and "k_errors" in pm and all("FETCH_SIZE" in pm[k] for k in step_k):
+    if step_k and all("FETCH_SIZE" in pm[k] for k in step_k):
         known = 16.0 * a.envs  # k_errors: one 16-B uint4 per env, 16 B per lane
-        raw_err = pm["k_errors"]["FETCH_SIZE"] * 1024.0
+        raw_err = pm.get("k_errors", {}).get("FETCH_SIZE", 0.0) * 1024.0
         cal = known / raw_err if raw_err > 0 else None
         valid = (prof_line or {}).get("valid_step_frac", 0.0) * a.envs
         regens = (prof_line or {}).get("regens_per_step", 0.0)
@@ -112,10 +117,10 @@ def main():
             base = k.split("<")[0]
             if base == "k_classify":
                 coal = 44.0 * a.envs
-            elif base == "k_run":  # regens: generations; one source read per half of G = 4
-                coal = 44.0 * valid + 2500.0 / 4 * regens
+            elif base == "k_run":  # regens: generations; one source read per half
+                coal = 44.0 * valid + 2500.0 / MT_HALF_GENS * regens
             else:  # k_step: env-order state loads + the refills' sources
-                coal = 44.0 * a.envs + 2496.0 / 4 * regens
+                coal = 44.0 * a.envs + 2496.0 / MT_HALF_GENS * regens
             scat = max(fr - coal / 2.0, 0.0)
             rd = coal + scat
             kn = ks.get(k, {}).get("avg_ns")
@@ -153,8 +158,8 @@ def main():
                                      "coalesced reads reported at 1/2, scattered 8/16-B loads "
                                      "and LDS-DMA at one 64-B read each, writes 1:1",
                       "fetch_calibration_kerrors": cal,
-                      "kerrors_note": "k_errors reads %d B, FETCH_SIZE reported %.0f B" %
-                                      (known, raw_err)}
+                      "kerrors_note": ("k_errors reads %d B, FETCH_SIZE reported %.0f B" %
+                                       (known, raw_err)) if raw_err else "k_errors not profiled"}
         ns = sum(ks[k]["avg_ns"] for k in ks if k.split("<")[0] in names)
         res["step_kernels_avg_ns"] = ns
         # VALU issue utilisation of the step kernels: wave64 VALU instructions x 2 cycles
@@ -173,10 +178,11 @@ def main():
               "burn_in": prof_line.get("burn_in") if prof_line else None,
               "source": "profiles/%s_summary.json (rocprofv3 --pmc passes of bench.py %s)"
                         % (a.tag, "steps=%s" % last)}
-        with open(os.path.join(ROOT, "profiles", "traffic_step_%s.json" % a.policy), "w") as f:
+        os.makedirs(a.dest, exist_ok=True)
+        with open(os.path.join(a.dest, "traffic_step_%s.json" % a.policy), "w") as f:
             json.dump(tj, f, indent=1)
-    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "%s_summary.json" % a.tag), "w") as f:
+    os.makedirs(a.dest, exist_ok=True)
+    with open(os.path.join(a.dest, "%s_summary.json" % a.tag), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps({k: res[k] for k in res if k in ("hbm", "step_kernels_avg_ns")}, indent=1))
 
