@@ -377,45 +377,64 @@ __device__ __forceinline__ void twist_load(const glb_u32* src, TwistIn& t) {
     if (r < 4) t.c[r] = p < MT_N - MT_M ? src[p + MT_M] : 0u;
   }
 }
+// The rounds of a twist go in groups {0, 1, 2} {3, 4, 5} {6, 7, 8} {9}: round r reads new words
+// p - 227 written by rounds r - 4 and r - 3 only, so a group needs nothing from itself, and its
+// reads issue together (4 LDS round trips per generation instead of 10).
+constexpr int TWIST_GROUP = 3;
 __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint8_t* dst_c,
                                             lds_u32* scratch) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int r = 0; r < TwistIn::ROUNDS; ++r) {
-    const int p = r * 64 + lane;
-    if (p < MT_N) {
-      const uint32_t bb = p + 1 < MT_N ? t.b[r] : scratch[0];
-      const uint32_t cc = p < MT_N - MT_M ? t.c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
-      const uint32_t w = mt_twist(t.a[r], bb, cc);
-      scratch[p] = w;
-      dst[p] = w;
+  for (int r0 = 0; r0 < TwistIn::ROUNDS; r0 += TWIST_GROUP) {
+#pragma unroll
+    for (int r = r0; r < r0 + TWIST_GROUP && r < TwistIn::ROUNDS; ++r) {
+      const int p = r * 64 + lane;
+      if (p < MT_N) {
+        const uint32_t bb = p + 1 < MT_N ? t.b[r] : scratch[0];
+        const uint32_t cc = p < MT_N - MT_M ? t.c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
+        const uint32_t w = mt_twist(t.a[r], bb, cc);
+        scratch[p] = w;
+        dst[p] = w;
+      }
     }
-    // round r visible to later rounds, whose lanes read what other lanes wrote: a wavefront-scope
-    // fence orders the LDS accesses in the compiler (one wave's LDS operations execute in
-    // order), without the hardware wait for the store's completion (A/B against s_waitcnt
-    // lgkmcnt(0) after every round: 0.1322 vs 0.1340 ms)
+    // the group visible to later groups, whose lanes read what other lanes wrote: a
+    // wavefront-scope fence orders the LDS accesses in the compiler (one wave's LDS operations
+    // execute in order), without the hardware wait for the store's completion (A/B against
+    // s_waitcnt lgkmcnt(0) after every round: 0.1322 vs 0.1340 ms)
     wave_fence();
   }
   codes_from_lds(scratch, dst_c);
 }
 // The next generation in place in LDS (s: a generation -> its successor), stored to dst with
-// its codes.  Round r reads words p + 1 (old: written by round r + 1's lanes) and p + 397 (old
-// for p < 227: rounds >= 6 write them) or p - 227 (new: >= 3 rounds earlier) and then writes
-// p; a lane's store depends on its three reads, and the wave's reads of a round precede its
-// writes (one wave's LDS operations execute in order).  Must be reached by all 64 lanes.
+// its codes.  Round r reads words p + 1 (old: round r + 1 writes it, for lane 63), p + 397
+// (old for p < 227: rounds >= 6 write them) or p - 227 (new: rounds r - 4 / r - 3), then
+// writes p.  A group's reads are all issued before its writes (the compiler barrier: one
+// wave's LDS operations execute in order), so round r + 1's write cannot overtake round r's
+// read of word 64 (r + 1).  Must be reached by all 64 lanes.
 __device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst_c) {
   const int lane = threadIdx.x & 63;
   wave_fence();  // the previous codes pass's reads of s before this twist's writes
 #pragma unroll
-  for (int r = 0; r < TwistIn::ROUNDS; ++r) {
-    const int p = r * 64 + lane;
-    if (p < MT_N) {
-      const uint32_t a = s[p];
-      const uint32_t b = s[p + 1 < MT_N ? p + 1 : 0];
-      const uint32_t c = s[p < MT_N - MT_M ? p + MT_M : p - (MT_N - MT_M)];
-      const uint32_t w = mt_twist(a, b, c);
-      s[p] = w;
-      dst[p] = w;
+  for (int r0 = 0; r0 < TwistIn::ROUNDS; r0 += TWIST_GROUP) {
+    uint32_t w[TWIST_GROUP];
+#pragma unroll
+    for (int r = r0; r < r0 + TWIST_GROUP && r < TwistIn::ROUNDS; ++r) {
+      const int p = r * 64 + lane;
+      if (p < MT_N) {
+        const uint32_t a = s[p];
+        const uint32_t b = s[p + 1 < MT_N ? p + 1 : 0];
+        const uint32_t c = s[p < MT_N - MT_M ? p + MT_M : p - (MT_N - MT_M)];
+        w[r - r0] = mt_twist(a, b, c);
+      }
+    }
+    asm volatile("" ::: "memory");  // the group's reads before its writes, in program order
+#pragma unroll
+    for (int r = r0; r < r0 + TWIST_GROUP && r < TwistIn::ROUNDS; ++r) {
+      const int p = r * 64 + lane;
+      if (p < MT_N) {
+        s[p] = w[r - r0];
+        dst[p] = w[r - r0];
+      }
     }
     wave_fence();
   }
@@ -944,10 +963,11 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
 
 #ifdef TG_DIAG_STAMPS
 // DIAGNOSTIC BUILD ONLY (scripts/diag_stamps.py): per-wave s_memtime stamps of k_run
-constexpr int NSTAMP = 10;
+constexpr int NSTAMP = 11;
 // per wave: 4 durations/counts, 100 MHz start and end, the option loop's phases (walk, refill,
 // full tick: lane 0's sums) and rounds
-__device__ unsigned long long g_stamps[(1 << 16) * NSTAMP];
+constexpr int NSTAMP_WAVES = 1 << 17;
+__device__ unsigned long long g_stamps[NSTAMP_WAVES * NSTAMP];
 #define TG_STAMP(v) v = __builtin_amdgcn_s_memtime()
 #else
 #define TG_STAMP(v) (void)0
@@ -1135,18 +1155,21 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     const unsigned long long p1 = __shfl(ph1, lmax, 64), p2 = __shfl(ph2, lmax, 64),
                              p3 = __shfl(ph3, lmax, 64);
     const uint32_t pr = __shfl(prounds, lmax, 64);
-    if ((threadIdx.x & 63) == 0 && bl && wv < (1 << 16)) {
+    if ((threadIdx.x & 63) == 0 && wv < NSTAMP_WAVES) {
       unsigned long long* const g = g_stamps + (size_t)wv * NSTAMP;
-      g[0] = a1 - t0;
-      g[1] = a2 - a1;
-      g[2] = t3 - a2;
-      g[3] = (unsigned long long)mx | ((unsigned long long)sum << 32) | ((unsigned long long)k << 56);
+      // an idle wave (no option: the refill queue only) is option 15 with 1 iteration
+      g[0] = bl ? a1 - t0 : 0;
+      g[1] = bl ? a2 - a1 : 0;
+      g[2] = bl ? t3 - a2 : t3 - t0;
+      g[3] = bl ? (unsigned long long)mx | ((unsigned long long)sum << 32) | ((unsigned long long)k << 56)
+                : 1ull | (15ull << 56);
       g[4] = rt0;
       g[5] = rt3;
       g[6] = p1;
       g[7] = p2;
       g[8] = p3;
       g[9] = pr;
+      g[10] = (unsigned long long)regens;  // halves this wave regenerated from the queue
     }
   }
 #endif
@@ -2469,7 +2492,7 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
 
 #ifdef TG_DIAG_STAMPS
 int tg_diag_stamps(unsigned long long* out, int n_waves) {
-  if (n_waves > (1 << 16)) n_waves = 1 << 16;
+  if (n_waves > NSTAMP_WAVES) n_waves = NSTAMP_WAVES;
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * NSTAMP * n_waves));
   return TG_OK;

@@ -14,11 +14,17 @@
 //   G  F with the draw codes from integer thresholds on the 53-bit draw (no f64 work)
 //   H  E with the integer codes
 //   I  C with the integer codes (one twist per source load, as k_run's refill queue)
+//   J  a half of 8 generations per job, twisted in place in one LDS buffer, every generation's
+//      words and codes stored (the product's twist_chain, source by LDS-DMA)
+//   K  J with TWO jobs per wave, their rounds interleaved (two independent dependency chains)
+//   L  J with the rounds in groups {0,1,2} {3,4,5} {6,7,8} {9} (the product's twist_lds)
+//   M  L without the draw-code pass;  N  L without the global stores (latency anatomy)
 // Prints one JSON line: twists per microsecond and the HBM bytes rate (5,304 B per twist).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #include "../../gym-treasure-game_amd/csrc/tg_core.h"
@@ -172,11 +178,93 @@ __device__ __forceinline__ void chain_lds(lds_u32* s, lds_u32* t, uint32_t* dst,
   }
 }
 
+// in-place successor of the generation in s (the product's twist_lds), words + codes stored
+__device__ __forceinline__ void inplace_round(lds_u32* s, int r, uint32_t* dst) {
+  const int lane = threadIdx.x & 63;
+  const int p = r * 64 + lane;
+  if (p < MT_N) {
+    const uint32_t a = s[p];
+    const uint32_t b = s[p + 1 < MT_N ? p + 1 : 0];
+    const uint32_t c = s[p < MT_N - MT_M ? p + MT_M : p - (MT_N - MT_M)];
+    const uint32_t w = mt_twist(a, b, c);
+    s[p] = w;
+    dst[p] = w;
+  }
+}
+template <int G>
+__device__ __forceinline__ void chain1(lds_u32* s, uint32_t* dst, uint8_t* dst_c) {
+#pragma unroll 1
+  for (int g = 0; g < G; ++g) {
+    wave_fence();
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+      inplace_round(s, r, dst + g * MT_N);
+      wave_fence();
+    }
+    codes_out(s, dst_c + g * (MT_N / 2));
+  }
+}
+template <int G>
+__device__ __forceinline__ void chain2(lds_u32* s, uint32_t* dst, uint8_t* dst_c, lds_u32* s2, uint32_t* dst2,
+                                       uint8_t* dst_c2) {
+#pragma unroll 1
+  for (int g = 0; g < G; ++g) {
+    wave_fence();
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+      inplace_round(s, r, dst + g * MT_N);
+      inplace_round(s2, r, dst2 + g * MT_N);
+      wave_fence();
+    }
+    codes_out(s, dst_c + g * (MT_N / 2));
+    codes_out(s2, dst_c2 + g * (MT_N / 2));
+  }
+}
+
+// the product's grouped in-place twist (tg_amd.hip twist_lds), with parts switched off
+template <bool CODES, bool STORES>
+__device__ __forceinline__ void inplace_grouped(lds_u32* s, uint32_t* dst, uint8_t* dst_c) {
+  const int lane = threadIdx.x & 63;
+  wave_fence();
+#pragma unroll
+  for (int r0 = 0; r0 < ROUNDS; r0 += 3) {
+    uint32_t w[3];
+#pragma unroll
+    for (int r = r0; r < r0 + 3 && r < ROUNDS; ++r) {
+      const int p = r * 64 + lane;
+      if (p < MT_N) {
+        const uint32_t a = s[p];
+        const uint32_t b = s[p + 1 < MT_N ? p + 1 : 0];
+        const uint32_t c = s[p < MT_N - MT_M ? p + MT_M : p - (MT_N - MT_M)];
+        w[r - r0] = mt_twist(a, b, c);
+      }
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int r = r0; r < r0 + 3 && r < ROUNDS; ++r) {
+      const int p = r * 64 + lane;
+      if (p < MT_N) {
+        s[p] = w[r - r0];
+        if (STORES) dst[p] = w[r - r0];
+      }
+    }
+    wave_fence();
+  }
+  if (CODES) codes_out(s, dst_c);
+}
+template <int G, bool CODES, bool STORES>
+__device__ __forceinline__ void chain_g(lds_u32* s, uint32_t* dst, uint8_t* dst_c) {
+#pragma unroll 1
+  for (int g = 0; g < G; ++g) inplace_grouped<CODES, STORES>(s, dst + g * MT_N, dst_c + g * (MT_N / 2));
+}
+
 struct Job {
   uint32_t* mt;   // [envs][1248]
   uint8_t* mc;    // [envs][624]
   uint8_t* mc4;   // [envs][4 * 312] (variants E-G)
   uint32_t* mt4;  // [envs][4 * 624] (variants F, G)
+  uint32_t* mt8;  // [envs][8 * 624] (variants J, K)
+  uint8_t* mc8;   // [envs][8 * 312]
   const uint32_t* ent;  // env | src half << 31
   int n;
 };
@@ -256,6 +344,43 @@ __global__ __launch_bounds__(BLOCK) void k_twist(Job J) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       store_lds<true>(base, dst, dc, base + MT_N);
     }
+  } else if constexpr (V == 9) {
+    for (int j = w; j < J.n; j += nw) {
+      job_ptrs(J, J.ent[j], src, dst, dc);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      dma_src(src, base);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t env = J.ent[j] & 0x7FFFFFFFu;
+      chain1<8>(base, J.mt8 + env * (8 * MT_N), J.mc8 + env * (8 * MT_N / 2));
+    }
+  } else if constexpr (V == 10) {
+    for (int j = 2 * w; j < J.n; j += 2 * nw) {
+      const uint32_t *src2;
+      uint32_t* dst2;
+      uint8_t* dc2;
+      const bool two = j + 1 < J.n;
+      job_ptrs(J, J.ent[j], src, dst, dc);
+      job_ptrs(J, J.ent[two ? j + 1 : j], src2, dst2, dc2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      dma_src(src, base);
+      dma_src(src2, base + MT_N);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t env = J.ent[j] & 0x7FFFFFFFu, env2 = J.ent[two ? j + 1 : j] & 0x7FFFFFFFu;
+      if (two)
+        chain2<8>(base, J.mt8 + env * (8 * MT_N), J.mc8 + env * (8 * MT_N / 2), base + MT_N,
+                  J.mt8 + env2 * (8 * MT_N), J.mc8 + env2 * (8 * MT_N / 2));
+      else
+        chain1<8>(base, J.mt8 + env * (8 * MT_N), J.mc8 + env * (8 * MT_N / 2));
+    }
+  } else if constexpr (V >= 11 && V <= 13) {
+    for (int j = w; j < J.n; j += nw) {
+      job_ptrs(J, J.ent[j], src, dst, dc);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      dma_src(src, base);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t env = J.ent[j] & 0x7FFFFFFFu;
+      chain_g<8, V != 12, V != 13>(base, J.mt8 + env * (8 * MT_N), J.mc8 + env * (8 * MT_N / 2));
+    }
   } else if constexpr (V == 5 || V == 6) {
     for (int j = w; j < J.n; j += nw) {
       job_ptrs(J, J.ent[j], src, dst, dc);
@@ -311,6 +436,10 @@ int main(int argc, char** argv) {
   uint32_t* mt4;
   CHECK(hipMalloc(&mc4, envs * 4 * MT_N / 2));
   CHECK(hipMalloc(&mt4, envs * 4 * MT_N * 4));
+  uint32_t* mt8;
+  uint8_t* mc8;
+  CHECK(hipMalloc(&mt8, envs * 8 * MT_N * 4));
+  CHECK(hipMalloc(&mc8, envs * 8 * MT_N / 2));
   {  // integer thresholds of draw_code on k = r * 2^53 (each field is monotone in r)
     auto code_k = [](uint64_t k) { return draw_code((double)k * (1.0 / 9007199254740992.0)); };
     auto first = [&](auto pred) {  // smallest k in [0, 2^53] with pred(code_k(k))
@@ -355,13 +484,13 @@ int main(int argc, char** argv) {
     e[j] = v | ((rand() & 1) ? 0x80000000u : 0u);
   }
   CHECK(hipMemcpy(ent, e.data(), njobs * 4, hipMemcpyHostToDevice));
-  const Job J{mt, mc, mc4, mt4, ent, njobs};
+  const Job J{mt, mc, mc4, mt4, mt8, mc8, ent, njobs};
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  std::vector<uint32_t> ref_w, ref_c, ref4_w, ref4_c;
+  std::vector<uint32_t> ref_w, ref_c, ref4_w, ref4_c, ref8_w, ref8_c;
   printf("{\"jobs\": %d, \"grid\": %d, \"variants\": {", njobs, grid);
-  for (int v = 0; v < 9; ++v) {
+  for (int v = 0; v < 14; ++v) {
     float best = 1e30f;
     for (int rep = 0; rep < 5; ++rep) {
       // jobs name distinct envs and read one half, write the other: every run sees the same input
@@ -375,6 +504,11 @@ int main(int argc, char** argv) {
       if (v == 6) hipLaunchKernelGGL(k_twist<6>, dim3(grid), dim3(BLOCK), 0, 0, J);
       if (v == 7) hipLaunchKernelGGL(k_twist<7>, dim3(grid), dim3(BLOCK), 0, 0, J);
       if (v == 8) hipLaunchKernelGGL(k_twist<8>, dim3(grid), dim3(BLOCK), 0, 0, J);
+      if (v == 9) hipLaunchKernelGGL(k_twist<9>, dim3(grid), dim3(BLOCK), 0, 0, J);
+      if (v == 10) hipLaunchKernelGGL(k_twist<10>, dim3(grid), dim3(BLOCK), 0, 0, J);
+      if (v == 11) hipLaunchKernelGGL(k_twist<11>, dim3(grid), dim3(BLOCK), 0, 0, J);
+      if (v == 12) hipLaunchKernelGGL(k_twist<12>, dim3(grid), dim3(BLOCK), 0, 0, J);
+      if (v == 13) hipLaunchKernelGGL(k_twist<13>, dim3(grid), dim3(BLOCK), 0, 0, J);
       CHECK(hipEventRecord(b));
       CHECK(hipEventSynchronize(b));
       float ms = 0;
@@ -389,6 +523,13 @@ int main(int argc, char** argv) {
     if (v == 0) ref_w = w, ref_c = c;
     else if (v < 4 || v == 8) same = (w == ref_w) && (c == ref_c);
     std::vector<uint32_t> w4(envs * 4 * MT_N / 64), c4(envs * 4 * MT_N / 2 / 64 / 4);
+    std::vector<uint32_t> w8(envs * 8 * MT_N / 64), c8(envs * 8 * MT_N / 2 / 64 / 4);
+    if (v >= 9 && v <= 11) {
+      CHECK(hipMemcpy(w8.data(), mt8, w8.size() * 4, hipMemcpyDeviceToHost));
+      CHECK(hipMemcpy(c8.data(), mc8, c8.size() * 4, hipMemcpyDeviceToHost));
+      if (v == 9) ref8_w = w8, ref8_c = c8;
+      else same = (w8 == ref8_w) && (c8 == ref8_c);
+    }
     if (v >= 5 && v <= 6) {
       CHECK(hipMemcpy(w4.data(), mt4, w4.size() * 4, hipMemcpyDeviceToHost));
       CHECK(hipMemcpy(c4.data(), mc4, c4.size() * 4, hipMemcpyDeviceToHost));
@@ -396,12 +537,17 @@ int main(int argc, char** argv) {
       else same = (w4 == ref4_w) && (c4 == ref4_c);
     }
     const double us = best * 1e3;
-    const int gens = v >= 4 && v <= 7 ? 4 : 1;
+    const int gens = v >= 4 && v <= 7 ? 4 : v >= 9 ? 8 : 1;
+    // per-wave latency of one generation: waves busy x time / generations
+    const int waves_busy = std::min(njobs / (v == 10 ? 2 : 1), grid * 4);
     const double bytes = v == 4 || v == 7 ? 2 * 2496.0 + 4 * 312.0
-                         : v == 5 || v == 6 ? 5 * 2496.0 + 4 * 312.0 : 5304.0;
-    printf("%s\"%c\": {\"ms\": %.4f, \"twists_per_us\": %.1f, \"GBps\": %.0f, \"same_as_A\": %s}",
-           v ? ", " : "", 'A' + v, best, njobs * gens / us, njobs * bytes / us / 1e3,
-           v == 4 || v == 5 || v == 7 ? "null" : same ? "true" : "false");
+                         : v == 5 || v == 6 ? 5 * 2496.0 + 4 * 312.0
+                         : v >= 9 ? 9 * 2496.0 + 8 * 312.0 : 5304.0;
+    printf("%s\"%c\": {\"ms\": %.4f, \"twists_per_us\": %.1f, \"us_per_gen_per_wave\": %.2f, "
+           "\"GBps\": %.0f, \"same_as_A\": %s}",
+           v ? ", " : "", 'A' + v, best, njobs * gens / us, waves_busy * us / ((double)njobs * gens),
+           njobs * bytes / us / 1e3,
+           v == 4 || v == 5 || v == 7 || v == 9 || v >= 12 ? "null" : same ? "true" : "false");
   }
   printf("}}\n");
   return 0;

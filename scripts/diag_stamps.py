@@ -35,13 +35,33 @@ def main():
     for t in range(int(os.environ.get("STEPS", 30))):
         vec.step(vec.policy_actions(t, policy=pol))
     torch.cuda.synchronize()
-    nw = n // 64
-    buf = np.zeros((nw, 10), np.uint64)
+    # k_run's waves (tg_amd.hip run_grid_for): the env workgroups, 3 of padding, REFILL_BLOCKS
+    nw = min(((n + 255) // 256 + 3 + 64) * 4, 1 << 17)
+    buf = np.zeros((nw, 11), np.uint64)
     vec.stats_reset()
     vec.step(vec.policy_actions(999, policy=pol))
     torch.cuda.synchronize()
     _lib.check(L.tg_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), nw), "stamps")
-    act = buf[:, 3] > 0
+    allw = buf[:, 3] > 0
+    idle = allw & ((buf[:, 3] >> 56) == 15)
+    if idle.any():
+        ist = buf[idle, 4].astype(np.int64)
+        ien = buf[idle, 5].astype(np.int64)
+        t00 = buf[allw, 4].astype(np.int64).min()
+        ih = buf[idle, 10].astype(np.int64)
+        print("idle waves %d (refill queue only): halves %d (%.1f per wave, max %d); started by "
+              "10%% %.1f 50%% %.1f 90%% %.1f us; ended by 10%% %.1f 50%% %.1f 90%% %.1f 100%% %.1f us"
+              % (idle.sum(), ih.sum(), ih.mean(), ih.max(),
+                 *np.percentile((ist - t00) / 100.0, [10, 50, 90]),
+                 *np.percentile((ien - t00) / 100.0, [10, 50, 90, 100])))
+        with_job = idle & (buf[:, 10] > 0)
+        if with_job.any():
+            jen = (buf[with_job, 5].astype(np.int64) - t00) / 100.0
+            print("idle waves that regenerated >= 1 half: %d, ended by 50%% %.1f 90%% %.1f 100%% %.1f us"
+                  % (with_job.sum(), *np.percentile(jen, [50, 90, 100])))
+    act = allw & ~idle
+    oh = buf[act, 10].astype(np.int64)
+    print("option waves' queue halves: %d (%.2f per wave)" % (oh.sum(), oh.mean()))
     b = buf[act].astype(np.float64)
     mx = (buf[act, 3] & 0xFFFFFFFF).astype(np.float64)
     sm = ((buf[act, 3] >> 32) & 0xFFFFFF).astype(np.float64)

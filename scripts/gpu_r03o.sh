@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# r03o: DIAGNOSTIC lower bound: k_run without its refill queue (results not exact) vs the product
+# r03o: DIAGNOSTIC lower bound: k_run without its refill queue (results not exact) vs the product; one refill region per grab
 set -u
 OUT=gpurun_out
 mkdir -p $OUT
@@ -13,5 +13,5 @@ run() {
   if [ $rc -ne 0 ]; then echo "stop ($name rc=$rc)"; exit $rc; fi
 }
 cp gym-treasure-game_amd/libtg_amd.so gym-treasure-game_amd/libtg_amd_p0.so
-VARIANTS="p0=gym-treasure-game_amd/libtg_amd_p0.so,noq=gym-treasure-game_amd/libtg_amd_noq.so" ROUNDS=2 STEPS=50 run ab_noq 600 python scripts/ab.py
+VARIANTS="p0=gym-treasure-game_amd/libtg_amd_p0.so,noq=gym-treasure-game_amd/libtg_amd_noq.so,grab1=gym-treasure-game_amd/libtg_amd_grab1.so" ROUNDS=2 STEPS=50 run ab_noq 600 python scripts/ab.py
 echo "== all done"
