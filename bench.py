@@ -59,7 +59,8 @@ PREGEN_BYTES = 8 << 30  # pre-generated action rows for the timed steps, at most
 EP_CAP = 4096          # episode records gathered per rank per step of a drain interval (padded)
 # algorithmic bytes of one tg_step for THIS data layout, per kernel:
 #   k_classify, every env: action 4 + state word 16 + angles 16 + episode 8 read (44)
-#     reward-None env: episode 8 + obs 72 + reward/valid/done 6 written (86)
+#     reward-None env: obs 72 + reward/valid/done 6 written (78; its episode word holds the
+#     return and the episode's start step, unchanged by a reward-None step)
 #     valid env: worklist index 4 + state 16 + angles 16 + episode 8 written (44)
 #     stale MT half: its refill-list entry 4 written (a half is MT_HALF_GENS generations)
 #   k_run, valid env: the worklist row 44 read; state 16 + angles 16 + episode 8 + obs 72 +
@@ -69,10 +70,10 @@ EP_CAP = 4096          # episode records gathered per rank per step of a drain i
 #     4-B refill entry read
 #   k_step (direct mode): one kernel, the same without the worklist round trip
 MT_HALF_GENS = 8
-CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 86, 44, 4 / MT_HALF_GENS
+CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 78, 44, 4 / MT_HALF_GENS
 RUN_VALID, RUN_DRAW = 162, 1
 RUN_REGEN = 2496 + 312 + (2496 + 4) / MT_HALF_GENS
-DIRECT_ENV, DIRECT_INVALID, DIRECT_VALID = 44, 86, 118
+DIRECT_ENV, DIRECT_INVALID, DIRECT_VALID = 44, 78, 118
 DIRECT_REGEN = 2496 + 312 + 2496 / MT_HALF_GENS
 BYTES_DRAW = RUN_DRAW
 # SURVEY.md §8(d)'s layout-independent count per env-step: action 4 + obs 72 + reward 4 +

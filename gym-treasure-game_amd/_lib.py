@@ -17,14 +17,12 @@ TG_POLICY_UNIFORM = 0
 TG_POLICY_MASKED = 1
 TG_MODE_DIRECT = 0
 TG_MODE_COMPACT = 1
-TG_MODE_ASYNC = 2
 TG_ERR_TICKCAP = 1 << 24
 TG_ERR_BAG = 1 << 25
 TG_ERR_ACTION = 1 << 26
 TG_ERR_NEARINT = 1 << 27
 TG_ERR_RENDER = 1 << 28
 TG_ERR_WINDOW = 1 << 29
-TG_ERR_STALL = 1 << 31
 TG_SPR_COUNT = 24
 OBS_DIM = 9
 NUM_ACTIONS = 9

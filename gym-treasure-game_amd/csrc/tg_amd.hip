@@ -115,11 +115,10 @@ __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o
 //   Draws that need the double (handle angles in a flip cascade, an auto-reset's uniform and
 //   gauss) consume the code and read the position's two words (one 8-B load).
 // ------------------------------------------------------------------------------------------
-#ifndef TG_WIN_UNIT
-#define TG_WIN_UNIT 16
-#endif
-constexpr int WIN_UNIT = TG_WIN_UNIT;  // code bytes per lane per LDS-DMA (16: dwordx4, 4: dword)
-static_assert(WIN_UNIT == 16 || WIN_UNIT == 4, "global_load_lds_dwordx4 or _dword");
+// code bytes per lane per LDS-DMA (global_load_lds_dwordx4).  The dword form (lane l's 4 B at
+// M0 + 4l, no LDS bank conflicts) needs 4x the DMA instructions per fill and measured 7 %
+// slower (profiles/r03/lds_window_ab.json)
+constexpr int WIN_UNIT = 16;
 constexpr int WIN_DRAWS = 64;                       // codes per lane in the window
 constexpr int WIN_SLOTS = WIN_DRAWS / WIN_UNIT;     // DMA instructions per fill
 constexpr int WIN_SLOT_BYTES = 64 * WIN_UNIT;       // one slot: every lane's unit
@@ -142,11 +141,7 @@ __device__ __forceinline__ void glds_unit(uint32_t m0, const void* gptr) {
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"
-#if TG_WIN_UNIT == 16
       "global_load_lds_dwordx4 %2, off\n\t"
-#else
-      "global_load_lds_dword %2, off\n\t"
-#endif
       "s_mov_b32 m0, %0"
       : "=&s"(save)
       : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
@@ -534,7 +529,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_codes(Soa S, int64_t n) {
 
 __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
                                                   const uint8_t* __restrict__ mask,
-                                                  double* __restrict__ obs) {
+                                                  double* __restrict__ obs, uint32_t tstep) {
   __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < n;
@@ -561,7 +556,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
     e.mti &= ~MT_STALE;
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
-    S.ep[i] = make_int2(0, 0);
+    S.ep[i] = make_int2(0, (int32_t)tstep);  // the episode starts with the next step
   }
 }
 
@@ -576,6 +571,8 @@ struct StepIO {
                                    // (selects the kernels' POL instantiation)
   uint64_t a0;                     // the policy's action seed and step index
   int64_t t;
+  uint32_t tstep;                  // this step's index in the handle's step count (launch_step):
+                                   // an episode's length is tstep + 1 - its start step (S.ep.y)
 };
 
 __device__ __forceinline__ uint64_t sm64(uint64_t x) {
@@ -616,8 +613,8 @@ struct EpQueue {
 // waves in flight (<= cap + n < 2^31 with cap <= 2^28 and n < 2^30); slots are compared
 // unsigned.  The records that do not fit are counted per wave in the wave's own block slot.
 // Must be reached by every lane of the wave.
-__device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, const EpQueue& q,
-                                                unsigned long long* stats) {
+__device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, uint32_t tstep,
+                                                const EpQueue& q, unsigned long long* stats) {
   const unsigned long long b = __ballot(mine);
   if (!b) return;
   const int lane = threadIdx.x & 63;
@@ -640,10 +637,10 @@ __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, 
       tg_episode r;
       r.env = g;
       r.ret = ep.x;
-      r.len = ep.y;
+      r.len = (int32_t)(tstep + 1u - (uint32_t)ep.y);
       q.eps[slot] = r;
     }
-    ep = make_int2(0, 0);
+    ep = make_int2(0, (int32_t)(tstep + 1u));  // the next episode starts with the next step
   }
 }
 
@@ -681,8 +678,7 @@ __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int6
   io.reward[i] = r.reward;
   io.valid[i] = (uint8_t)r.ran;
   io.done[i] = (uint8_t)r.done;
-  ep.x += r.reward;
-  ep.y += 1;
+  ep.x += r.reward;  // (ep.y, the episode's start step, stays: no store for a reward-None step)
   if (FINAL) store_obs(io.final_obs, i, o);
   if (AUTORESET && r.done) {
     reset_env(L, e, rng);
@@ -738,10 +734,11 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
   int lregen = 0;  // halves this lane regenerated in its option loop
   Env e;
   e.mti = 0u;
-  int2 ep = make_int2(0, 0);
+  int2 ep = make_int2(0, 0), ep_in = ep;
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
+    ep_in = ep;
     RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
     int act;
     if constexpr (POL >= 0) {
@@ -765,11 +762,11 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
               S.mc + (live ? i : 0) * MT_CODES, e.mti,
               (lds_u32*)wscr);
   e.mti &= ~MT_STALE;
-  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
+  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats);
   if (live) {
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
-    S.ep[i] = ep;
+    if (ep.x != ep_in.x || ep.y != ep_in.y) S.ep[i] = ep;  // a reward-None step changes nothing
   }
   wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
               __popcll(need) + wave_sum(lregen), true);
@@ -937,7 +934,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     draws = rng.draws;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
-  if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, q, stats);
+  const int2 ep_in = ep;
+  if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, io.tstep, q, stats);
   store_obs_wave(io.obs, i - lane, __ballot(live && !runs), orow,
                  ostage + (threadIdx.x & ~63) * 9);
   if (live && !runs) {
@@ -946,7 +944,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
       S.st4[i] = s4n;
       S.ang[i] = make_double2(e.ang0, e.ang1);
     }
-    S.ep[i] = ep;
+    // reward None: the return and the episode's start step are unchanged unless it ended
+    if (ep.x != ep_in.x || ep.y != ep_in.y) S.ep[i] = ep;
   }
   if (threadIdx.x < O_COUNT) bbase[threadIdx.x] = my_base;
   __syncthreads();
@@ -1075,7 +1074,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     lregen = (int)rng.regens;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
-  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, q, stats);
+  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats);
   if (live) {
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
@@ -1173,464 +1172,6 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     }
   }
 #endif
-}
-
-// ------------------------------------------------------------------------------------------
-// tg_rollout, TG_MODE_ASYNC: K steps of every env in ONE launch, no step barrier.
-//   Workgroup b owns envs [b*E, b*E + E) for the whole launch (E <= RO_EMAX; nothing is
-//   shared between workgroups, so there is no cross-CU hand-off and no grid-wide wait).  Inside
-//   a workgroup the envs sit in per-option queues (LDS bitmaps over the E local indices, one
-//   bit per env, plus a count); each wave repeatedly pops up to 64 envs of ONE option, runs
-//   their option loops (the same run_option as k_run: wave-uniform k), finishes the step (the
-//   step's outputs at row t of [K][N]), and then, per lane, evaluates the env's NEXT step: the
-//   policy's action, can_run (a reward-None step is finished right there, as k_classify does,
-//   and the next one evaluated), and pushes the env onto that option's queue.  Envs therefore
-//   advance at their own pace — env i's step t still depends only on env i's state, so every
-//   output row, state word and episode record is the one K x tg_step produces (the episode
-//   queue's ORDER differs) — and a wave never waits for the slowest option of a step.
-//   Stale MT halves: an env that leaves a half goes onto queue RO_REFILL first; a wave that
-//   pops it regenerates the half with the coalesced whole-wave twist (wave_refill), then moves
-//   the env on to the option recorded for it (nextk).  So no env enters a stale half here.
-//   Same-CU hand-offs only: a lane's global stores of an env (state, MT) are complete
-//   (s_waitcnt vmcnt(0)) before the env's bit is set; pops and pushes are LDS atomics; pops
-//   hold a workgroup LDS lock while they scan the bitmap.
-// ------------------------------------------------------------------------------------------
-constexpr int RO_WAVES = 4;
-#ifndef TG_RO_MINW
-#define TG_RO_MINW 3  // waves per SIMD the register budget is sized for (launch bounds)
-#endif
-constexpr int RO_THREADS = RO_WAVES * 64;
-constexpr int RO_EMAX = 2048;            // envs per workgroup: 64 bitmap words (one per lane)
-constexpr int RO_WORDS = RO_EMAX / 32;
-constexpr int RO_REFILL = O_COUNT;       // queue of envs whose stale MT half comes first
-constexpr int RO_NEXT = O_COUNT + 1;     // queue of envs whose next step is to be evaluated
-constexpr int RO_NQ = O_COUNT + 2;
-constexpr uint8_t RO_RETIRE = 0xFF;      // nextk: the env has done its K steps
-constexpr uint8_t RO_TONEXT = 0xFE;      // nextk: after the refill, on to RO_NEXT
-constexpr uint32_t RO_E_STALL = TG_ERR_STALL;  // a workgroup's queues stopped making progress (bug)
-constexpr unsigned long long RO_STALL_TICKS = 200000000ull;  // 2 s of the 100 MHz clock without progress
-static_assert(RO_WORDS == 64, "one bitmap word per lane");
-
-struct RollIO {
-  StepIO io;         // row-0 pointers ([K][N] arrays), policy, action seed, t = the first step
-  int32_t steps;     // K
-  bool obs_rows;     // obs is [K][N][9] (else [N][9] scratch, overwritten every step)
-};
-__device__ __forceinline__ StepIO step_io(const RollIO& R, int t, int64_t n) {
-  StepIO s = R.io;
-  const size_t off = (size_t)t * (size_t)n;
-  if (s.actions) s.actions += off;
-  if (R.obs_rows) s.obs += off * 9;
-  s.reward += off;
-  s.valid += off;
-  s.done += off;
-  s.t = R.io.t + t;
-  return s;
-}
-
-struct RoLds {
-  uint32_t bits[RO_NQ][RO_WORDS];
-  int cnt[RO_NQ];
-  int cursor[RO_NQ];
-  int lock, running, retired;
-  uint16_t tstep[RO_EMAX];  // steps done in this launch
-  uint8_t nextk[RO_EMAX];   // the option an env on RO_REFILL moves on to (or RO_RETIRE)
-  uint16_t stage[RO_WAVES][64];
-  unsigned long long count[6];  // steps, valid, ticks, draws, episodes, regens (the launch's)
-  unsigned long long wticks;
-};
-
-struct LaneCount {
-  int steps, valid, ticks, draws, episodes, regens;
-};
-// a batch's counts into the workgroup's (LDS) totals; all 64 lanes
-__device__ __forceinline__ void ro_count(RoLds& Q, const LaneCount& c) {
-  const int v[6] = {wave_sum(c.steps), wave_sum(c.valid), wave_sum(c.ticks), wave_sum(c.draws),
-                    wave_sum(c.episodes), wave_sum(c.regens)};
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-      if (v[k]) atomicAdd(&Q.count[k], (unsigned long long)v[k]);
-  }
-}
-
-// one completed episode, from a lane on its own (the rare reward-None step that ends one)
-__device__ __forceinline__ void record_episode_lane(int64_t g, int2& ep, const EpQueue& q,
-                                                    unsigned long long* stats) {
-  const int slot = atomicAdd(q.count, 1);
-  if ((uint32_t)slot >= (uint32_t)q.cap) {
-    atomicMin(q.count, q.cap);
-    atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + ST_EP_OVERFLOW], 1ull);
-  } else {
-    tg_episode r;
-    r.env = g;
-    r.ret = ep.x;
-    r.len = ep.y;
-    q.eps[slot] = r;
-  }
-  ep = make_int2(0, 0);
-}
-
-// The env's next step(s) after `t` steps: reward-None steps are finished here (k_classify's
-// path) until one whose option can run, or the K-th step.  Returns the queue to push the env
-// onto: its option, RO_REFILL (a stale half; nk = the option or RO_RETIRE), or -1 (retired).
-template <bool AUTORESET, int POL>
-__device__ __forceinline__ int ro_advance(const Level& L, const Map& m, Env& e, int2& ep,
-                                          int64_t i, int64_t g, int& t, const RollIO& R,
-                                          int64_t n, const Soa& S, const EpQueue& q,
-                                          unsigned long long* stats, uint8_t& nk, LaneCount& c) {
-  nk = RO_RETIRE;
-  while (t < R.steps) {
-    const int act = policy_action(L, m, e, POL, R.io.a0, g, R.io.t + t);
-    const StepIO io = step_io(R, t, n);
-    if (io.actions) io.actions[i] = act;
-    const int k = option_index(act);
-    if (k >= 0 && can_run(L, m, e, k)) {
-      nk = (uint8_t)k;
-      break;
-    }
-    // reward None, state unchanged (TG/:91-96, OP/:22-23)
-    if (k < 0) e.f |= E_ACTION;
-    const bool dn = is_done(e);
-    Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
-    const StepResult r{0, 0, (int)dn, 0};
-    finish_step<AUTORESET, false>(L, e, rng, i, r, ep, io);
-    e.mti = rng.finish();
-    c.draws += (int)rng.draws;
-    c.steps += 1;
-    if (AUTORESET && dn) {
-      record_episode_lane(g, ep, q, stats);
-      c.episodes += 1;
-    }
-    ++t;
-  }
-  if (e.mti & MT_STALE) return RO_REFILL;
-  return nk == RO_RETIRE ? -1 : (int)nk;
-}
-
-// push every lane's env (local index j) onto queue `dest` (-1: retired, -2: nothing); all 64
-// lanes.  The lanes' global stores must be complete (the caller's vmcnt(0)).
-__device__ __forceinline__ void ro_push(RoLds& Q, int dest, int j) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int qq = 0; qq < RO_NQ; ++qq) {
-    const unsigned long long b = __ballot(dest == qq);
-    if (b) {
-      if (dest == qq) atomicOr(&Q.bits[qq][j >> 5], 1u << (j & 31));
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the bits before the count
-      if (lane == __ffsll((long long)b) - 1) atomicAdd(&Q.cnt[qq], __popcll(b));
-    }
-  }
-  const unsigned long long r = __ballot(dest == -1);
-  if (r && lane == __ffsll((long long)r) - 1) atomicAdd(&Q.retired, __popcll(r));
-}
-
-// the workgroup's queue lock (lane 0 spins; bounded by RO_STALL_TICKS of real time): false =
-// give up (flagged).  Waves with nothing to do poll the counts WITHOUT the lock, so a holder
-// never competes with idle pollers.
-__device__ __forceinline__ bool ro_lock(RoLds& Q, uint32_t* err_or) {
-  int got = 1;
-  if ((threadIdx.x & 63) == 0) {
-    unsigned long long t0 = 0;
-    while (atomicCAS(&Q.lock, 0, 1) != 0) {
-      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-      if (!t0) t0 = now;
-      if (now - t0 > RO_STALL_TICKS) {  // cannot happen unless the bookkeeping is broken
-        got = 0;
-        atomicOr(err_or, RO_E_STALL);
-        printf("k_rollout: block %d wave %d: queue lock not released\n", (int)blockIdx.x,
-               (int)(threadIdx.x >> 6));
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  got = __shfl(got, 0, 64);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  return got != 0;
-}
-__device__ __forceinline__ void ro_unlock(RoLds& Q) {
-  if ((threadIdx.x & 63) == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    atomicExch(&Q.lock, 0);
-  }
-}
-// With the lock held: take up to `want` envs off queue qsel into Q.stage[wave][0, take), scanning
-// its bitmap from the queue's cursor (lane l reads word cursor + l), so every queued env is
-// reached within one sweep.  Returns take (wave-uniform).  All 64 lanes.
-__device__ __forceinline__ int ro_pop(RoLds& Q, int qsel, int want) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int take = __builtin_amdgcn_readfirstlane(
-      __hip_atomic_load(&Q.cnt[qsel], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-  if (take > want) take = want;
-  if (take <= 0) return 0;
-  const int cur = __builtin_amdgcn_readfirstlane(Q.cursor[qsel]);
-  const int wd = (cur + lane) & (RO_WORDS - 1);
-  uint32_t v = __hip_atomic_load(&Q.bits[qsel][wd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  const int pc = __popc(v);
-  int incl = pc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
-  }
-  const int avail = __shfl(incl, 63, 64);
-  if (avail < take) take = avail;  // never (a counted env's bit is set before its count)
-  const int excl = incl - pc;
-  const int mine = excl >= take ? 0 : (take - excl < pc ? take - excl : pc);
-  uint32_t picked = 0;
-  for (int r = 0; r < mine; ++r) {
-    const uint32_t bit = v & (0u - v);
-    picked |= bit;
-    v ^= bit;
-    Q.stage[wave][excl + r] = (uint16_t)(wd * 32 + __builtin_ctz(bit));
-  }
-  if (picked) atomicAnd(&Q.bits[qsel][wd], ~picked);
-  const unsigned long long tk = __ballot(mine > 0);
-  const int last = tk ? 63 - __clzll((long long)tk) : 0;
-  const int lastw = __shfl(wd, last, 64), lastleft = __shfl(pc - mine, last, 64);
-  if (lane == 0 && take > 0) {
-    Q.cursor[qsel] = lastleft ? lastw : ((lastw + 1) & (RO_WORDS - 1));
-    atomicSub(&Q.cnt[qsel], take);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the stage entries, for every lane
-  return take;
-}
-
-// the queued envs' next steps (ro_advance: the policy's action, can_run, reward-None steps
-// finished on the spot), then on to their option's queue.  All 64 lanes; `take` envs staged.
-template <bool AUTORESET, int POL>
-__device__ __forceinline__ void ro_next_batch(const Soa& S, int64_t n, const Level& L,
-                                              const Map& m, const RollIO& R, const EpQueue& q,
-                                              int64_t g0, int64_t base, int take, RoLds& Q,
-                                              unsigned long long* stats, uint32_t* err_or) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool live = lane < take;
-  const int j = live ? (int)Q.stage[wave][lane] : 0;
-  int dest = -2;
-  LaneCount c{0, 0, 0, 0, 0, 0};
-  if (live) {
-    const int64_t i = base + j;
-    Env e;
-    unpack(S.st4[i], S.ang[i], e);
-    int2 ep = S.ep[i];
-    int t = Q.tstep[j];
-    const int t0 = t;
-    uint8_t nk;
-    dest = ro_advance<AUTORESET, POL>(L, m, e, ep, i, g0 + i, t, R, n, S, q, stats, nk, c);
-    if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
-    if (t != t0) {
-      S.st4[i] = pack(e);
-      S.ang[i] = make_double2(e.ang0, e.ang1);
-      S.ep[i] = ep;
-      Q.tstep[j] = (uint16_t)t;
-    }
-    Q.nextk[j] = nk;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the envs' stores before their bits
-  ro_push(Q, dest, j);
-  ro_count(Q, c);
-}
-
-// the queued envs' stale MT halves, regenerated with the whole wave (wave_refill), then on to
-// the option recorded for each (nextk).  All 64 lanes; `take` envs staged by ro_pop.
-__device__ __forceinline__ void ro_refill_batch(const Soa& S, int64_t base, int take, RoLds& Q,
-                                                lds_u8* wscr) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool live = lane < take;
-  const int j = live ? (int)Q.stage[wave][lane] : 0;
-  const int64_t i = base + j;
-  Env e;
-  e.mti = 0u;
-  uint4 s4 = make_uint4(0, 0, 0, 0);
-  if (live) {
-    s4 = S.st4[i];
-    unpack_st4(s4, e);
-  }
-  wave_refill(__ballot(live), S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES,
-              e.mti, (lds_u32*)wscr);
-  int dest = -2;
-  LaneCount c{0, 0, 0, 0, 0, 0};
-  if (live) {
-    s4.w = e.mti & ~MT_STALE;
-    S.st4[i] = s4;
-    c.regens = 1;
-    const uint8_t nk = Q.nextk[j];
-    dest = nk == RO_RETIRE ? -1 : nk == RO_TONEXT ? RO_NEXT : (int)nk;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new half and state before the bits
-  ro_push(Q, dest, j);
-  ro_count(Q, c);
-}
-
-template <bool AUTORESET, int POL>
-__global__ __launch_bounds__(RO_THREADS, TG_RO_MINW) void k_rollout(Soa S, int64_t n, Level L,
-                                                          const uint32_t* __restrict__ grid,
-                                                          RollIO R, EpQueue q, int64_t g0,
-                                                          int32_t E,
-                                                          unsigned long long* __restrict__ stats,
-                                                          uint32_t* __restrict__ err_or) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[RO_WAVES * WIN_WAVE_BYTES];
-  __shared__ RoLds Q;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t base = (int64_t)blockIdx.x * E;
-  const int ne = (int)(n - base < (int64_t)E ? n - base : (int64_t)E);
-  for (int w = threadIdx.x; w < RO_NQ * RO_WORDS; w += RO_THREADS) (&Q.bits[0][0])[w] = 0u;
-  if (threadIdx.x < RO_NQ) Q.cnt[threadIdx.x] = Q.cursor[threadIdx.x] = 0;
-  if (threadIdx.x == 0) Q.lock = Q.running = Q.retired = 0;
-  if (threadIdx.x < 6) Q.count[threadIdx.x] = 0ull;
-  if (threadIdx.x == 6) Q.wticks = 0ull;
-  LEVEL_IN_LDS();  // includes the barrier
-  lds_u8* const wscr = (lds_u8*)win + wave * WIN_WAVE_BYTES;
-
-  // every env's first step: its action, and the reward-None steps before one that runs
-  for (int j0 = 0; j0 < ne; j0 += RO_THREADS) {
-    const int j = j0 + (int)threadIdx.x;
-    int dest = -2;
-    LaneCount c{0, 0, 0, 0, 0, 0};
-    if (j < ne) {
-      const int64_t i = base + j;
-      Env e;
-      unpack(S.st4[i], S.ang[i], e);
-      int2 ep = S.ep[i];
-      int t = 0;
-      uint8_t nk;
-      dest = ro_advance<AUTORESET, POL>(L, m, e, ep, i, g0 + i, t, R, n, S, q, stats, nk, c);
-      if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
-      if (t) {
-        S.st4[i] = pack(e);
-        S.ang[i] = make_double2(e.ang0, e.ang1);
-        S.ep[i] = ep;
-      }
-      Q.tstep[j] = (uint16_t)t;
-      Q.nextk[j] = nk;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ro_push(Q, dest, j);
-    ro_count(Q, c);
-  }
-  __syncthreads();
-
-  unsigned long long idle0 = 0;  // when this wave last found no work (0: it did find some)
-  while (true) {
-    // ---- the next batch of this wave (counts polled without the lock; the pop re-reads them
-    // under it).  Full 64-env batches of one option while the queues hold them, so a wave's
-    // lanes start together (their plain-tick spans stay in step); partial ones when the
-    // workgroup runs low.
-    const int cl = lane < RO_NQ ? __hip_atomic_load(&Q.cnt[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
-    const int retired = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&Q.retired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    const int running = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&Q.running, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    int qsel = -1;
-    {
-      int total = 0, best = 0, bk = -1;
-#pragma unroll
-      for (int qq = 0; qq < O_COUNT; ++qq) {
-        const int v = __builtin_amdgcn_readlane(cl, qq);
-        total += v;
-        if (v > best) best = v, bk = qq;
-      }
-      const int rf = __builtin_amdgcn_readlane(cl, RO_REFILL);
-      const int nx = __builtin_amdgcn_readlane(cl, RO_NEXT);
-      const bool few_running = running < RO_WAVES / 2;
-      if (rf > 0 && (rf >= 8 || few_running || best < 64))
-        qsel = RO_REFILL;
-      else if (nx > 0 && (nx >= 64 || few_running || best < 64))
-        qsel = RO_NEXT;
-      else if (bk >= 0 && (best >= 64 || 4 * best >= total || few_running))
-        qsel = bk;
-    }
-    int take = 0;
-    if (qsel >= 0) {
-      if (!ro_lock(Q, err_or)) break;
-      take = ro_pop(Q, qsel, 64);
-      if (take && lane == 0) atomicAdd(&Q.running, 1);
-      ro_unlock(Q);
-    }
-    if (take == 0) {
-      if (retired >= ne) break;
-      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-      if (!idle0) idle0 = now;
-      if (now - idle0 > RO_STALL_TICKS) {  // cannot happen unless the bookkeeping is broken
-        if (lane == 0) {
-          atomicOr(err_or, RO_E_STALL);
-          printf("k_rollout: block %d wave %d: no work, retired %d of %d\n", (int)blockIdx.x,
-                 (int)(threadIdx.x >> 6), retired, ne);
-        }
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    idle0 = 0;
-    if (qsel == RO_REFILL) {
-      ro_refill_batch(S, base, take, Q, wscr);
-      if (lane == 0) atomicSub(&Q.running, 1);
-      continue;
-    }
-    if (qsel == RO_NEXT) {
-      ro_next_batch<AUTORESET, POL>(S, n, L, m, R, q, g0, base, take, Q, stats, err_or);
-      if (lane == 0) atomicSub(&Q.running, 1);
-      continue;
-    }
-    // ---- one step of option qsel for every popped env
-    const int k = qsel;
-    const bool live = lane < take;
-    const int j = live ? (int)Q.stage[wave][lane] : 0;
-    const int64_t i = base + j;
-    int dest = -2;
-    LaneCount c{0, 0, 0, 0, 0, 0};
-    StepResult r{0, 0, 0, 0};
-    if (live) {
-      Env e;
-      unpack(S.st4[i], S.ang[i], e);
-      int2 ep = S.ep[i];
-      int t = Q.tstep[j];
-      RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
-      rng.prime();
-      if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
-      run_option(L, trig, m, e, k, rng, r);
-      __builtin_amdgcn_s_setprio(0);
-      r.done = is_done(e);
-      finish_step<AUTORESET, false>(L, e, rng, i, r, ep, step_io(R, t, n));
-      e.mti = rng.finish();
-      c.steps = c.valid = 1;
-      c.ticks = r.ticks;
-      c.draws = (int)rng.draws;
-      c.regens = (int)rng.regens;
-      ++t;
-      if (AUTORESET && r.done) {
-        record_episode_lane(g0 + i, ep, q, stats);
-        c.episodes = 1;
-      }
-      // the next step is evaluated by a RO_NEXT batch (kept out of this code path: its
-      // registers would add to the option loops')
-      const uint8_t nk = t >= R.steps ? RO_RETIRE : RO_TONEXT;
-      dest = (e.mti & MT_STALE) ? RO_REFILL : nk == RO_RETIRE ? -1 : RO_NEXT;
-      if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
-      S.st4[i] = pack(e);
-      S.ang[i] = make_double2(e.ang0, e.ang1);
-      S.ep[i] = ep;
-      Q.tstep[j] = (uint16_t)t;
-      Q.nextk[j] = nk;
-    }
-    const int wt = wave_max(r.ticks);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the envs' stores before their bits
-    ro_push(Q, dest, j);
-    ro_count(Q, c);
-    if (lane == 0) {
-      if (wt) atomicAdd(&Q.wticks, (unsigned long long)wt);
-      atomicSub(&Q.running, 1);
-    }
-  }
-  __syncthreads();  // every wave has left the loop: the workgroup's counts are final
-  if (threadIdx.x < 7) {
-    const unsigned long long v = threadIdx.x < 6 ? Q.count[threadIdx.x] : Q.wticks;
-    const int slot = threadIdx.x < 5 ? ST_STEPS + (int)threadIdx.x
-                     : threadIdx.x == 5 ? ST_REGENS : ST_WTICKS;
-    if (v) atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + slot], v);
-  }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
@@ -1784,42 +1325,55 @@ __device__ __forceinline__ void lds_twist64(const uint32_t* src, uint32_t* dst) 
     __syncthreads();
   }
 }
+// The Python stream's generation and its two successors, kept on the device between calls
+// (tg_batch::pyc): cache_in is it when the caller's state is the one the last call returned
+// (the host compares them), else null and the generation is read from the caller's state (py,
+// pinned host memory) and its successors twisted here.  q0 / gauss: the caller's index and
+// gauss_next, as kernel arguments (no host-memory reads in the common case).  On return py
+// holds the state after the call: its index and gauss_next, and the generation's words when
+// the generation changed (otherwise py's words already are the generation's), and cache_out
+// holds the new generation and its two successors.
 template <bool RESET>
 __global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __restrict__ grid,
-                                            int action, tg_pystate* py, TgOne* out,
+                                            int action, tg_pystate* py, const uint32_t* cache_in,
+                                            uint32_t* cache_out, uint32_t q0, int has_gauss,
+                                            double gauss_next, TgOne* out, uint32_t tstep,
                                             unsigned long long* __restrict__ stats,
                                             uint32_t* __restrict__ err_or) {
   __shared__ uint32_t W[PY_GENS * MT_N];
   __shared__ LdsLevel lv;
-  __shared__ uint32_t out_gen, out_idx;
+  __shared__ uint32_t out_g, out_lo, out_idx;
   const int lane = threadIdx.x;
   const int nwords = ((L.W + 2 * PAD) * (L.H + 2 * PAD) + 3) / 4;
   for (int i = lane; i < nwords; i += 64) lv.grid[i] = grid[i];
   if (lane < 12) lv.trig[lane] = L.trig[lane >> 1][lane & 1];
-  for (int i = lane; i < MT_N; i += 64) W[i] = py->mt[i];
-  __syncthreads();
-  lds_twist64(W, W + MT_N);
-  lds_twist64(W + MT_N, W + 2 * MT_N);
+  if (cache_in) {
+    for (int i = lane; i < PY_GENS * MT_N; i += 64) W[i] = cache_in[i];
+    __syncthreads();
+  } else {
+    for (int i = lane; i < MT_N; i += 64) W[i] = py->mt[i];
+    __syncthreads();
+    lds_twist64(W, W + MT_N);
+    lds_twist64(W + MT_N, W + 2 * MT_N);
+  }
   StepResult r{0, 0, 0, 0};
   uint32_t draws = 0;
   if (lane == 0) {
     const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
-    const uint32_t q0 = py->index;
     PyRng rng{W, q0, 0u, 0u};
     Env e;
     unpack(S.st4[0], S.ang[0], e);
     int2 ep = S.ep[0];
     double o[9];
     if (RESET) {
-      GaussNext g{py->has_gauss != 0u, py->gauss_next};
+      GaussNext g{has_gauss != 0, gauss_next};
       reset_env_gauss(L, e, rng, g);
       py->has_gauss = g.has ? 1u : 0u;
       py->gauss_next = g.has ? g.v : 0.0;
-      ep = make_int2(0, 0);
+      ep = make_int2(0, (int32_t)tstep);  // the episode starts with the next step
     } else {
       r = env_step(L, lv.trig, m, e, action, rng);
-      ep.x += r.reward;
-      ep.y += 1;
+      ep.x += r.reward;  // (ep.y: the episode's start step)
     }
     observe(L, e, o);
 #pragma unroll
@@ -1833,14 +1387,26 @@ __global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __re
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
     // CPython's state after the last word read: its generation and the index past it
     const uint32_t g = rng.q == q0 ? 0u : (rng.q - 1u) / MT_N;
-    out_gen = g % PY_GENS;
+    out_g = g;
+    out_lo = rng.lo;
     out_idx = rng.q == q0 ? q0 : rng.q - g * MT_N;
     draws = rng.draws;
   }
   __syncthreads();
-  const uint32_t* src = W + out_gen * MT_N;
-  for (int i = lane; i < MT_N; i += 64) py->mt[i] = src[i];
+  const uint32_t g = out_g;
+  if (g != 0u) {  // the caller's generation changed
+    const uint32_t* src = W + (g % PY_GENS) * MT_N;
+    for (int i = lane; i < MT_N; i += 64) py->mt[i] = src[i];
+  }
   if (lane == 0) py->index = out_idx;
+  if (g != 0u || !cache_in) {
+    // the cache: generations g, g + 1, g + 2 (the ring holds out_lo .. out_lo + 2, g among
+    // them; the missing successors are twisted over generations older than g)
+    for (uint32_t hi = out_lo + PY_GENS - 1; hi < g + PY_GENS - 1; ++hi)
+      lds_twist64(W + (hi % PY_GENS) * MT_N, W + ((hi + 1) % PY_GENS) * MT_N);
+    for (int j = 0; j < PY_GENS; ++j)
+      for (int i = lane; i < MT_N; i += 64) cache_out[j * MT_N + i] = W[((g + j) % PY_GENS) * MT_N + i];
+  }
   wave_stats(stats, lane == 0 && !RESET ? 1 : 0, r.ran, r.ticks, (int)draws, 0);
 }
 
@@ -1860,13 +1426,8 @@ int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 // regenerations start at once, measured no faster for the masked policy and slower for the
 // uniform one: DESIGN.md §3.3)
 int run_grid_for(int64_t n) { return grid_for(n) + (O_COUNT * 64 + BLOCK - 1) / BLOCK + REFILL_BLOCKS; }
-// per-block launch-counter slots cover the largest step grid
-// one counter slot per workgroup of the widest step launch: k_run, or k_rollout (>= 64 envs
-// per workgroup)
-int stat_slots(int64_t n) {
-  const int64_t ro = (n + 63) / 64;
-  return ro > run_grid_for(n) ? (int)ro : run_grid_for(n);
-}
+// one launch-counter slot per workgroup of the widest step launch (k_run)
+int stat_slots(int64_t n) { return run_grid_for(n); }
 
 int flush_timing(tg_batch* h) {
   for (size_t k = 0; k + 3 <= h->ev_used; k += 3) {
@@ -2000,7 +1561,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n,
                      (uint32_t)(MT_WORDS - MT_N), 0u, 2 * MT_HALF_GENS);
   hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, h->L,
-                     (const uint8_t*)nullptr, (double*)nullptr);
+                     (const uint8_t*)nullptr, (double*)nullptr, 0u);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) return cleanup(fail(TG_E_HIP, "k_create: %s", hipGetErrorString(e)));
@@ -2022,13 +1583,14 @@ void tg_destroy(tg_batch* h) {
     if (b) (void)hipFree(b);
   if (h->one) (void)hipHostFree(h->one);
   if (h->py) (void)hipHostFree(h->py);
+  if (h->pyc) (void)hipFree(h->pyc);
   delete h;
 }
 
 int tg_reset(tg_batch* h, const uint8_t* mask, double* obs, void* stream) {
   BIND(h);
   hipLaunchKernelGGL(k_reset, dim3(grid_for(h->n)), dim3(BLOCK), 0, (hipStream_t)stream, h->S,
-                     h->n, h->L, mask, obs);
+                     h->n, h->L, mask, obs, h->tstep);
   HIP_TRY(hipGetLastError());
   return TG_OK;
 }
@@ -2037,7 +1599,9 @@ int tg_reset(tg_batch* h, const uint8_t* mask, double* obs, void* stream) {
 
 namespace {
 // one step's kernels on `st`, timed with HIP events when enabled
-int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
+int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
+  StepIO io = io_in;
+  io.tstep = h->tstep++;
   const bool fo = io.final_obs != nullptr;
   int rc;
   const bool timed = timing_begin(h, st, rc);
@@ -2088,40 +1652,6 @@ int launch_step(tg_batch* h, const StepIO& io, bool ar, hipStream_t st) {
   return timed ? timing_mark(h, st, 2) : TG_OK;
 }
 
-// envs per k_rollout workgroup: one round of workgroups fills every CU's resident slots
-// (a second, partial round would run on a few CUs after the rest had finished); at least 64
-int32_t ro_envs_per_block(int64_t n, int slots) {
-  const int64_t e = (n + slots - 1) / slots;
-  return (int32_t)(e < 64 ? 64 : (e > RO_EMAX ? RO_EMAX : e));
-}
-
-int launch_rollout(tg_batch* h, const RollIO& R, bool ar, hipStream_t st) {
-  int rc;
-  const bool timed = timing_begin(h, st, rc);
-  if (rc) return rc;
-  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
-  decltype(&k_rollout<true, 0>) kern;
-  if (R.io.policy == TG_POLICY_UNIFORM)
-    kern = ar ? k_rollout<true, 0> : k_rollout<false, 0>;
-  else
-    kern = ar ? k_rollout<true, 1> : k_rollout<false, 1>;
-  if (!h->ro_per_cu) {
-    int nb = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kern),
-                                                         RO_THREADS, 0));
-    h->ro_per_cu = nb > 0 ? nb : 1;
-  }
-  const int32_t E = ro_envs_per_block(h->n, h->cus * h->ro_per_cu);
-  const dim3 grid((unsigned)((h->n + E - 1) / E)), block(RO_THREADS);
-  if ((int64_t)grid.x > (int64_t)stat_slots(h->n))
-    return fail(TG_E_INVAL, "k_rollout: %u workgroups exceed the %d counter slots", grid.x,
-                stat_slots(h->n));
-  if (timed && (rc = timing_mark(h, st, 1))) return rc;
-  hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, R, q, h->g0, E,
-                     h->stats, h->err);
-  HIP_TRY(hipGetLastError());
-  return timed ? timing_mark(h, st, 2) : TG_OK;
-}
 }  // namespace
 
 extern "C" {
@@ -2148,7 +1678,7 @@ int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t*
   hipStream_t st = (hipStream_t)stream;
   TgOne* const d = h->one_dev;
   const StepIO io{nullptr, d->obs, &d->reward, &d->valid, &d->done, nullptr, POL_IMMEDIATE,
-                  (uint64_t)(int64_t)action, 0};
+                  (uint64_t)(int64_t)action, 0, h->tstep++};
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   hipLaunchKernelGGL((k_step<false, false, POL_IMMEDIATE>), dim3(1), dim3(BLOCK), 0, st, h->S,
                      h->n, h->L, h->grid, io, q, h->g0, h->stats, h->err);
@@ -2180,12 +1710,26 @@ int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) 
       return fail(TG_E_NOMEM, "tg_*1_py: pinned stream state");
     HIP_TRY(hipHostGetDevicePointer((void**)&h->py_dev, h->py, 0));
   }
-  memcpy(h->py, st, sizeof(tg_pystate));
+  if (!h->pyc) {
+    if (hipMalloc((void**)&h->pyc, sizeof(uint32_t) * PY_GENS * MT_N) != hipSuccess)
+      return fail(TG_E_NOMEM, "tg_*1_py: stream cache");
+    h->py_warm = false;
+  }
+  // the device's cached generations serve the call iff the caller's state is the one the last
+  // call returned (no other draws on the stream since: the user's own, another env's)
+  const bool warm = h->py_warm && memcmp(st, &h->py_last, sizeof(tg_pystate)) == 0;
+  if (!warm) memcpy(h->py, st, sizeof(tg_pystate));
+  // a step's tstep is its index; a reset's, the next step's (the new episode's start)
+  const uint32_t tstep = RESET ? h->tstep : h->tstep++;
+  h->py_warm = false;  // until the call has returned
   hipLaunchKernelGGL(k_py1<RESET>, dim3(1), dim3(64), 0, stream, h->S, h->L, h->grid, (int)action,
-                     h->py_dev, h->one_dev, h->stats, h->err);
+                     h->py_dev, warm ? h->pyc : nullptr, h->pyc, st->index, (int)st->has_gauss,
+                     st->gauss_next, h->one_dev, tstep, h->stats, h->err);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(stream));
   memcpy(st, h->py, sizeof(tg_pystate));
+  h->py_last = *st;
+  h->py_warm = true;
   return TG_OK;
 }
 }  // namespace
@@ -2226,20 +1770,6 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
     if (hipMalloc((void**)&h->obs_scratch, sizeof(double) * 9 * (size_t)n) != hipSuccess)
       return fail(TG_E_NOMEM, "tg_rollout: obs scratch");
   const bool ar = (flags & TG_STEP_AUTORESET) != 0;
-  if (h->mode == TG_MODE_ASYNC) {
-    constexpr int32_t KMAX = 0xFFFF;  // k_rollout counts an env's steps in 16 bits
-    for (int32_t s0 = 0; s0 < steps; s0 += KMAX) {
-      const int32_t k = steps - s0 < KMAX ? steps - s0 : KMAX;
-      const size_t off = (size_t)s0 * (size_t)n;
-      const RollIO R{StepIO{actions ? actions + off : nullptr, obs ? obs + off * 9 : h->obs_scratch,
-                            reward + off, valid + off, done + off, nullptr, policy, action_seed,
-                            t0 + s0},
-                     k, obs != nullptr};
-      const int rc = launch_rollout(h, R, ar, (hipStream_t)stream);
-      if (rc) return rc;
-    }
-    return TG_OK;
-  }
   for (int32_t s = 0; s < steps; ++s) {
     const StepIO io{actions ? actions + (size_t)s * n : nullptr,
                     obs ? obs + (size_t)s * n * 9 : h->obs_scratch,
@@ -2304,7 +1834,7 @@ int tg_errors(tg_batch* h, uint32_t* out, void* stream) {
 
 int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
   BIND(h);
-  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT && mode != TG_MODE_ASYNC)
+  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT)
     return fail(TG_E_INVAL, "tg_set_mode: unknown mode %d", mode);
   h->mode = mode;
   (void)run_blocks;  // reserved
@@ -2411,7 +1941,10 @@ int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, dou
     }
   }
   if (ang) HIP_TRY(hipMemcpy(ang, h->S.ang, sizeof(double2) * n, hipMemcpyDeviceToHost));
-  if (ep) HIP_TRY(hipMemcpy(ep, h->S.ep, sizeof(int2) * n, hipMemcpyDeviceToHost));
+  if (ep) {  // (return, start step) -> (return, length): the steps since the start
+    HIP_TRY(hipMemcpy(ep, h->S.ep, sizeof(int2) * n, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; ++i) ep[2 * i + 1] = (int32_t)(h->tstep - (uint32_t)ep[2 * i + 1]);
+  }
   if (mt_pos) {
     // CPython's index into the generation holding the position
     for (int64_t i = 0; i < n; ++i) mt_pos[i] = (st[(size_t)i].w & MT_POS_MASK) % MT_N;
@@ -2478,8 +2011,13 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(h->S.st4, st.data(), sizeof(uint4) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->S.ang, ang, sizeof(double2) * n, hipMemcpyHostToDevice));
-  if (ep) HIP_TRY(hipMemcpy(h->S.ep, ep, sizeof(int2) * n, hipMemcpyHostToDevice));
-  else HIP_TRY(hipMemset(h->S.ep, 0, sizeof(int2) * n));
+  {  // (return, length) -> (return, start step)
+    std::vector<int2> e2((size_t)n);
+    for (int64_t i = 0; i < n; ++i)
+      e2[(size_t)i] = ep ? make_int2(ep[2 * i], (int32_t)(h->tstep - (uint32_t)ep[2 * i + 1]))
+                         : make_int2(0, (int32_t)h->tstep);
+    HIP_TRY(hipMemcpy(h->S.ep, e2.data(), sizeof(int2) * n, hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMemcpy2D(h->S.mt, sizeof(uint32_t) * MT_WORDS, mt, sizeof(uint32_t) * MT_N,
                       sizeof(uint32_t) * MT_N, (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_gen_codes, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n);

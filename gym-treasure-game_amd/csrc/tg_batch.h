@@ -59,9 +59,9 @@ struct tg_batch {
   tg::Level L{};
   uint32_t* grid = nullptr;  // bordered cell grid, padded to whole words
   uint32_t* genrand = nullptr;
-  uint32_t* gotab = nullptr;  // GoTable (tg_core.h go_lookup), W * H * 32 entries
-  int cus = 0;               // compute units (k_rollout sizes its workgroups to fill them once)
-  int ro_per_cu = 0;         // k_rollout workgroups resident per CU (occupancy API, first use)
+  // GoTable (tg_core.h go_lookup): W * H * 32 entries
+  uint32_t* gotab = nullptr;
+  int cus = 0;  // compute units
   tg::Soa S{};
   tg_episode* eps = nullptr;
   int32_t* eps_count = nullptr;
@@ -77,6 +77,7 @@ struct tg_batch {
   uint32_t* refill = nullptr;  // stale MT halves to regenerate in k_run (compact mode)
   uint8_t* nrefill = nullptr;
   int parity = 0;  // which half of wctr this compact step counts in
+  uint32_t tstep = 0;  // steps taken by the handle (mod 2^32): S.ep holds each episode's start step
   int64_t shard_cap = 0;
   int timing_every = 0;        // HIP-event timing of every k-th step launch (0: off)
   uint64_t timing_calls = 0;   // step launches since timing was enabled
@@ -91,6 +92,9 @@ struct tg_batch {
   tg::TgOne* one_dev = nullptr;        //   (its device-side address)
   tg_pystate* py = nullptr;            // tg_step1_py / tg_reset1_py's stream state (pinned)
   tg_pystate* py_dev = nullptr;
+  uint32_t* pyc = nullptr;  // the Python stream's generation + 2 successors, on the device
+  tg_pystate py_last{};     // the state the last tg_*1_py call returned
+  bool py_warm = false;     // pyc matches py_last
   tg::RenderState* rs = nullptr;   // tg_render_init
 };
 

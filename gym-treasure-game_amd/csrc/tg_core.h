@@ -127,7 +127,7 @@ TG_HD int floordiv48(int a) { return div48(a + 16 * S) - 16; }              // -
 //   regenerated: MT_HALF_GENS twists in sequence from the last generation of the half the
 //   lane is in (twist_half); the env's state word carries MT_STALE meanwhile.  The kernels
 //   regenerate it later, a whole wavefront per env, coalesced, the chained twists in LDS
-//   (tg_amd.hip wave_twist_gens: k_run's refill queue, k_reset, k_rollout).  A launch that
+//   (tg_amd.hip wave_twist_gens: k_run's refill queue, k_reset).  A launch that
 //   would enter a stale half (> MT_HALF draws since the refill) regenerates it first, per
 //   lane.  Seeding (init_by_array) fills the ring's last generation; 2 x MT_HALF_GENS twists
 //   then give generations 1 .. 2 x MT_HALF_GENS, pos 0 (init_mt).
@@ -1090,37 +1090,17 @@ TG_HD int ladder_plain_limit(const Map& m, const Env& e) {
 // tick's precondition), up_clear (the jump ticker's rise).  Same outcomes and draws as
 // policy<K> + tick<prims_of(K)>.
 // ==========================================================================================
-#ifndef TG_AIR_NBHD
-#define TG_AIR_NBHD 1  // 0: every predicate through Map's pixel probes (A/B builds)
-#endif
-#ifndef TG_AIR_CACHE
-#define TG_AIR_CACHE 1  // 0: AirCells rebuilt every tick (A/B builds)
-#endif
 // ac: the option loop's AirCells, rebuilt only when the player leaves its window (a jump
 // changes cell column or row every ~12 ticks)
 template <int K, class R>
 TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng, AirCells& ac) {
   constexpr int DIR = (K == O_JUMP_LEFT || K == O_DOWN_LEFT) ? -1 : 1;
   constexpr bool JUMP = K == O_JUMP_LEFT || K == O_JUMP_RIGHT;
-#if defined(__HIP_DEVICE_COMPILE__) && defined(TG_DIAG_MARK)
-  asm volatile("; AIR_TICK_BEGIN");
-#endif
-#if TG_AIR_NBHD
-#if TG_AIR_CACHE
   if (!ac.holds(Map::dc_of(e.f), e.px, e.py)) ac = m.air_cells(Map::dc_of(e.f), e.px, e.py);
-#else
-  ac = m.air_cells(Map::dc_of(e.f), e.px, e.py);
-#endif
   const bool cf0 = ac.can_fall(e.px, e.py);
   const bool fwd = ac.side(e.px, e.py, DIR);
   const bool bwd = JUMP ? ac.side(e.px, e.py, -DIR) : false;
   const bool uc = ac.up_clear(e.px, e.py);
-#else
-  const bool cf0 = m.can_fall(e);
-  const bool fwd = m.can_go_side(e, DIR);
-  const bool bwd = JUMP ? m.can_go_side(e, -DIR) : false;
-  const bool uc = m.up_clear(e);
-#endif
   int mv = 0;  // the primitive: -1 LEFT, +1 RIGHT, 0 NOP
   if (close_x(e, o.tx)) {
     if (!cf0) o.done = true;
@@ -1141,11 +1121,7 @@ TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng, AirCell
   }
   e.px += xd;
   if (yd > 0) {  // IM/:341-348 (e.px moved by <= 4: still inside the AirCells)
-#if TG_AIR_NBHD
     const uint32_t cf = ac.can_fall4(e.px, e.py);
-#else
-    const uint32_t cf = m.can_fall4(Map::dc_of(e.f), e.px, e.py);
-#endif
     if (cf & 1u) {
       int dist = yd;
       for (int k = yd - 1; k >= 1; --k)
@@ -1155,9 +1131,6 @@ TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng, AirCell
   }
   e.py += yd;
   pickups(L, e);
-#if defined(__HIP_DEVICE_COMPILE__) && defined(TG_DIAG_MARK)
-  asm volatile("; AIR_TICK_END");
-#endif
   return -1;  // STEP_REWARD (no JUMP after the first tick)
 }
 
@@ -1167,7 +1140,6 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
                         StepResult& r) {
   r.ran = 1;
   Opt o{0, false, false};
-#ifndef TG_NO_PLAIN
   if constexpr (K == O_GO_LEFT || K == O_GO_RIGHT) {
     constexpr int DIR = K == O_GO_LEFT ? -1 : 1;
     int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
@@ -1261,7 +1233,6 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
     } while (!o.done);
     return;
   }
-#endif
   do {
     rng.reserve(K == O_INTERACT ? L.interact_draws : TICK_DRAWS);
     const int prim = policy<K>(L, m, e, o);

@@ -37,10 +37,7 @@
 
 namespace tg {
 
-#ifndef TG_RENDER_BLOCK
-#define TG_RENDER_BLOCK 256  // 4 waves
-#endif
-constexpr int RBLOCK = TG_RENDER_BLOCK;
+constexpr int RBLOCK = 256;  // 4 waves (1,024 threads lost 1.5-9 ms)
 
 struct RenderState {
   int Wpx = 0, Hpx = 0, CH = 0;  // pixels, 16-B chunks per row
@@ -60,36 +57,16 @@ void render_free(RenderState* rs) {
 
 namespace {
 
-#ifndef TG_RENDER_STORE
-#define TG_RENDER_STORE 1  // frame stores: 0 plain, 1 non-temporal (streamed once, never
-#endif                     // re-read here); A/B only: 2 sc1, 3 sc0 sc1, 4 nt sc1
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// frame stores are non-temporal: streamed once, never re-read here (plain, sc1, sc0 sc1 and
+// nt sc1 stores measured equal or up to 0.8 ms slower)
 __device__ __forceinline__ void store16(uint4* p, const uint4 x) {
   u32x4 v = {x.x, x.y, x.z, x.w};
-#if TG_RENDER_STORE == 0
-  *reinterpret_cast<u32x4*>(p) = v;
-#elif TG_RENDER_STORE == 1
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-#elif TG_RENDER_STORE == 2
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-#elif TG_RENDER_STORE == 3
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
-#else
-  asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
-#endif
 }
 
-#ifndef TG_RENDER_DIAG_COPY
-#define TG_RENDER_DIAG_COPY 0
-#endif
-#ifndef TG_RENDER_DIAG_NOCOMPOSE
-#define TG_RENDER_DIAG_NOCOMPOSE 0  // DIAGNOSTIC ONLY (wrong frames): store the static chunk
-#endif                               // where items are, to price the composition
-#ifndef TG_RENDER_G
-#define TG_RENDER_G 4  // envs per workgroup: each static-layer chunk is loaded once per G frames
-#endif
-constexpr int RG = TG_RENDER_G;
+constexpr int RG = 4;  // envs per workgroup: each static-layer chunk is loaded once per RG frames
 constexpr int MAX_W = 128;  // cell columns (levels are at most 120 wide, tg_level.h)
 
 // block = (group of RG envs, band of 48 rows): lane l of wave w renders chunks 64w + l,
@@ -103,10 +80,6 @@ __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __
   __shared__ uint32_t live[RG];
   __shared__ uint16_t rows[RG][RS];  // items covering each row of the band, per env
   __shared__ uint16_t sel[RG][MAX_W];  // each cell's source, per env
-#ifdef TG_RENDER_LDS_PAD  // A/B only: cap the workgroups per CU
-  __shared__ uint8_t pad[TG_RENDER_LDS_PAD];
-  if (threadIdx.x == 0) pad[blockIdx.x % TG_RENDER_LDS_PAD] = 0;
-#endif
   const int64_t grp = blockIdx.x / A.H;
   const int band = (int)(blockIdx.x - grp * A.H);
   const int ylo = band * RS;
@@ -154,17 +127,7 @@ __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __
     uint4* dst = base + c;
     for (int k = 0; k < ne; ++k, dst += frame_chunks) {
       const uint32_t rm = rows[k][r];
-#if TG_RENDER_DIAG_COPY  // DIAGNOSTIC ONLY (wrong frames): the static chunk everywhere
-      (void)rm;
-      (void)sel;
-      store16(dst, v);
-#elif TG_RENDER_DIAG_NOCOMPOSE
-      const uint32_t hit = rm ? chunk_items(lay[k], rm, q) : 0u;
-      (void)sel;
-      store16(dst, hit ? make_uint4(v.x ^ hit, v.y, v.z, v.w) : v);
-#else
       store16(dst, rm ? render_chunk(A, lay[k], rm, sel[k], band, r, q, v) : v);
-#endif
     }
   }
 }

@@ -295,8 +295,7 @@ class TreasureGameVec:
     def set_mode(self, mode="compact", run_blocks=0):
         """Step implementation: "compact" (two-pass, default) or "direct" (one lane per env
         runs in place); both are bit-identical."""
-        m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT,
-             "async": _lib.TG_MODE_ASYNC}[mode]
+        m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT}[mode]
         check(self._L.tg_set_mode(self.handle, m, int(run_blocks)), "tg_set_mode")
 
     def set_episode_capacity(self, cap):
@@ -439,6 +438,67 @@ class GpuOption:
         return "<%s (GPU)>" % self.name
 
 
+class _GlobalMT:
+    """The global ``random``'s MT19937 state read and written in place.
+
+    ``random.getstate()`` + packing and unpacking + ``random.setstate`` cost ~50 us per call
+    (a 625-int tuple each way); the drop-in exchanges the state every call.  CPython 3's
+    ``_random.Random`` object is ``{PyObject_HEAD; int index; uint32_t state[624];}``
+    (Modules/_randommodule.c), so two ``memmove`` of 2.5 KB do the same job, and
+    ``gauss_next`` is the Python-level attribute ``random.Random`` keeps.  Enabled only after
+    the layout is checked against ``random.getstate()`` (type sizes and the words, both
+    directions); otherwise ``ok`` is False and the tuple path runs."""
+
+    def __init__(self):
+        self.ok = False
+        try:
+            self.ok = self._check()
+        except Exception:
+            self.ok = False
+
+    def _check(self):
+        inst = random._inst
+        base_t = type(inst).__mro__[-2]  # _random.Random, the C base
+        head = object.__basicsize__
+        if base_t.__basicsize__ < head + 4 + 4 * 624:
+            return False
+        self._inst = inst
+        self._index = head
+        self._state = head + 4
+        probe = random.getstate()
+        try:
+            random.random()  # a state whose index is not 0 or 624
+            st = random.getstate()
+            ps = _lib.PyState()
+            self.load(ps)
+            if list(ps.mt) + [ps.index] != list(st[1]):
+                return False
+            ps.mt[0] ^= 1  # round trip: a store must be what setstate would give
+            self.store(ps)
+            if random.getstate()[1] != tuple(list(ps.mt) + [ps.index]):
+                return False
+        finally:
+            random.setstate(probe)
+        return True
+
+    def load(self, ps):
+        base = id(self._inst)
+        ctypes.memmove(ctypes.addressof(ps.mt), base + self._state, 4 * 624)
+        ps.index = ctypes.c_int.from_address(base + self._index).value
+        g = self._inst.gauss_next
+        ps.has_gauss = g is not None
+        ps.gauss_next = 0.0 if g is None else g
+
+    def store(self, ps):
+        base = id(self._inst)
+        ctypes.memmove(base + self._state, ctypes.addressof(ps.mt), 4 * 624)
+        ctypes.c_int.from_address(base + self._index).value = ps.index
+        self._inst.gauss_next = ps.gauss_next if ps.has_gauss else None
+
+
+_GLOBAL_MT = _GlobalMT()
+
+
 class TreasureGame:
     """Drop-in for the reference ``TreasureGame`` (treasure_game.py:54-114), one env on the GPU.
 
@@ -494,6 +554,9 @@ class TreasureGame:
     _WORDS = struct.Struct("625I")  # tg_pystate's mt[624] + index
 
     def _load_global(self):
+        if _GLOBAL_MT.ok:
+            _GLOBAL_MT.load(self._py)
+            return None
         st = random.getstate()
         self._WORDS.pack_into(self._py, 0, *st[1])
         g = st[2]
@@ -502,11 +565,15 @@ class TreasureGame:
         return st
 
     def _store_global(self):
+        if _GLOBAL_MT.ok:
+            _GLOBAL_MT.store(self._py)
+            return
         random.setstate((3, self._WORDS.unpack_from(self._py, 0),
                          self._py.gauss_next if self._py.has_gauss else None))
 
     def _reset_py(self, obs):
-        st = self._load_global()
+        st = random.getstate()
+        self._load_global()
         check(self._vec._L.tg_reset1_py(self._vec.handle, ctypes.byref(self._py),
                                         obs.ctypes.data, self._vec._stream()), "tg_reset1_py")
         # The reset's draws (IM/:55-73): two uniform(), then gauss twice.  Their stream position

@@ -58,8 +58,6 @@ extern "C" {
 #define TG_ERR_RENDER (1u << 28)   /* render: a handle shaft end point within 1e-9 of an int()
                                       boundary (libm watch), or a shaft off the screen */
 #define TG_ERR_WINDOW (1u << 29)  /* a lane drew past its staged draw codes (a bound broken: bug) */
-#define TG_ERR_STALL (1u << 31)   /* TG_MODE_ASYNC tg_rollout: a workgroup's queues stopped
-                                      making progress (a bookkeeping bug; the launch gave up) */
 
 /* step flags */
 #define TG_STEP_AUTORESET 1u       /* reset() an env right after a step that returned done */
@@ -189,12 +187,8 @@ int tg_errors(tg_batch *h, uint32_t *or_of_flags, void *stream);
  *   TG_MODE_DIRECT: one k_step lane per env runs its option in place. */
 #define TG_MODE_DIRECT 0
 #define TG_MODE_COMPACT 1
-/*   TG_MODE_ASYNC: tg_step as TG_MODE_COMPACT; tg_rollout runs all K steps in ONE launch
- *     (k_rollout): each workgroup owns a contiguous block of envs and its waves pop 64-env
- *     batches of one option from per-option queues in LDS, so envs advance at their own pace
- *     with no step barrier.  Outputs and states identical; completed episodes are queued in a
- *     different order. */
-#define TG_MODE_ASYNC 2
+/*   (Round 2's TG_MODE_ASYNC, all K steps of tg_rollout in one persistent launch, was exact
+ *     but slower, 0.214 vs 0.142 ms per step, and was removed in round 3: DESIGN.md §9.1.) */
 int tg_set_mode(tg_batch *h, int mode, int run_blocks);
 
 /* HIP-event timing of every `every`-th step launch (tg_step, tg_rollout's launches; 0 = off):

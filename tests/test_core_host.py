@@ -166,3 +166,4 @@ def test_core_gotable_matches_direct(hostcheck, level, policy):
     assert_same(direct, table)
     np.testing.assert_array_equal(direct["ticks"], table["ticks"])
 
+

@@ -354,7 +354,7 @@ def test_checkpoint_restore_continues_bit_exact(tg, oracle, tmp_path, mode):
     b.close()
 
 
-@pytest.mark.parametrize("mode", MODES + ["async"])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("policy", ["uniform", "masked"])
 def test_rollout_equals_step_loop_and_oracle(tg, oracle, mode, policy):
     """tg_rollout (the on-device policy inside the step kernels, K steps per call, continued

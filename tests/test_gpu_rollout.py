@@ -1,9 +1,10 @@
-"""TG_MODE_ASYNC's tg_rollout (k_rollout: every env's K steps in one launch, per-workgroup
-option queues, no step barrier) against the per-step kernels, bit for bit: every output row,
-the final env states and MT streams, and the SET of completed episodes (their queue order is
-the one thing that differs).  Sizes up to the bench's 1M envs (2,048 envs per workgroup, the
-largest the LDS bitmaps hold), levels whose options cross MT generations inside one step, and
-batches that enter the rollout with stale MT halves left by tg_step."""
+"""tg_rollout (K steps per call, the synthetic policy evaluated inside k_classify: no action
+launch, no host round trip) against K x (tg_policy_actions + tg_step), bit for bit: every
+output row, the final env states and MT streams, and the completed episodes.  Ragged batch
+sizes up to the bench's 1M envs, levels whose options cross MT generations inside one step,
+rollouts split over several calls, and batches that enter the rollout with stale MT halves
+left by tg_step.  (Round 2's one-launch TG_MODE_ASYNC rollout, slower, was removed in round 3:
+DESIGN.md §9.1.)"""
 import os
 
 import numpy as np
@@ -21,17 +22,17 @@ def episodes_sorted(vec):
 
 
 def run_pair(tg, n, k, policy, pre_steps=0, level=None, seed=5, a0=0xA5A5, chunks=(None,)):
-    """the same batch through K x (tg_policy_actions + tg_step) and through async tg_rollout
-    (in `chunks` calls); returns both sides' outputs, final states and sorted episodes"""
+    """the same batch through K x (tg_policy_actions + tg_step) and through tg_rollout (in
+    `chunks` calls); returns both sides' outputs, final states and sorted episodes"""
     ld = None if level is None else os.path.join(LEVELS, level)
     sides = []
-    for mode in ("compact", "async"):
-        v = tg.TreasureGameVec(n, seed=seed, autoreset=True, mode=mode, level_dir=ld)
+    for side in ("steps", "rollout"):
+        v = tg.TreasureGameVec(n, seed=seed, autoreset=True, level_dir=ld)
         v.reset()
         for t in range(pre_steps):  # leaves stale MT halves for the rollout to start from
             v.step(v.policy_actions(t, a0, policy))
         outs = []
-        if mode == "compact":
+        if side == "steps":
             for t in range(pre_steps, pre_steps + k):
                 act = v.policy_actions(t, a0, policy).clone()
                 o, r, va, d, _ = v.step(act)
@@ -67,20 +68,20 @@ def check_pair(sides, n, k, errors=0):
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 1000, 70001])
-def test_async_rollout_ragged_batches(tg, n):
-    """batches that leave a partial workgroup / partial bitmap word; rollouts in 3 calls"""
+def test_rollout_ragged_batches(tg, n):
+    """batches that leave a partial wave / workgroup; rollouts in 3 calls"""
     k = 21
     check_pair(run_pair(tg, n, k, "uniform", chunks=(7, 1, 13)), n, k)
 
 
-def test_async_rollout_after_steps(tg):
-    """envs enter the rollout with MT_STALE halves left by tg_step (the refill queue first)"""
+def test_rollout_after_steps(tg):
+    """envs enter the rollout with MT_STALE halves left by tg_step"""
     n, k = 50000, 30
     check_pair(run_pair(tg, n, k, "masked", pre_steps=9), n, k)
 
 
 @pytest.mark.parametrize("level", ["corridor", "gen2", "exit", "cascade"])
-def test_async_rollout_levels(tg, level):
+def test_rollout_levels(tg, level):
     """corridor: go options of ~650 draws (two MT generation crossings inside one step).  Some
     of its envs get stuck against an end wall in an option that never ends (the reference
     would loop forever; the kernels stop at TICK_CAP and flag E_TICKCAP): both sides must
@@ -90,14 +91,23 @@ def test_async_rollout_levels(tg, level):
                errors=(1 << 24) if level == "corridor" else 0)
 
 
-def test_async_rollout_no_obs_and_no_autoreset(tg):
-    """obs=None (the scratch row) and auto-reset off: the other k_rollout instantiation"""
+def test_rollout_no_obs_and_no_autoreset(tg):
+    """obs=None (the scratch row) and auto-reset off, against the per-step API"""
     n, k, a0 = 20000, 20, 77
     res = []
-    for mode in ("compact", "async"):
-        v = tg.TreasureGameVec(n, seed=9, autoreset=False, mode=mode)
+    for side in ("steps", "rollout"):
+        v = tg.TreasureGameVec(n, seed=9, autoreset=False)
         v.reset()
-        r = v.rollout(k, t0=0, action_seed=a0, policy="uniform", obs=False)
+        if side == "steps":
+            outs = []
+            for t in range(k):
+                act = v.policy_actions(t, a0, "uniform").clone()
+                _, rw, va, d, _ = v.step(act)
+                outs.append({"reward": rw.clone(), "valid": va.clone(), "done": d.clone(),
+                             "actions": act})
+            r = {key: torch.stack([x[key] for x in outs]) for key in outs[0]}
+        else:
+            r = v.rollout(k, t0=0, action_seed=a0, policy="uniform", obs=False)
         res.append((r, v.read_state(mt=True), v.observe().clone()))
         v.close()
     (ra, sa, oa), (rb, sb, ob) = res
@@ -109,7 +119,7 @@ def test_async_rollout_no_obs_and_no_autoreset(tg):
 
 
 @pytest.mark.parametrize("policy", ["uniform", "masked"])
-def test_async_rollout_1m_envs(tg, policy):
-    """the bench's size: 1M envs, 2,048 per workgroup"""
+def test_rollout_1m_envs(tg, policy):
+    """the bench's size: 1M envs"""
     n, k = 1 << 20, 24
     check_pair(run_pair(tg, n, k, policy), n, k)
