@@ -64,15 +64,16 @@ EP_CAP = 4096          # episode records gathered per rank per step of a drain i
 #     valid env: worklist index 4 + state 16 + angles 16 + episode 8 written (44)
 #     stale MT half: its refill-list entry 4 written (a half is MT_HALF_GENS generations)
 #   k_run, valid env: the worklist row 44 read; state 16 + angles 16 + episode 8 + obs 72 +
-#     rows 6 written (118); random() draw: its 1-B code (tg_core.h draw_code); MT generation
-#     regenerated (tg_core.h: halves of MT_HALF_GENS = 8 generations, chained in LDS): 624
-#     words + 312 codes written, an eighth of the source generation's 624 words and of the
-#     4-B refill entry read
+#     rows 6 written (118); random() draw: its 1-B code (tg_core.h draw_code)
+#   k_regen (every 16 compact steps, tg_regenerate), per MT generation regenerated (tg_core.h:
+#     halves of MT_HALF_GENS = 8 generations, chained in LDS): 624 words + 312 codes written,
+#     an eighth of the source generation's 624 words, of the 4-B list entry and of the env's
+#     4-B state word read and written
 #   k_step (direct mode): one kernel, the same without the worklist round trip
 MT_HALF_GENS = 8
 CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 78, 44, 4 / MT_HALF_GENS
 RUN_VALID, RUN_DRAW = 162, 1
-RUN_REGEN = 2496 + 312 + (2496 + 4) / MT_HALF_GENS
+REGEN_GEN = 2496 + 312 + (2496 + 4 + 8) / MT_HALF_GENS
 DIRECT_ENV, DIRECT_INVALID, DIRECT_VALID = 44, 78, 118
 DIRECT_REGEN = 2496 + 312 + 2496 / MT_HALF_GENS
 BYTES_DRAW = RUN_DRAW
@@ -87,17 +88,17 @@ MT_DRAWS_PER_GEN = 312  # random() values per MT19937 generation
 
 
 def alg_bytes(st, mode="compact"):
-    """algorithmic bytes of the counted steps per kernel: (first, second) = (k_classify, k_run),
-    or (0, k_step) in the direct mode"""
+    """algorithmic bytes of the counted steps per kernel: (k_classify, k_run, k_regen), or
+    (0, k_step, 0) in the direct mode (k_step regenerates the halves its envs left itself)"""
     inval = st["steps"] - st["valid_steps"]
     if mode == "direct":
         return 0, (DIRECT_ENV * st["steps"] + DIRECT_INVALID * inval +
                    DIRECT_VALID * st["valid_steps"] + BYTES_DRAW * st["draws"] +
-                   DIRECT_REGEN * st["regens"])
+                   DIRECT_REGEN * st["regens"]), 0
     cls = (CLS_ENV * st["steps"] + CLS_INVALID * inval + CLS_VALID * st["valid_steps"] +
            CLS_REGEN * st["regens"])
-    run = RUN_VALID * st["valid_steps"] + RUN_DRAW * st["draws"] + RUN_REGEN * st["regens"]
-    return cls, run
+    run = RUN_VALID * st["valid_steps"] + RUN_DRAW * st["draws"]
+    return cls, run, REGEN_GEN * st["regens"]
 
 
 def survey_bytes(st):
@@ -414,6 +415,9 @@ class Runner:
                     self.h, ACTION_SEED, t + j, self.pol, self.p(self.pre[j]), self.stream),
                     "actions")
         self.drain_all(log=False)  # the timed region's records are its own
+        # no MT regeneration pending from the untimed steps: the timed region does exactly the
+        # regeneration work of its own steps (the deferred lists drained again at its end)
+        self.tg._lib.check(self.L.tg_regenerate(self.h, self.stream), "tg_regenerate")
         torch.cuda.synchronize(self.dev)
         self.log.reset()
         vec = self.vec
@@ -427,6 +431,7 @@ class Runner:
         for _ in range(steps):
             self.step(t)
             t += 1
+        self.tg._lib.check(self.L.tg_regenerate(self.h, self.stream), "tg_regenerate")
         torch.cuda.synchronize(self.dev)
         if self.world > 1:
             dist.barrier()
@@ -487,7 +492,11 @@ def step_line(args, runner, dt, st, node, world, total):
     step_s = st["kernel_ms"] / 1e3 / timed      # k_classify + k_run of a timed launch
     run_s = st["run_ms"] / 1e3 / timed          # k_run alone
     cls_s = step_s - run_s
-    cls_b, run_b = (b / launches for b in alg_bytes(st, args.mode))
+    cls_b, run_b, regen_b = (b / launches for b in alg_bytes(st, args.mode))
+    # k_regen: its own event pairs; per step = per launch x launches per step
+    rl = st.get("regen_launches", 0)
+    regen_launch_s = st["regen_ms"] / 1e3 / st["regen_timed"] if st.get("regen_timed") else 0.0
+    regen_s = regen_launch_s * rl / launches
     surv = survey_bytes(st) / launches
     d = node["draws"] / max(node["steps"], 1)
     regens = st["regens"] / launches
@@ -525,14 +534,20 @@ def step_line(args, runner, dt, st, node, world, total):
     kernels = {"run": run_k}
     if args.mode == "compact":
         kernels["classify"] = kern("k_classify", cls_b, cls_s, cls_pmc)
+        if rl:
+            regen_pmc = next((v for k, v in kp.items() if k.split("<")[0] == "k_regen"), None)
+            kernels["regen"] = kern("k_regen", regen_b * launches / rl, regen_launch_s, regen_pmc)
+            kernels["regen"].update({"launches": rl, "steps_per_launch": launches / rl})
+    all_b, all_s = cls_b + run_b + regen_b, step_s + regen_s
     roof["step"] = {"kernel": "tg_step = " + (" + ".join(
-                        ["k_classify", "k_run"] if args.mode == "compact" else ["k_step"])),
-                    "alg_bytes_per_launch": cls_b + run_b, "kernel_ms": step_s * 1e3,
-                    "achieved": (cls_b + run_b) / step_s / 1e9,
-                    "frac": (cls_b + run_b) / step_s / 1e9 / HBM_PEAK_GBS,
+                        ["k_classify", "k_run", "k_regen / 16 steps"] if args.mode == "compact"
+                        else ["k_step"])),
+                    "alg_bytes_per_launch": all_b, "kernel_ms": all_s * 1e3,
+                    "achieved": all_b / all_s / 1e9,
+                    "frac": all_b / all_s / 1e9 / HBM_PEAK_GBS,
                     "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                     "alg_bytes_per_launch_survey": surv,
-                    "frac_survey": surv / step_s / 1e9 / HBM_PEAK_GBS,
+                    "frac_survey": surv / all_s / 1e9 / HBM_PEAK_GBS,
                     "kernels": kernels}
     return {
         "ticks_per_s": node["ticks"] / dt,

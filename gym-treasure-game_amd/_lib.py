@@ -31,7 +31,7 @@ NUM_ACTIONS = 9
 EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_step1", "tg_step1_py",
            "tg_reset1_py", "tg_rollout",
            "tg_available_mask",
-           "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing",
+           "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing", "tg_regenerate",
            "tg_set_episode_capacity", "tg_predicate_table",
            "tg_get_stats", "tg_stats_reset", "tg_read_state", "tg_write_state", "tg_render_init", "tg_frame_shape",
            "tg_render", "tg_last_error", "tg_version")
@@ -58,7 +58,8 @@ class Stats(ctypes.Structure):
                 ("launches", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("regens", ctypes.c_int64),
                 ("wave_ticks", ctypes.c_int64), ("timed_launches", ctypes.c_int64),
-                ("run_ms", ctypes.c_double)]
+                ("run_ms", ctypes.c_double), ("regen_ms", ctypes.c_double),
+                ("regen_timed", ctypes.c_int64), ("regen_launches", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -96,6 +97,7 @@ def load():
         "tg_errors": (i32, [P, ctypes.POINTER(u32), P]),
         "tg_set_mode": (i32, [P, i32, i32]),
         "tg_set_timing": (i32, [P, i32]),
+        "tg_regenerate": (i32, [P, P]),
         "tg_set_episode_capacity": (i32, [P, i32]),
         "tg_predicate_table": (i32, [P, i32, i32, i32, i32, u32, P, P]),
         "tg_get_stats": (i32, [P, ctypes.POINTER(Stats)]),

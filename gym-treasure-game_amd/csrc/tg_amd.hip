@@ -166,6 +166,7 @@ struct RngCodes {
   uint32_t left;     // draws left in the window
   uint32_t nxc;      // the next draw's code (read one draw ahead)
   uint32_t stale;    // word offset (0 / 624) of the half that is two generations behind, or NONE
+  uint32_t tag;      // the state word's MT_STALE | MT_LISTED bits on entry
   uint32_t draws;
   uint32_t regens;   // halves this lane regenerated itself (regen_half)
   bool primed, loaded, entered;  // entered: a half was entered in this launch (as tg::Rng)
@@ -175,6 +176,7 @@ struct RngCodes {
         m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_win)),
         pos(state & MT_POS_MASK), n(0u), rd(0u), left(0u), nxc(0u),
         stale((state & MT_STALE) ? (uint32_t)MT_HALF - mt_half(state & MT_POS_MASK) : NONE),
+        tag(state & (MT_STALE | MT_LISTED)),
         draws(0u), regens(0u), primed(false), loaded(false), entered(false) {}
 
   // fold the draws taken since the window start into pos (a window is < MT_HALF / 2 draws, so
@@ -321,17 +323,14 @@ struct RngCodes {
     return mt_double(w.x, w.y);
   }
   __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
-  // drain the DMAs (the window is reused as scratch); returns the state word to store
+  // drain the DMAs (the window is reused as scratch); returns the state word to store: the
+  // entry's stale half, still stale, keeps its bits (listed or not); a half left in this launch
+  // is stale and not listed yet; none, if the lane regenerated the stale half itself
   __device__ __forceinline__ uint32_t finish() {
     if (primed) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     sync();
     primed = loaded = false;
-    return pos | (stale != NONE ? MT_STALE : 0u);
-  }
-  // the same when a refill of the half that was stale on entry is already queued
-  __device__ __forceinline__ uint32_t finish_queued() {
-    (void)finish();
-    return pos | (entered ? MT_STALE : 0u);
+    return pos | (stale == NONE ? 0u : entered ? MT_STALE : tag);
   }
 };
 
@@ -553,7 +552,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
   wave_refill(__ballot(stale), S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES, e.mti,
               (lds_u32*)scratch[threadIdx.x >> 6]);
   if (reset) {
-    e.mti &= ~MT_STALE;
+    e.mti &= ~(MT_STALE | MT_LISTED);
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
     S.ep[i] = make_int2(0, (int32_t)tstep);  // the episode starts with the next step
@@ -761,7 +760,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
   wave_refill(need, S.mt + (live ? i : 0) * MT_WORDS,
               S.mc + (live ? i : 0) * MT_CODES, e.mti,
               (lds_u32*)wscr);
-  e.mti &= ~MT_STALE;
+  e.mti &= ~(MT_STALE | MT_LISTED);
   if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats);
   if (live) {
     S.st4[i] = pack(e);
@@ -799,7 +798,7 @@ constexpr RunPos make_runpos() {
 constexpr RunPos kRunPos = make_runpos();
 constexpr int NSEG = O_COUNT * SHARDS;  // segment = run position * SHARDS + shard
 static_assert(NSEG <= 2 * BLOCK, "k_run's prefix: two segments per thread");
-constexpr int NCTR = NSEG + 8;  // the worklist counters, then k_run's refill queues (one per XCD)
+constexpr int NCTR = NSEG;      // the worklist counters
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
 struct Work {
   int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = run position * SHARDS + shard
@@ -815,8 +814,6 @@ struct Work {
   uint8_t* __restrict__ nrefill;  // [n / 64]: entries of classify wave w (no atomics)
   int64_t shard_cap;
 };
-constexpr int REFILL_BLOCKS = 64;  // k_run workgroups beyond the padded worklists (>= 256 idle waves)
-constexpr int REFILL_GRAB = 2;     // refill regions a wave takes from its XCD's queue at a time
 // worklist order = the order the chunks' loads reach HBM at the kernel's start (all option
 // waves are resident at once and issue their loads together): the jump waves first, whose
 // ticks are the slowest in wall time (~2,100 cycles each) and which end the kernel, then the
@@ -881,16 +878,19 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     k = option_index(act);
     runs = k >= 0 && can_run(L, m, e, k);
   }
-  const int bk = runs ? k : -1;  // the env's worklist  // halves left in the previous step (MT_STALE) go on the refill list; k_run's idle waves
-  // regenerate them beside the option loops (a lane that needs one first does it itself)
+  const int bk = runs ? k : -1;  // the env's worklist
+  // halves left stale and not listed yet go on this step's refill list (MT_LISTED); k_regen
+  // regenerates the lists of several steps at once (a lane that needs a half first does it
+  // itself: the ring leaves >= ~2,400 draws of slack, launch_step)
   {
-    const bool stale = live && (e.mti & MT_STALE);
+    const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
     const unsigned long long b = __ballot(stale);
     const int64_t wv = i >> 6;
     if (stale)
       w.refill[wv * 64 + __popcll(b & ((1ull << lane) - 1ull))] =
           (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
     if (lane == 0) w.nrefill[wv] = (uint8_t)__popcll(b);
+    if (stale) e.mti |= MT_LISTED;
   }
   // workgroup-local slots: one LDS atomic per wave and option present in the wave (the
   // wave's lanes are matched option by option)
@@ -918,6 +918,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     my_base = c ? atomicAdd(&w.ctr[(kSegBase[threadIdx.x] + shard) * CTR_STRIDE], c) : 0;
   }
   uint4 s4w = s4;  // the state the worklist copy carries
+  s4w.w = e.mti;
 
   // envs whose option cannot run: reward None, state unchanged (TG/:91-96, OP/:22-23)
   bool dn = false;
@@ -930,7 +931,9 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
     StepResult r{0, 0, (int)dn, 0};
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io, orow);
-    e.mti = rng.finish_queued();  // the stale half, if any, is on the refill list
+    // the stale half keeps its bits unless the auto-reset's draws crossed into it (the Rng then
+    // regenerated it; the half left is stale, not listed)
+    e.mti = rng.entered ? (rng.pos | MT_STALE) : (rng.pos | (e.mti & (MT_STALE | MT_LISTED)));
     draws = rng.draws;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
@@ -1069,7 +1072,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
 #endif
     r.done = is_done(e);
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
-    e.mti = rng.finish_queued();  // MT_STALE if a half was left: the next step refills it
+    e.mti = rng.finish();  // a half left here: MT_STALE, listed by the next k_classify
     draws = rng.draws;
     lregen = (int)rng.regens;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
@@ -1081,55 +1084,6 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     S.ep[i] = ep;
   }
   __builtin_amdgcn_s_setprio(0);
-  // The stale MT halves k_classify listed (per classify wave = region of 64 envs), regenerated
-  // by whichever waves are free: idle waves at once, option waves as soon as their option is
-  // done.  Regions go out REFILL_GRAB at a time from one counter per XCD (blockIdx.x % 8:
-  // regions xcd, xcd + 8, ...), so the twists spread over every wave: with the idle waves alone
-  // a masked step queued its ~130k halves on ~300 waves (~690 us of k_run's ~885, r03a stamps).
-  // An env's half may also be regenerated by its own lane if it needs it first; both write the
-  // same generation.  Every lane of the wave reaches this.
-  {
-    const int xcd = (int)(blockIdx.x & 7u);
-    const int nregions = (int)((n + 63) >> 6);  // k_classify's waves
-    const int nmine = (nregions - xcd + 7) >> 3;  // this XCD's regions: xcd + 8 j, j < nmine
-    int32_t* const rq = w.ctr + (NSEG + xcd) * CTR_STRIDE;
-    const int lane = threadIdx.x & 63;
-    while (true) {
-      int j0 = 0;
-      if (lane == 0) j0 = atomicAdd(rq, REFILL_GRAB);
-      j0 = __builtin_amdgcn_readfirstlane(j0);
-      if (j0 >= nmine) break;
-      const int j1 = j0 + REFILL_GRAB < nmine ? j0 + REFILL_GRAB : nmine;
-      for (int j = j0; j < j1; ++j) {
-        const int rg = xcd + 8 * j;
-        // lane e holds entry e; the twists are software-pipelined: twist e + 1's loads are in
-        // flight while twist e computes and stores (A/B in DESIGN.md §3.3)
-        const int cnt = __builtin_amdgcn_readfirstlane((int)w.nrefill[rg]);
-        regens += cnt;
-        if (!cnt) continue;
-        const uint32_t ent_l = lane < cnt ? w.refill[(int64_t)rg * 64 + lane] : 0u;
-        // entry: env | (the half holding its position) << 31; the other half is regenerated
-        // from the last generation of that one
-        TwistIn t;
-        uint32_t ent = __builtin_amdgcn_readfirstlane(ent_l);
-        auto dst_of = [](uint32_t en) { return (en >> 31) ? 0u : (uint32_t)MT_HALF; };
-        twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
-                                    mt_prev_gen(dst_of(ent))), t);
-        for (int e2 = 0; e2 < cnt; ++e2) {
-          const int64_t env = (int64_t)(ent & 0x7FFFFFFFu);
-          const uint32_t dst = dst_of(ent);
-          TwistIn u = t;
-          if (e2 + 1 < cnt) {
-            ent = __builtin_amdgcn_readlane(ent_l, e2 + 1);
-            twist_load((const glb_u32*)(S.mt + (int64_t)(ent & 0x7FFFFFFFu) * MT_WORDS +
-                                        mt_prev_gen(dst_of(ent))), t);
-          }
-          twist_chain(u, (glb_u32*)(S.mt + env * MT_WORDS + dst), S.mc + env * MT_CODES + dst / 2,
-                      MT_HALF_GENS, (lds_u32*)wscr);
-        }
-      }
-    }
-  }
   wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
              regens + wave_sum(lregen), true);
 #ifdef TG_DIAG_STAMPS
@@ -1172,6 +1126,68 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     }
   }
 #endif
+}
+
+// ---- deferred regeneration of the listed stale MT halves (k_regen) ----------------------------
+// k_classify lists the halves the previous step left stale (MT_STALE) on the refill list of the
+// step's slot and marks them MT_LISTED; every REGEN_STEPS compact steps (and on tg_regenerate)
+// k_regen regenerates the lists of all pending slots at once with a full-occupancy grid and no
+// option loops beside it: each wave takes a contiguous range of list regions (a region = one
+// classify wave's <= 64 entries), its twists software-pipelined (the next half's source loads in
+// flight while this half is twisted).  An entry is regenerated iff its env's state word still
+// says MT_STALE (its lane may have regenerated the half itself, or crossed again since): the
+// half not holding the position, from the last generation of the one holding it; then the word
+// loses MT_STALE | MT_LISTED.  It runs alone on the stream, so nothing else touches the state.
+// Slack: a listed half is needed again only after the env consumes the rest of the half it is
+// in, >= MT_HALF / 2 - (one step's draws) ~ 2,400 draws, more than REGEN_STEPS steps draw on the
+// default level (<= ~110 per step); a lane that gets there first regenerates the half itself.
+constexpr int REGEN_STEPS = 16;
+__global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
+                                                 const uint8_t* __restrict__ nrefill, int64_t n,
+                                                 int slots, unsigned long long* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
+  lds_u32* const scr = (lds_u32*)scratch[threadIdx.x >> 6];
+  const int lane = threadIdx.x & 63;
+  const int64_t nreg = (n + 63) >> 6;  // regions per slot
+  const int64_t total = nreg * slots;
+  const int64_t nw = (int64_t)gridDim.x * (BLOCK / 64);
+  const int64_t wv = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  const int64_t r0 = total * wv / nw, r1 = total * (wv + 1) / nw;
+  uint32_t* const st_w = reinterpret_cast<uint32_t*>(S.st4);  // word 4i + 3: env i's MT word
+  auto src_of = [&](uint32_t env, uint32_t s) {
+    const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
+    return (const glb_u32*)(S.mt + (int64_t)env * MT_WORDS + mt_prev_gen(dst));
+  };
+  int halves = 0;
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t slot = r / nreg, rg = r - slot * nreg;
+    const int cnt = __builtin_amdgcn_readfirstlane((int)nrefill[slot * nreg + rg]);
+    if (!cnt) continue;
+    const uint32_t env_l = lane < cnt ? refill[(slot * nreg + rg) * 64 + lane] & 0x7FFFFFFFu : 0u;
+    const uint32_t st_l = lane < cnt ? st_w[(int64_t)env_l * 4 + 3] : 0u;
+    unsigned long long need = __ballot(lane < cnt && (st_l & MT_STALE));
+    if (!need) continue;
+    TwistIn t;
+    int L = __ffsll((long long)need) - 1;
+    twist_load(src_of(__builtin_amdgcn_readlane(env_l, L), __builtin_amdgcn_readlane(st_l, L)), t);
+    while (need) {
+      L = __ffsll((long long)need) - 1;
+      need &= need - 1;
+      const uint32_t env = __builtin_amdgcn_readlane(env_l, L), s = __builtin_amdgcn_readlane(st_l, L);
+      const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
+      TwistIn u = t;
+      if (need) {
+        const int L2 = __ffsll((long long)need) - 1;
+        twist_load(src_of(__builtin_amdgcn_readlane(env_l, L2), __builtin_amdgcn_readlane(st_l, L2)), t);
+      }
+      twist_chain(u, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
+                  S.mc + (int64_t)env * MT_CODES + dst / 2, MT_HALF_GENS, scr);
+      if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
+      ++halves;
+    }
+  }
+  if (lane == 0 && halves)
+    atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + ST_REGENS], (unsigned long long)halves);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
@@ -1425,7 +1441,7 @@ int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 // at most n/64 + O_COUNT chunks (idle blocks interleaved among the option blocks, so that MT
 // regenerations start at once, measured no faster for the masked policy and slower for the
 // uniform one: DESIGN.md §3.3)
-int run_grid_for(int64_t n) { return grid_for(n) + (O_COUNT * 64 + BLOCK - 1) / BLOCK + REFILL_BLOCKS; }
+int run_grid_for(int64_t n) { return grid_for(n) + (O_COUNT * 64 + BLOCK - 1) / BLOCK; }
 // one launch-counter slot per workgroup of the widest step launch (k_run)
 int stat_slots(int64_t n) { return run_grid_for(n); }
 
@@ -1440,6 +1456,14 @@ int flush_timing(tg_batch* h) {
     ++h->timed_launches;
   }
   h->ev_used = 0;
+  for (size_t k = 0; k + 2 <= h->rev_used; k += 2) {
+    HIP_TRY(hipEventSynchronize(h->rev[k + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, h->rev[k], h->rev[k + 1]));
+    h->regen_ms_done += ms;
+    ++h->regen_timed;
+  }
+  h->rev_used = 0;
   return TG_OK;
 }
 // timing of one step launch (tg_set_timing): whether this launch is sampled, and its events
@@ -1544,8 +1568,8 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->wang, sizeof(double2) * NSEG * (size_t)h->shard_cap);
   ALLOC(h->wep, sizeof(int2) * NSEG * (size_t)h->shard_cap);
   ALLOC(h->wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
-  ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63));
-  ALLOC(h->nrefill, (size_t)((n + 63) >> 6));
+  ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63) * REGEN_STEPS);
+  ALLOC(h->nrefill, (size_t)((n + 63) >> 6) * REGEN_STEPS);
 #undef ALLOC
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1574,6 +1598,7 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   for (auto ev : h->ev) (void)hipEventDestroy(ev);
+  for (auto ev : h->rev) (void)hipEventDestroy(ev);
   render_free(h->rs);
   void* bufs[] = {h->grid,  h->genrand, h->gotab, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
                   h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
@@ -1598,6 +1623,41 @@ int tg_reset(tg_batch* h, const uint8_t* mask, double* obs, void* stream) {
 }  // extern "C"
 
 namespace {
+// k_regen over the pending refill-list slots (timed with its own event pair when timing is on)
+int launch_regen(tg_batch* h, hipStream_t st) {
+  if (!h->rpend) return TG_OK;
+  const bool timed = h->timing_every != 0;
+  if (timed) {
+    while (h->rev.size() < h->rev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      h->rev.push_back(ev);
+    }
+    HIP_TRY(hipEventRecord(h->rev[h->rev_used], st));
+  }
+  // exactly the resident workgroups (each wave's share of the lists is fixed: a second round of
+  // workgroups would start its shares after the first had finished), within the counter slots
+  if (!h->regen_per_cu) {
+    int nb = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k_regen),
+                                                         BLOCK, 0));
+    h->regen_per_cu = nb > 0 ? nb : 1;
+  }
+  int grid = h->cus * h->regen_per_cu;
+  if (grid > stat_slots(h->n)) grid = stat_slots(h->n);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_regen, dim3(grid), dim3(BLOCK), 0, st, h->S, h->refill, h->nrefill, h->n,
+                     h->rpend, h->stats);
+  HIP_TRY(hipGetLastError());
+  h->rpend = 0;
+  ++h->regen_launches;
+  if (timed) {
+    HIP_TRY(hipEventRecord(h->rev[h->rev_used + 1], st));
+    h->rev_used += 2;
+    if (h->rev_used >= 4094) return flush_timing(h);
+  }
+  return TG_OK;
+}
 // one step's kernels on `st`, timed with HIP events when enabled
 int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
   StepIO io = io_in;
@@ -1628,7 +1688,10 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
     int32_t* const cur = h->wctr + (h->parity ? NCTR * CTR_STRIDE : 0);
     int32_t* const nxt = h->wctr + (h->parity ? 0 : NCTR * CTR_STRIDE);
     h->parity ^= 1;
-    const Work w{h->wl, h->wst4, h->wang, h->wep, cur, nxt, h->refill, h->nrefill, h->shard_cap};
+    // this step's refill-list slot (k_regen drains the pending slots every REGEN_STEPS steps)
+    const int64_t nreg = (h->n + 63) >> 6;
+    const Work w{h->wl,  h->wst4, h->wang, h->wep, cur, nxt, h->refill + h->rpend * nreg * 64,
+                 h->nrefill + h->rpend * nreg, h->shard_cap};
     decltype(&k_classify<true, true>) kc;
     if (io.policy == TG_POLICY_UNIFORM)
       kc = ar ? (fo ? k_classify<true, true, 0> : k_classify<true, false, 0>)
@@ -1649,7 +1712,9 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
                        q, w, h->g0, h->stats, h->err);
   }
   HIP_TRY(hipGetLastError());
-  return timed ? timing_mark(h, st, 2) : TG_OK;
+  if (timed && (rc = timing_mark(h, st, 2))) return rc;
+  if (h->mode != TG_MODE_DIRECT && ++h->rpend == REGEN_STEPS) return launch_regen(h, st);
+  return TG_OK;
 }
 
 }  // namespace
@@ -1841,6 +1906,11 @@ int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
   return TG_OK;
 }
 
+int tg_regenerate(tg_batch* h, void* stream) {
+  BIND(h);
+  return launch_regen(h, (hipStream_t)stream);
+}
+
 int tg_set_timing(tg_batch* h, int every) {
   BIND(h);
   if (every < 0) return fail(TG_E_INVAL, "tg_set_timing: every %d < 0", every);
@@ -1900,6 +1970,9 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   out->wave_ticks = (int64_t)s[ST_WTICKS];
   out->timed_launches = h->timed_launches;
   out->run_ms = h->run_ms_done;
+  out->regen_ms = h->regen_ms_done;
+  out->regen_timed = h->regen_timed;
+  out->regen_launches = h->regen_launches;
   return TG_OK;
 }
 
@@ -1911,6 +1984,10 @@ int tg_stats_reset(tg_batch* h) {
   h->kernel_ms_done = 0.0;
   h->run_ms_done = 0.0;
   h->timed_launches = 0;
+  h->rev_used = 0;
+  h->regen_ms_done = 0.0;
+  h->regen_timed = 0;
+  h->regen_launches = 0;
   return TG_OK;
 }
 
@@ -1980,6 +2057,7 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
   BIND(h);
   if (!pos || !flags || !objs || !ang || !mt || !mt_pos)
     return fail(TG_E_INVAL, "tg_write_state: pos, flags, objs, ang, mt and mt_pos are required");
+  h->rpend = 0;  // the pending refill lists name the old states' halves: every ring is rebuilt
   const int64_t n = h->n;
   std::vector<uint4> st((size_t)n);
   for (int64_t i = 0; i < n; ++i) {

@@ -74,7 +74,7 @@ struct tg_batch {
   double2* wang = nullptr;
   int2* wep = nullptr;
   int32_t* wctr = nullptr; // sharded counters
-  uint32_t* refill = nullptr;  // stale MT halves to regenerate in k_run (compact mode)
+  uint32_t* refill = nullptr;  // stale MT halves listed by k_classify: REGEN_STEPS slots (k_regen)
   uint8_t* nrefill = nullptr;
   int parity = 0;  // which half of wctr this compact step counts in
   uint32_t tstep = 0;  // steps taken by the handle (mod 2^32): S.ep holds each episode's start step
@@ -86,6 +86,13 @@ struct tg_batch {
   double kernel_ms_done = 0.0;  // the timed launches' step kernels
   double run_ms_done = 0.0;     //   of which the second (k_run), or the single kernel
   int64_t timed_launches = 0;
+  int rpend = 0;                    // compact steps whose refill lists k_regen has not drained
+  int regen_per_cu = 0;             // k_regen workgroups resident per CU (occupancy API, first use)
+  std::vector<hipEvent_t> rev;      // k_regen's (start, stop) pairs while timing is on
+  size_t rev_used = 0;
+  double regen_ms_done = 0.0;       // the timed k_regen launches
+  int64_t regen_launches = 0;       // k_regen launches (timed or not)
+  int64_t regen_timed = 0;
   std::string domain;              // domain.txt text (the renderer's cell sprites)
   double* obs_scratch = nullptr;   // tg_rollout without an obs output
   tg::TgOne* one = nullptr;            // tg_step1's row: pinned host memory the kernel writes

@@ -142,6 +142,7 @@ constexpr int MT_HALF_GENS = 8;                // generations per half
 constexpr int MT_HALF = MT_HALF_GENS * MT_N;   // words per half
 constexpr int MT_WORDS = 2 * MT_HALF;          // per env
 constexpr uint32_t MT_STALE = 1u << 31;   // state word: the half not holding pos is stale
+constexpr uint32_t MT_LISTED = 1u << 30;  // state word: that stale half is on a refill list (k_regen)
 constexpr uint32_t MT_POS_MASK = 0xFFFFu;
 static_assert(MT_WORDS <= (int)MT_POS_MASK, "positions fit the state word");
 constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu;

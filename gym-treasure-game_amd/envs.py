@@ -316,6 +316,11 @@ class TreasureGameVec:
         launch).  stats() then holds kernel_ms / run_ms summed over timed_launches."""
         check(self._L.tg_set_timing(self.handle, int(every)), "tg_set_timing")
 
+    def regenerate(self):
+        """Regenerate every stale MT half still queued (tg_regenerate: results never depend on
+        it; a timed loop calls it at its end so that it holds its own steps' regeneration)."""
+        check(self._L.tg_regenerate(self.handle, self._stream()), "tg_regenerate")
+
     def stats(self):
         s = _lib.Stats()
         check(self._L.tg_get_stats(self.handle, ctypes.byref(s)), "tg_get_stats")

@@ -102,7 +102,10 @@ typedef struct {
                            go loops, whose lanes may also wait for the others' plain ticks) */
   int64_t timed_launches; /* launches timed with HIP events (tg_set_timing) */
   double run_ms;        /* of kernel_ms, the second kernel's time (k_run in the compact mode; the
-                           single kernel of the direct / async launches) */
+                           single kernel of the direct launches) */
+  double regen_ms;      /* summed k_regen time of the timed k_regen launches */
+  int64_t regen_timed;  /* k_regen launches timed with HIP events (while tg_set_timing is on) */
+  int64_t regen_launches; /* k_regen launches (deferred MT regenerations, tg_regenerate) */
 } tg_stats;
 
 /* Create N envs on `device`: env i is `random.seed(seed_base + global_offset + i);
@@ -196,6 +199,13 @@ int tg_set_mode(tg_batch *h, int mode, int run_blocks);
  * into tg_stats.kernel_ms / run_ms / timed_launches.  An event record between two kernels costs
  * the stream a gap of several microseconds, so a benchmark samples (e.g. every 8th step). */
 int tg_set_timing(tg_batch *h, int every);
+
+/* Regenerate every stale MT half still queued now (k_regen).  The compact step lists the halves
+ * its envs left stale and regenerates the lists of REGEN_STEPS (16) steps at once, so up to 15
+ * steps' worth may be pending after a tg_step; results never depend on when this runs (a lane
+ * that reaches a stale half regenerates it itself).  A timed loop calls it at its end so that it
+ * contains the regeneration work of its own steps.  Asynchronous on `stream`. */
+int tg_regenerate(tg_batch *h, void *stream);
 /* Capacity of the completed-episode queue (default max(4N, 65536) records).  Records that
  * arrive while it is full are dropped and counted (tg_stats.episodes_dropped); the count is
  * clamped so that an undrained queue never overflows.  Reallocates the queue and discards

@@ -39,6 +39,9 @@ def time_one(path, policy, n, burn, steps):
     acts = None
     if policy == "uniform":  # inputs resident before timing, as the bench
         acts = [vec.policy_actions(burn + j, ACTION_SEED, policy).clone() for j in range(steps)]
+    regen = hasattr(vec._L, "tg_regenerate")  # deferred MT regeneration (round 3 r03aa+)
+    if regen:
+        vec.regenerate()
     torch.cuda.synchronize()
     vec.stats_reset()
     vec.set_timing(True)
@@ -47,6 +50,8 @@ def time_one(path, policy, n, burn, steps):
         vec.step(acts[j] if acts is not None else vec.policy_actions(burn + j, ACTION_SEED, policy))
         if j % 10 == 9:
             vec.drain_episodes(rec, cnt)
+    if regen:
+        vec.regenerate()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     st = vec.stats()

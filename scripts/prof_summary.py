@@ -92,7 +92,7 @@ def main():
     if prof_line is None:
         prof_line = bench_line(os.path.join(a.out, "pmc_fetch.log"))
     last = prof_line["steps"] if prof_line else None
-    for p in ("fetch", "write", "sq1", "sq2"):
+    for p in ("fetch", "write", "sq1", "sq2", "regen_fetch", "regen_write", "regen_sq1", "regen_sq2"):
         path = os.path.join(a.out, "pmc_%s_%s" % (p, a.tag), "run_counter_collection.csv")
         if os.path.exists(path):
             avg, m = counters(path, last)
@@ -102,7 +102,10 @@ def main():
     res["pmc_avg_per_dispatch"] = pm
     res["dispatch_meta"] = meta
     # the step's kernels: k_classify + k_run (compact) or k_step (direct)
-    names = (("k_classify", "k_run") if a.mode == "compact" else ("k_step",))
+    names = (("k_classify", "k_run", "k_regen") if a.mode == "compact" else ("k_step",))
+    # k_regen drains REGEN_STEPS steps' refill lists per launch: its per-step share
+    spl = (prof_line or {}).get("roofline", {}).get("step", {}).get("kernels", {}).get(
+        "regen", {}).get("steps_per_launch", 16.0)
     step_k = [k for k in pm if k.split("<")[0] in names]
     if step_k and all("FETCH_SIZE" in pm[k] for k in step_k):
         known = 16.0 * a.envs  # k_errors: one 16-B uint4 per env, 16 B per lane
@@ -117,8 +120,10 @@ def main():
             base = k.split("<")[0]
             if base == "k_classify":
                 coal = 44.0 * a.envs
-            elif base == "k_run":  # regens: generations; one source read per half
-                coal = 44.0 * valid + 2500.0 / MT_HALF_GENS * regens
+            elif base == "k_run":  # the worklist rows (no regeneration since r03aa: k_regen)
+                coal = 44.0 * valid
+            elif base == "k_regen":  # per launch: spl steps' halves, one source read each
+                coal = (2500.0 + 8.0) / MT_HALF_GENS * regens * spl
             else:  # k_step: env-order state loads + the refills' sources
                 coal = 44.0 * a.envs + 2496.0 / MT_HALF_GENS * regens
             scat = max(fr - coal / 2.0, 0.0)
@@ -152,7 +157,7 @@ def main():
                                   (g, g / 80.0, "%.0f %%" % (100 * vu) if vu is not None else "?",
                                    "%.0f %%" % (100 * wf) if wf is not None else "?"))
             per[k] = ent
-        tot = sum(v["hbm_bytes"] for v in per.values())
+        tot = sum(v["hbm_bytes"] / (spl if k.startswith("k_regen") else 1.0) for k, v in per.items())
         res["hbm"] = {"kernels": per, "hbm_bytes_per_launch": tot,
                       "calibration": "per access pattern (profiles/r03/fetch_calibration.json): "
                                      "coalesced reads reported at 1/2, scattered 8/16-B loads "
@@ -160,7 +165,8 @@ def main():
                       "fetch_calibration_kerrors": cal,
                       "kerrors_note": ("k_errors reads %d B, FETCH_SIZE reported %.0f B" %
                                        (known, raw_err)) if raw_err else "k_errors not profiled"}
-        ns = sum(ks[k]["avg_ns"] for k in ks if k.split("<")[0] in names)
+        ns = sum(ks[k]["avg_ns"] / (spl if k.startswith("k_regen") else 1.0)
+                 for k in ks if k.split("<")[0] in names)
         res["step_kernels_avg_ns"] = ns
         # VALU issue utilisation of the step kernels: wave64 VALU instructions x 2 cycles
         # (SIMD-32) over the SIMD-cycles of their duration at the 2.4 GHz nominal clock
