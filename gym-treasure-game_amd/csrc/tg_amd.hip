@@ -347,12 +347,17 @@ __device__ __forceinline__ void wave_fence() {
 // a generation's 312 draw codes from its words in LDS, draw d = r * 64 + lane per round: its
 // two words are one 8-B LDS read at an 8-B lane stride (conflict-free; four draws per lane at a
 // 32-B stride were 2-way conflicts), its code one byte of a coalesced 64-B store
+// (FAST: from the top 27 bits of the draw, draw_code_words; k_regen only: in k_run it measured
+// 8 % slower)
+template <bool FAST = false>
 __device__ __forceinline__ void codes_from_lds(const lds_u32* w, uint8_t* dst_c) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
     const int d = r * 64 + lane;
-    if (d < MT_N / 2) dst_c[d] = (uint8_t)draw_code(mt_double(w[2 * d], w[2 * d + 1]));
+    if (d < MT_N / 2)
+      dst_c[d] = (uint8_t)(FAST ? draw_code_words(w[2 * d], w[2 * d + 1])
+                                : draw_code(mt_double(w[2 * d], w[2 * d + 1])));
   }
 }
 // The whole-wave twist's inputs: 30 dwords per lane, loaded by twist_load, used by twist_store.
@@ -375,6 +380,7 @@ __device__ __forceinline__ void twist_load(const glb_u32* src, TwistIn& t) {
 // p - 227 written by rounds r - 4 and r - 3 only, so a group needs nothing from itself, and its
 // reads issue together (4 LDS round trips per generation instead of 10).
 constexpr int TWIST_GROUP = 3;
+template <bool FAST = false>
 __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint8_t* dst_c,
                                             lds_u32* scratch) {
   const int lane = threadIdx.x & 63;
@@ -397,7 +403,7 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
     // s_waitcnt lgkmcnt(0) after every round: 0.1322 vs 0.1340 ms)
     wave_fence();
   }
-  codes_from_lds(scratch, dst_c);
+  codes_from_lds<FAST>(scratch, dst_c);
 }
 // The next generation in place in LDS (s: a generation -> its successor), stored to dst with
 // its codes.  Round r reads words p + 1 (old: round r + 1 writes it, for lane 63), p + 397
@@ -405,6 +411,7 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
 // writes p.  A group's reads are all issued before its writes (the compiler barrier: one
 // wave's LDS operations execute in order), so round r + 1's write cannot overtake round r's
 // read of word 64 (r + 1).  Must be reached by all 64 lanes.
+template <bool FAST = false>
 __device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst_c) {
   const int lane = threadIdx.x & 63;
   wave_fence();  // the previous codes pass's reads of s before this twist's writes
@@ -432,16 +439,17 @@ __device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst
     }
     wave_fence();
   }
-  codes_from_lds(s, dst_c);
+  codes_from_lds<FAST>(s, dst_c);
 }
 // `gens` generations in sequence after src (a generation in HBM) into dst, dst + MT_N, ...
 // (words) and dst_c, dst_c + MT_N / 2, ... (codes): the first twisted from registers, the rest
 // chained in the wave's LDS scratch, so a half's regeneration reads one generation from HBM.
 // src / dst are wave-uniform; must be reached by all 64 lanes.
+template <bool FAST = false>
 __device__ __forceinline__ void twist_chain(const TwistIn& t, glb_u32* dst, uint8_t* dst_c, int gens,
                                             lds_u32* scratch) {
-  twist_store(t, dst, dst_c, scratch);
-  for (int g = 1; g < gens; ++g) twist_lds(scratch, dst + g * MT_N, dst_c + g * (MT_N / 2));
+  twist_store<FAST>(t, dst, dst_c, scratch);
+  for (int g = 1; g < gens; ++g) twist_lds<FAST>(scratch, dst + g * MT_N, dst_c + g * (MT_N / 2));
 }
 __device__ __forceinline__ void wave_twist_gens(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
                                                 int gens, lds_u32* scratch) {
@@ -1180,8 +1188,8 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
         const int L2 = __ffsll((long long)need) - 1;
         twist_load(src_of(__builtin_amdgcn_readlane(env_l, L2), __builtin_amdgcn_readlane(st_l, L2)), t);
       }
-      twist_chain(u, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
-                  S.mc + (int64_t)env * MT_CODES + dst / 2, MT_HALF_GENS, scr);
+      twist_chain<true>(u, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
+                        S.mc + (int64_t)env * MT_CODES + dst / 2, MT_HALF_GENS, scr);
       if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
       ++halves;
     }

@@ -197,6 +197,25 @@ TG_HD uint32_t draw_code(double r) {
   const uint32_t neg = (uint32_t)((int)rint(-4.0 + 2.0 * r) + 4);
   return pos | (neg << CODE_NEG_SHIFT) | (r > 0.25 ? CODE_JUMP : 0u) | (r <= 0.8 ? CODE_FLIP : 0u);
 }
+// draw_code from the draw's first word: r lies in [a / 2^27, (a + 1) / 2^27) for a = the top
+// 27 bits (mt_double), and every outcome in draw_code is monotone in r, so the code is constant
+// on that interval unless one of the thresholds 0.25, 0.75, 0.8 lies in it or next to it
+// (CODE_SLOW: then the exact f64 path, ~3 draws in 2^25).  Checked for every a against
+// draw_code at both ends of its interval (tests/test_core_host.py).  k_regen's code pass takes
+// it: one word tempered instead of two, integer compares instead of f64 work.
+constexpr uint32_t CODE_SLOW = 0xFFu;
+TG_HD uint32_t code_of_top27(uint32_t a) {
+  constexpr uint32_t Q1 = 1u << 25, Q3 = 3u << 25, F8 = 107374182u;  // floor(x * 2^27)
+  if (a - (Q1 - 1u) < 3u || a - (Q3 - 1u) < 3u || a - (F8 - 1u) < 3u) return CODE_SLOW;
+  constexpr uint32_t LOW = CODE_FLIP;                                            // r < 0.25
+  constexpr uint32_t MID = 1u | (1u << CODE_NEG_SHIFT) | CODE_JUMP | CODE_FLIP;  // < 0.75
+  constexpr uint32_t HIGH = 2u | (2u << CODE_NEG_SHIFT) | CODE_JUMP;             // > 0.75
+  return a < Q1 ? LOW : a < Q3 ? MID : a < F8 ? (HIGH | CODE_FLIP) : HIGH;
+}
+TG_HD uint32_t draw_code_words(uint32_t w0, uint32_t w1) {
+  const uint32_t c = code_of_top27(mt_temper(w0) >> 5);
+  return c != CODE_SLOW ? c : draw_code(mt_double(w0, w1));
+}
 // the noisy step of a code: +2..+4 (DIR > 0: RIGHT / DOWN) or -4..-2 (LEFT / UP)
 TG_HD int code_step(uint32_t c, bool neg) {
   return neg ? (int)((c >> CODE_NEG_SHIFT) & 3u) - 4 : (int)(c & CODE_POS) + 2;

@@ -223,25 +223,6 @@ __device__ __forceinline__ void chain2(lds_u32* s, uint32_t* dst, uint8_t* dst_c
 }
 
 // the product's grouped in-place twist (tg_amd.hip twist_lds), with parts switched off
-// draw_code from the draw's first word: r lies in [a / 2^27, (a + 1) / 2^27) for a = the top
-// 27 bits (mt_double), and every outcome in draw_code is monotone in r, so the code is constant
-// on that interval unless one of the thresholds 0.25, 0.75, 0.8 lies in it or next to it
-// (CODE_SLOW: then the exact f64 path, ~3 draws in 2^25).  (Exact: every a checked against draw_code at both ends of
-// its interval on the host.)  Measured in the product's k_run: uniform 8 % SLOWER (A/B
-// 0.169 vs 0.156 ms, profiles/r03/ab_r03s_top27.log), masked equal; not kept.
-constexpr uint32_t CODE_SLOW = 0xFFu;
-__host__ __device__ inline uint32_t code_of_top27(uint32_t a) {
-  constexpr uint32_t Q1 = 1u << 25, Q3 = 3u << 25, F8 = 107374182u;  // floor(x * 2^27)
-  if (a - (Q1 - 1u) < 3u || a - (Q3 - 1u) < 3u || a - (F8 - 1u) < 3u) return CODE_SLOW;
-  constexpr uint32_t LOW = CODE_FLIP;                                            // r < 0.25
-  constexpr uint32_t MID = 1u | (1u << CODE_NEG_SHIFT) | CODE_JUMP | CODE_FLIP;  // < 0.75
-  constexpr uint32_t HIGH = 2u | (2u << CODE_NEG_SHIFT) | CODE_JUMP;             // > 0.75
-  return a < Q1 ? LOW : a < Q3 ? MID : a < F8 ? (HIGH | CODE_FLIP) : HIGH;
-}
-__host__ __device__ inline uint32_t draw_code_words(uint32_t w0, uint32_t w1) {
-  const uint32_t c = code_of_top27(mt_temper(w0) >> 5);
-  return c != CODE_SLOW ? c : draw_code(mt_double(w0, w1));
-}
 __device__ __forceinline__ void codes_top27(lds_u32* nw, uint8_t* dst_c) {
   const int lane = threadIdx.x & 63;
 #pragma unroll

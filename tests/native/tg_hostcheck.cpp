@@ -156,6 +156,25 @@ int hc_rng_stream(uint64_t seed, const int32_t* launches, int nl, int defer, dou
   return 0;
 }
 
+// code_of_top27 against draw_code at both ends of every top-27-bit interval it decides (the
+// outcomes are monotone in r, so the ends decide the interval); returns the mismatches and the
+// number of intervals left to the exact path
+int64_t hc_check_code_top27(int64_t* slow) {
+  int64_t bad = 0, ns = 0;
+  for (uint32_t a = 0; a < (1u << 27); ++a) {
+    const uint32_t c = tg::code_of_top27(a);
+    if (c == tg::CODE_SLOW) {
+      ++ns;
+      continue;
+    }
+    const double lo = (a * 67108864.0) * (1.0 / 9007199254740992.0);
+    const double hi = (a * 67108864.0 + 67108863.0) * (1.0 / 9007199254740992.0);
+    bad += (tg::draw_code(lo) != c) + (tg::draw_code(hi) != c);
+  }
+  *slow = ns;
+  return bad;
+}
+
 // the six collision predicates at a pixel position / door state (same bit order as the
 // oracle's tgo_predicates)
 unsigned hc_predicates(int px, int py, unsigned door_bits) {

@@ -167,3 +167,13 @@ def test_core_gotable_matches_direct(hostcheck, level, policy):
     np.testing.assert_array_equal(direct["ticks"], table["ticks"])
 
 
+def test_draw_code_from_the_top_27_bits(hostcheck):
+    """code_of_top27 (k_regen's code pass: one tempered word, integer compares) equals
+    draw_code(random()) at both ends of every interval of 2^26 draws it decides; draw_code's
+    outcomes are monotone in r, so it equals it on the whole interval.  The intervals next to
+    the thresholds 0.25, 0.75 and 0.8 go to the exact f64 path."""
+    slow = ctypes.c_int64(0)
+    hostcheck.hc_check_code_top27.restype = ctypes.c_int64
+    bad = hostcheck.hc_check_code_top27(ctypes.byref(slow))
+    assert bad == 0
+    assert slow.value == 9
