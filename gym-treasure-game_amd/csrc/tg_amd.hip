@@ -1150,6 +1150,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
 // in, >= MT_HALF / 2 - (one step's draws) ~ 2,400 draws, more than REGEN_STEPS steps draw on the
 // default level (<= ~110 per step); a lane that gets there first regenerates the half itself.
 constexpr int REGEN_STEPS = 16;
+constexpr bool REGEN_PIPE = true;  // the next half's source loads in flight during this one
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  const uint8_t* __restrict__ nrefill, int64_t n,
                                                  int slots, unsigned long long* __restrict__ stats) {
@@ -1175,6 +1176,21 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
     const uint32_t st_l = lane < cnt ? st_w[(int64_t)env_l * 4 + 3] : 0u;
     unsigned long long need = __ballot(lane < cnt && (st_l & MT_STALE));
     if (!need) continue;
+    if constexpr (!REGEN_PIPE) {
+      while (need) {
+        const int L = __ffsll((long long)need) - 1;
+        need &= need - 1;
+        const uint32_t env = __builtin_amdgcn_readlane(env_l, L), s = __builtin_amdgcn_readlane(st_l, L);
+        const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
+        TwistIn t;
+        twist_load(src_of(env, s), t);
+        twist_chain<true>(t, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
+                          S.mc + (int64_t)env * MT_CODES + dst / 2, MT_HALF_GENS, scr);
+        if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
+        ++halves;
+      }
+      continue;
+    }
     TwistIn t;
     int L = __ffsll((long long)need) - 1;
     twist_load(src_of(__builtin_amdgcn_readlane(env_l, L), __builtin_amdgcn_readlane(st_l, L)), t);

@@ -104,8 +104,7 @@ def main():
     # the step's kernels: k_classify + k_run (compact) or k_step (direct)
     names = (("k_classify", "k_run", "k_regen") if a.mode == "compact" else ("k_step",))
     # k_regen drains REGEN_STEPS steps' refill lists per launch: its per-step share
-    spl = (prof_line or {}).get("roofline", {}).get("step", {}).get("kernels", {}).get(
-        "regen", {}).get("steps_per_launch", 16.0)
+    spl = 16.0  # tg_amd.hip REGEN_STEPS: steps per k_regen launch at steady state
     step_k = [k for k in pm if k.split("<")[0] in names]
     if step_k and all("FETCH_SIZE" in pm[k] for k in step_k):
         known = 16.0 * a.envs  # k_errors: one 16-B uint4 per env, 16 B per lane
