@@ -1141,8 +1141,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
 // step's slot and marks them MT_LISTED; every REGEN_STEPS compact steps (and on tg_regenerate)
 // k_regen regenerates the lists of all pending slots at once with a full-occupancy grid and no
 // option loops beside it: each wave takes a contiguous range of list regions (a region = one
-// classify wave's <= 64 entries), its twists software-pipelined (the next half's source loads in
-// flight while this half is twisted).  An entry is regenerated iff its env's state word still
+// classify wave's <= 64 entries).  An entry is regenerated iff its env's state word still
 // says MT_STALE (its lane may have regenerated the half itself, or crossed again since): the
 // half not holding the position, from the last generation of the one holding it; then the word
 // loses MT_STALE | MT_LISTED.  It runs alone on the stream, so nothing else touches the state.
@@ -1150,7 +1149,6 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
 // in, >= MT_HALF / 2 - (one step's draws) ~ 2,400 draws, more than REGEN_STEPS steps draw on the
 // default level (<= ~110 per step); a lane that gets there first regenerates the half itself.
 constexpr int REGEN_STEPS = 16;
-constexpr bool REGEN_PIPE = true;  // the next half's source loads in flight during this one
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  const uint8_t* __restrict__ nrefill, int64_t n,
                                                  int slots, unsigned long long* __restrict__ stats) {
@@ -1176,35 +1174,16 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
     const uint32_t st_l = lane < cnt ? st_w[(int64_t)env_l * 4 + 3] : 0u;
     unsigned long long need = __ballot(lane < cnt && (st_l & MT_STALE));
     if (!need) continue;
-    if constexpr (!REGEN_PIPE) {
-      while (need) {
-        const int L = __ffsll((long long)need) - 1;
-        need &= need - 1;
-        const uint32_t env = __builtin_amdgcn_readlane(env_l, L), s = __builtin_amdgcn_readlane(st_l, L);
-        const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
-        TwistIn t;
-        twist_load(src_of(env, s), t);
-        twist_chain<true>(t, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
-                          S.mc + (int64_t)env * MT_CODES + dst / 2, MT_HALF_GENS, scr);
-        if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
-        ++halves;
-      }
-      continue;
-    }
-    TwistIn t;
-    int L = __ffsll((long long)need) - 1;
-    twist_load(src_of(__builtin_amdgcn_readlane(env_l, L), __builtin_amdgcn_readlane(st_l, L)), t);
+    // one half at a time: 52 VGPRs, 8 waves per SIMD (the next half's source loads pipelined
+    // into this one's twist took 76 VGPRs, 6 waves, and measured no faster: DESIGN.md §3.3)
     while (need) {
-      L = __ffsll((long long)need) - 1;
+      const int L = __ffsll((long long)need) - 1;
       need &= need - 1;
       const uint32_t env = __builtin_amdgcn_readlane(env_l, L), s = __builtin_amdgcn_readlane(st_l, L);
       const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
-      TwistIn u = t;
-      if (need) {
-        const int L2 = __ffsll((long long)need) - 1;
-        twist_load(src_of(__builtin_amdgcn_readlane(env_l, L2), __builtin_amdgcn_readlane(st_l, L2)), t);
-      }
-      twist_chain<true>(u, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
+      TwistIn t;
+      twist_load(src_of(env, s), t);
+      twist_chain<true>(t, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
                         S.mc + (int64_t)env * MT_CODES + dst / 2, MT_HALF_GENS, scr);
       if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
       ++halves;
