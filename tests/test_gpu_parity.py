@@ -280,6 +280,39 @@ def test_modes_identical_full_outputs(tg):
 CORRIDOR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", "corridor")
 
 
+@pytest.mark.parametrize("level,n,steps", [(None, 1 << 16, 80), ("corridor", 192, 40)])
+def test_deferred_regeneration_is_invisible(tg, level, n, steps):
+    """k_regen drains the listed stale MT halves every 16 compact steps; when it runs must not
+    matter.  The same batch stepped with the automatic drains only, and with tg_regenerate
+    after every step, gives identical rows, states, MT generations and counters.  Masked
+    policy (an option every step, ~37 draws per env-step), and the corridor level (~650 draws
+    per go step: lanes reach still-stale halves and regenerate them themselves)."""
+    ld = None if level is None else CORRIDOR
+    sides = []
+    for eager in (False, True):
+        vec = tg.TreasureGameVec(n, seed=6, autoreset=True, level_dir=ld)
+        vec.reset()
+        acc = []
+        for t in range(steps):
+            o, r, v, d, info = vec.step(vec.policy_actions(t, 0x77, "masked"))
+            acc.append(torch.cat([o.view(torch.int64).flatten(), r.to(torch.int64), v.to(torch.int64),
+                                  d.to(torch.int64), info["final_obs"].view(torch.int64).flatten()]).cpu())
+            if eager:
+                vec.regenerate()
+        vec.regenerate()
+        torch.cuda.synchronize()
+        sides.append((torch.stack(acc), vec.read_state(mt=True), vec.stats(), vec.errors()))
+        vec.close()
+    (a, sa, ta, ea), (b, sb, tb, eb) = sides
+    assert torch.equal(a, b)
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    for k in ("steps", "valid_steps", "ticks", "draws", "episodes"):
+        assert ta[k] == tb[k], k
+    assert tb["regen_launches"] >= steps and ta["regen_launches"] <= steps // 16 + 1
+    assert ea == eb == (0 if level is None else ea)
+
+
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("policy,autoreset", [(0, False), (1, True)])
 def test_corridor_multi_generation_steps(tg, oracle, mode, policy, autoreset):
