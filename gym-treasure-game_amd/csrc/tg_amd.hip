@@ -1149,24 +1149,36 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
 // in, >= MT_HALF / 2 - (one step's draws) ~ 2,400 draws, more than REGEN_STEPS steps draw on the
 // default level (<= ~110 per step); a lane that gets there first regenerates the half itself.
 constexpr int REGEN_STEPS = 16;
+constexpr int REGEN_GRAB = 16;  // list regions a wave takes from its XCD's counter at a time
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  const uint8_t* __restrict__ nrefill, int64_t n,
-                                                 int slots, unsigned long long* __restrict__ stats) {
+                                                 int slots, int32_t* __restrict__ ctr,
+                                                 unsigned long long* __restrict__ stats) {
   __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   lds_u32* const scr = (lds_u32*)scratch[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   const int64_t nreg = (n + 63) >> 6;  // regions per slot
   const int64_t total = nreg * slots;
-  const int64_t nw = (int64_t)gridDim.x * (BLOCK / 64);
-  const int64_t wv = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
-  const int64_t r0 = total * wv / nw, r1 = total * (wv + 1) / nw;
+  // regions go out REGEN_GRAB at a time from one counter per XCD (blockIdx.x % 8: regions
+  // xcd, xcd + 8, ...): the halves per region vary, and a fixed share per wave left the
+  // launch to its most loaded waves
+  const int xcd = (int)(blockIdx.x & 7u);
+  const int64_t nmine = (total - xcd + 7) >> 3;
+  int32_t* const q = ctr + xcd * CTR_STRIDE;
   uint32_t* const st_w = reinterpret_cast<uint32_t*>(S.st4);  // word 4i + 3: env i's MT word
   auto src_of = [&](uint32_t env, uint32_t s) {
     const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
     return (const glb_u32*)(S.mt + (int64_t)env * MT_WORDS + mt_prev_gen(dst));
   };
   int halves = 0;
-  for (int64_t r = r0; r < r1; ++r) {
+  while (true) {
+  int64_t j0 = 0;
+  if (lane == 0) j0 = atomicAdd(q, REGEN_GRAB);
+  j0 = __builtin_amdgcn_readfirstlane((int)j0);
+  if (j0 >= nmine) break;
+  const int64_t j1 = j0 + REGEN_GRAB < nmine ? j0 + REGEN_GRAB : nmine;
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t r = xcd + 8 * j;
     const int64_t slot = r / nreg, rg = r - slot * nreg;
     const int cnt = __builtin_amdgcn_readfirstlane((int)nrefill[slot * nreg + rg]);
     if (!cnt) continue;
@@ -1188,6 +1200,7 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
       if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
       ++halves;
     }
+  }
   }
   if (lane == 0 && halves)
     atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + ST_REGENS], (unsigned long long)halves);
@@ -1573,6 +1586,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
   ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63) * REGEN_STEPS);
   ALLOC(h->nrefill, (size_t)((n + 63) >> 6) * REGEN_STEPS);
+  ALLOC(h->regen_ctr, sizeof(int32_t) * 8 * CTR_STRIDE);
 #undef ALLOC
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1606,7 +1620,7 @@ void tg_destroy(tg_batch* h) {
   void* bufs[] = {h->grid,  h->genrand, h->gotab, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
                   h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
                   h->wst4,  h->wang,    h->wep,
-                  h->wctr,  h->refill,  h->nrefill,   h->obs_scratch};
+                  h->wctr,  h->refill,  h->nrefill,   h->obs_scratch, h->regen_ctr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->one) (void)hipHostFree(h->one);
@@ -1649,8 +1663,9 @@ int launch_regen(tg_batch* h, hipStream_t st) {
   int grid = h->cus * h->regen_per_cu;
   if (grid > stat_slots(h->n)) grid = stat_slots(h->n);
   if (grid < 1) grid = 1;
+  HIP_TRY(hipMemsetAsync(h->regen_ctr, 0, sizeof(int32_t) * 8 * CTR_STRIDE, st));
   hipLaunchKernelGGL(k_regen, dim3(grid), dim3(BLOCK), 0, st, h->S, h->refill, h->nrefill, h->n,
-                     h->rpend, h->stats);
+                     h->rpend, h->regen_ctr, h->stats);
   HIP_TRY(hipGetLastError());
   h->rpend = 0;
   ++h->regen_launches;

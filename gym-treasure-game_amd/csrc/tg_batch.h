@@ -88,6 +88,7 @@ struct tg_batch {
   int64_t timed_launches = 0;
   int rpend = 0;                    // compact steps whose refill lists k_regen has not drained
   int regen_per_cu = 0;             // k_regen workgroups resident per CU (occupancy API, first use)
+  int32_t* regen_ctr = nullptr;     // k_regen's per-XCD region counters (zeroed per launch)
   std::vector<hipEvent_t> rev;      // k_regen's (start, stop) pairs while timing is on
   size_t rev_used = 0;
   double regen_ms_done = 0.0;       // the timed k_regen launches

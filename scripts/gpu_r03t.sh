@@ -21,7 +21,7 @@ for pol in uniform masked; do
   # counters for the step kernels' dispatches around the timed steps only (the burn-in's
   # thousands of serialised counter dispatches are slow and their CSVs too large)
   K="--kernel-include-regex k_classify|k_run --kernel-iteration-range [$((B - 20))-$((B + 40))]"
-  T=r03t$pol
+  T=${TAGP:-r03t}$pol
   run trace_$pol 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_$T -o run --output-format csv -- python3 bench.py $A
   run pmc_fetch_$pol 300 rocprofv3 $K --pmc FETCH_SIZE -d $OUT/pmc_fetch_$T -o run --output-format csv -- python3 bench.py $A
   run pmc_write_$pol 300 rocprofv3 $K --pmc WRITE_SIZE -d $OUT/pmc_write_$T -o run --output-format csv -- python3 bench.py $A
