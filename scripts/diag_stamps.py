@@ -35,8 +35,9 @@ def main():
     for t in range(int(os.environ.get("STEPS", 30))):
         vec.step(vec.policy_actions(t, policy=pol))
     torch.cuda.synchronize()
-    # k_run's waves (tg_amd.hip run_grid_for): the env workgroups, 3 of padding, REFILL_BLOCKS
-    nw = min(((n + 255) // 256 + 3 + 64) * 4, 1 << 17)
+    # k_run's waves (tg_amd.hip run_grid_for): the env workgroups and 3 of padding (round 3:
+    # no REFILL_BLOCKS, the refills are k_regen's)
+    nw = min(((n + 255) // 256 + 3) * 4, 1 << 17)
     buf = np.zeros((nw, 11), np.uint64)
     vec.stats_reset()
     vec.step(vec.policy_actions(999, policy=pol))
