@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     const uint32_t pr = __shfl(prounds, lmax, 64);
     if ((threadIdx.x & 63) == 0 && wv < NSTAMP_WAVES) {
       unsigned long long* const g = g_stamps + (size_t)wv * NSTAMP;
-      // an idle wave (no option: the refill queue only) is option 15 with 1 iteration
+      // an idle wave (no listed chunk) is option 15 with 1 iteration
       g[0] = bl ? a1 - t0 : 0;
       g[1] = bl ? a2 - a1 : 0;
       g[2] = bl ? t3 - a2 : t3 - t0;

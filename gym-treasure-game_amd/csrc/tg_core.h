@@ -127,7 +127,7 @@ TG_HD int floordiv48(int a) { return div48(a + 16 * S) - 16; }              // -
 //   regenerated: MT_HALF_GENS twists in sequence from the last generation of the half the
 //   lane is in (twist_half); the env's state word carries MT_STALE meanwhile.  The kernels
 //   regenerate it later, a whole wavefront per env, coalesced, the chained twists in LDS
-//   (tg_amd.hip wave_twist_gens: k_run's refill queue, k_reset).  A launch that
+//   (tg_amd.hip twist_chain: k_regen every 16 steps, k_reset, k_step).  A launch that
 //   would enter a stale half (> MT_HALF draws since the refill) regenerates it first, per
 //   lane.  Seeding (init_by_array) fills the ring's last generation; 2 x MT_HALF_GENS twists
 //   then give generations 1 .. 2 x MT_HALF_GENS, pos 0 (init_mt).
