@@ -530,7 +530,10 @@ def step_line(args, runner, dt, st, node, world, total):
             "timing": "HIP events around every %d-th step on the step's stream (start, "
                       "between the kernels, end)" % args.timing_every,
             "limiter": run_k.get("limiter"), "valu_util": run_k.get("valu_util"),
-            "wait_frac": run_k.get("wait_frac"), "lane_efficiency": lane_eff}
+            "wait_frac": run_k.get("wait_frac"), "lane_efficiency": lane_eff,
+            "note": "dominant kernel by time; latency-bound option loops that move few bytes "
+                    "(the MT regeneration is k_regen's since round 3: step.kernels.regen; the "
+                    "whole step: step.frac) (DESIGN.md 3.6)"}
     kernels = {"run": run_k}
     if args.mode == "compact":
         kernels["classify"] = kern("k_classify", cls_b, cls_s, cls_pmc)
