@@ -24,6 +24,7 @@
 #include "tg_core.h"
 #include "tg_level.h"
 #include "tg_batch.h"
+#include "tg_twist.h"
 
 namespace tg {
 thread_local std::string g_err;
@@ -128,10 +129,6 @@ constexpr int WIN_WAVE_BYTES = WIN_SLOTS * WIN_SLOT_BYTES;  // 4 KB per wave
 constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
 static_assert(WIN_WAVE_BYTES >= WAVE_SCRATCH, "wave_refill reuses the window as scratch");
 static_assert(WIN_DRAWS - WIN_UNIT + 1 >= (int)MAX_TICK_DRAWS, "a refilled window holds a tick's draws");
-
-typedef __attribute__((address_space(1))) uint32_t glb_u32;
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // LDS-DMA of one WIN_UNIT-byte unit per active lane into LDS [m0 + lane * WIN_UNIT]; M0 is
 // saved/restored
@@ -338,124 +335,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
   const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
   return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ void wave_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-// a generation's 312 draw codes from its words in LDS, draw d = r * 64 + lane per round: its
-// two words are one 8-B LDS read at an 8-B lane stride (conflict-free; four draws per lane at a
-// 32-B stride were 2-way conflicts), its code one byte of a coalesced 64-B store
-// (FAST: from the top 27 bits of the draw, draw_code_words; k_regen only: in k_run it measured
-// 8 % slower)
-template <bool FAST = false>
-__device__ __forceinline__ void codes_from_lds(const lds_u32* w, uint8_t* dst_c) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
-    const int d = r * 64 + lane;
-    if (d < MT_N / 2)
-      dst_c[d] = (uint8_t)(FAST ? draw_code_words(w[2 * d], w[2 * d + 1])
-                                : draw_code(mt_double(w[2 * d], w[2 * d + 1])));
-  }
-}
-// The whole-wave twist's inputs: 30 dwords per lane, loaded by twist_load, used by twist_store.
-struct TwistIn {
-  static constexpr int ROUNDS = (MT_N + 63) / 64;  // 10
-  uint32_t a[ROUNDS], b[ROUNDS], c[4];
-};
-// the loads of wave_twist (issued, not waited for: a caller can overlap them with other work)
-__device__ __forceinline__ void twist_load(const glb_u32* src, TwistIn& t) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int r = 0; r < TwistIn::ROUNDS; ++r) {
-    const int p = r * 64 + lane;
-    t.a[r] = p < MT_N ? src[p] : 0u;
-    t.b[r] = p + 1 < MT_N ? src[p + 1] : 0u;
-    if (r < 4) t.c[r] = p < MT_N - MT_M ? src[p + MT_M] : 0u;
-  }
-}
-// The rounds of a twist go in groups {0, 1, 2} {3, 4, 5} {6, 7, 8} {9}: round r reads new words
-// p - 227 written by rounds r - 4 and r - 3 only, so a group needs nothing from itself, and its
-// reads issue together (4 LDS round trips per generation instead of 10).
-constexpr int TWIST_GROUP = 3;
-template <bool FAST = false>
-__device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint8_t* dst_c,
-                                            lds_u32* scratch) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int r0 = 0; r0 < TwistIn::ROUNDS; r0 += TWIST_GROUP) {
-#pragma unroll
-    for (int r = r0; r < r0 + TWIST_GROUP && r < TwistIn::ROUNDS; ++r) {
-      const int p = r * 64 + lane;
-      if (p < MT_N) {
-        const uint32_t bb = p + 1 < MT_N ? t.b[r] : scratch[0];
-        const uint32_t cc = p < MT_N - MT_M ? t.c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
-        const uint32_t w = mt_twist(t.a[r], bb, cc);
-        scratch[p] = w;
-        dst[p] = w;
-      }
-    }
-    // the group visible to later groups, whose lanes read what other lanes wrote: a
-    // wavefront-scope fence orders the LDS accesses in the compiler (one wave's LDS operations
-    // execute in order), without the hardware wait for the store's completion (A/B against
-    // s_waitcnt lgkmcnt(0) after every round: 0.1322 vs 0.1340 ms)
-    wave_fence();
-  }
-  codes_from_lds<FAST>(scratch, dst_c);
-}
-// The next generation in place in LDS (s: a generation -> its successor), stored to dst with
-// its codes.  Round r reads words p + 1 (old: round r + 1 writes it, for lane 63), p + 397
-// (old for p < 227: rounds >= 6 write them) or p - 227 (new: rounds r - 4 / r - 3), then
-// writes p.  A group's reads are all issued before its writes (the compiler barrier: one
-// wave's LDS operations execute in order), so round r + 1's write cannot overtake round r's
-// read of word 64 (r + 1).  Must be reached by all 64 lanes.
-template <bool FAST = false>
-__device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst_c) {
-  const int lane = threadIdx.x & 63;
-  wave_fence();  // the previous codes pass's reads of s before this twist's writes
-#pragma unroll
-  for (int r0 = 0; r0 < TwistIn::ROUNDS; r0 += TWIST_GROUP) {
-    uint32_t w[TWIST_GROUP];
-#pragma unroll
-    for (int r = r0; r < r0 + TWIST_GROUP && r < TwistIn::ROUNDS; ++r) {
-      const int p = r * 64 + lane;
-      if (p < MT_N) {
-        const uint32_t a = s[p];
-        const uint32_t b = s[p + 1 < MT_N ? p + 1 : 0];
-        const uint32_t c = s[p < MT_N - MT_M ? p + MT_M : p - (MT_N - MT_M)];
-        w[r - r0] = mt_twist(a, b, c);
-      }
-    }
-    asm volatile("" ::: "memory");  // the group's reads before its writes, in program order
-#pragma unroll
-    for (int r = r0; r < r0 + TWIST_GROUP && r < TwistIn::ROUNDS; ++r) {
-      const int p = r * 64 + lane;
-      if (p < MT_N) {
-        s[p] = w[r - r0];
-        dst[p] = w[r - r0];
-      }
-    }
-    wave_fence();
-  }
-  codes_from_lds<FAST>(s, dst_c);
-}
-// `gens` generations in sequence after src (a generation in HBM) into dst, dst + MT_N, ...
-// (words) and dst_c, dst_c + MT_N / 2, ... (codes): the first twisted from registers, the rest
-// chained in the wave's LDS scratch, so a half's regeneration reads one generation from HBM.
-// src / dst are wave-uniform; must be reached by all 64 lanes.
-template <bool FAST = false>
-__device__ __forceinline__ void twist_chain(const TwistIn& t, glb_u32* dst, uint8_t* dst_c, int gens,
-                                            lds_u32* scratch) {
-  twist_store<FAST>(t, dst, dst_c, scratch);
-  for (int g = 1; g < gens; ++g) twist_lds<FAST>(scratch, dst + g * MT_N, dst_c + g * (MT_N / 2));
-}
-__device__ __forceinline__ void wave_twist_gens(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
-                                                int gens, lds_u32* scratch) {
-  TwistIn t;
-  twist_load(src, t);
-  twist_chain(t, dst, dst_c, gens, scratch);
 }
 // For every lane in `need`: regenerate the stale half of its env (the one not holding the
 // position in its state word), one env at a time, with the whole wave (wave_twist_gens: its
@@ -1153,7 +1032,8 @@ constexpr int REGEN_GRAB = 16;  // list regions a wave takes from its XCD's coun
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  const uint8_t* __restrict__ nrefill, int64_t n,
                                                  int slots, int32_t* __restrict__ ctr,
-                                                 unsigned long long* __restrict__ stats) {
+                                                 unsigned long long* __restrict__ stats,
+                                                 int nstat) {
   __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   lds_u32* const scr = (lds_u32*)scratch[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
@@ -1195,15 +1075,17 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
       const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
       TwistIn t;
       twist_load(src_of(env, s), t);
-      twist_chain<true>(t, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
+      twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
                         S.mc + (int64_t)env * MT_CODES + dst / 2, MT_HALF_GENS, scr);
       if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
       ++halves;
     }
   }
   }
+  // the grid can exceed the stats slots (>= 8 workgroups, one per XCD counter, at small n)
   if (lane == 0 && halves)
-    atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + ST_REGENS], (unsigned long long)halves);
+    atomicAdd(&stats[(size_t)(blockIdx.x % (unsigned)nstat) * ST_COUNT + ST_REGENS],
+              (unsigned long long)halves);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
@@ -1652,20 +1534,24 @@ int launch_regen(tg_batch* h, hipStream_t st) {
     }
     HIP_TRY(hipEventRecord(h->rev[h->rev_used], st));
   }
-  // exactly the resident workgroups (each wave's share of the lists is fixed: a second round of
-  // workgroups would start its shares after the first had finished), within the counter slots
+  // Workgroups take list regions from the counter of their XCD (blockIdx.x % 8) until it runs
+  // out, so the grid needs at least 8 of them (one per counter; fewer would leave the regions
+  // of the missing counters undone) and no more than are resident at once (a second round
+  // would find the counters exhausted and only pay its launch).  Block b adds its halves to
+  // stats slot b % stat_slots.
   if (!h->regen_per_cu) {
     int nb = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k_regen),
                                                          BLOCK, 0));
     h->regen_per_cu = nb > 0 ? nb : 1;
   }
-  int grid = h->cus * h->regen_per_cu;
-  if (grid > stat_slots(h->n)) grid = stat_slots(h->n);
-  if (grid < 1) grid = 1;
+  const int64_t regions = ((h->n + 63) >> 6) * h->rpend;
+  int64_t grid = (int64_t)h->cus * h->regen_per_cu;
+  if (grid > (regions + 3) / 4) grid = (regions + 3) / 4;  // 4 waves per workgroup
+  if (grid < 8) grid = 8;
   HIP_TRY(hipMemsetAsync(h->regen_ctr, 0, sizeof(int32_t) * 8 * CTR_STRIDE, st));
-  hipLaunchKernelGGL(k_regen, dim3(grid), dim3(BLOCK), 0, st, h->S, h->refill, h->nrefill, h->n,
-                     h->rpend, h->regen_ctr, h->stats);
+  hipLaunchKernelGGL(k_regen, dim3((unsigned)grid), dim3(BLOCK), 0, st, h->S, h->refill, h->nrefill,
+                     h->n, h->rpend, h->regen_ctr, h->stats, stat_slots(h->n));
   HIP_TRY(hipGetLastError());
   h->rpend = 0;
   ++h->regen_launches;
@@ -2009,6 +1895,25 @@ int tg_stats_reset(tg_batch* h) {
   return TG_OK;
 }
 
+int tg_kernel_info(tg_batch* h, int kernel, int32_t* blocks_per_cu, int32_t* vgprs, int32_t* sgprs,
+                   int32_t* lds_bytes) {
+  BIND(h);
+  const void* k = kernel == TG_KERNEL_CLASSIFY ? reinterpret_cast<const void*>(k_classify<true, false>)
+                  : kernel == TG_KERNEL_RUN    ? reinterpret_cast<const void*>(k_run<true, false>)
+                  : kernel == TG_KERNEL_REGEN  ? reinterpret_cast<const void*>(k_regen)
+                                               : nullptr;
+  if (!k) return fail(TG_E_INVAL, "tg_kernel_info: unknown kernel %d", kernel);
+  hipFuncAttributes fa;
+  HIP_TRY(hipFuncGetAttributes(&fa, k));
+  int nb = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, BLOCK, 0));
+  if (blocks_per_cu) *blocks_per_cu = nb;
+  if (vgprs) *vgprs = fa.numRegs;
+  if (sgprs) *sgprs = -1;  // not reported by hipFuncGetAttributes
+  if (lds_bytes) *lds_bytes = (int32_t)fa.sharedSizeBytes;
+  return TG_OK;
+}
+
 int tg_read_state(tg_batch* h, int32_t* pos, uint32_t* flags, int32_t* objs, double* ang,
                   uint32_t* mt, uint32_t* mt_pos, int32_t* ep) {
   BIND(h);
@@ -2075,7 +1980,6 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
   BIND(h);
   if (!pos || !flags || !objs || !ang || !mt || !mt_pos)
     return fail(TG_E_INVAL, "tg_write_state: pos, flags, objs, ang, mt and mt_pos are required");
-  h->rpend = 0;  // the pending refill lists name the old states' halves: every ring is rebuilt
   const int64_t n = h->n;
   std::vector<uint4> st((size_t)n);
   for (int64_t i = 0; i < n; ++i) {
@@ -2105,6 +2009,8 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
     st[(size_t)i] = w;
   }
   HIP_TRY(hipDeviceSynchronize());
+  // validated: the pending refill lists name the old states' halves, and every ring is rebuilt
+  h->rpend = 0;
   HIP_TRY(hipMemcpy(h->S.st4, st.data(), sizeof(uint4) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->S.ang, ang, sizeof(double2) * n, hipMemcpyHostToDevice));
   {  // (return, length) -> (return, start step)

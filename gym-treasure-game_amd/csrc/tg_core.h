@@ -216,6 +216,26 @@ TG_HD uint32_t draw_code_words(uint32_t w0, uint32_t w1) {
   const uint32_t c = code_of_top27(mt_temper(w0) >> 5);
   return c != CODE_SLOW ? c : draw_code(mt_double(w0, w1));
 }
+// code_of_top27 in fewer instructions (the wave twist's code pass, tg_twist.h, is VALU-bound):
+// for an `a` that is not next to a threshold the outcome classes r < 0.25 | < 0.75 | <= 0.8 |
+// > 0.8 are a's top two bits (0 | 1, 2 | 3) plus one compare against F8 (F8 >= 3 * 2^25: only
+// class 3 splits); byte k of TOP27_LUT is class k's code.  top27_slow is a superset of
+// code_of_top27's CODE_SLOW set (a within one of any multiple of 2^25 — 0.25 and 0.75 are 2^25
+// and 3 * 2^25, the others harmless extra slow cases — or of F8): there the exact f64 path
+// runs.  Checked against code_of_top27 for every a (tests/test_core_host.py).
+constexpr uint32_t TOP27_F8 = 107374182u;  // floor(0.8 * 2^27), as code_of_top27
+constexpr uint32_t TOP27_LUT = CODE_FLIP |
+                               ((1u | (1u << CODE_NEG_SHIFT) | CODE_JUMP | CODE_FLIP) << 8) |
+                               ((1u | (1u << CODE_NEG_SHIFT) | CODE_JUMP | CODE_FLIP) << 16) |
+                               ((2u | (2u << CODE_NEG_SHIFT) | CODE_JUMP | CODE_FLIP) << 24);
+static_assert(TOP27_F8 >= (3u << 25), "only the top class splits at 0.8");
+TG_HD bool top27_slow(uint32_t a) {
+  return (((a + 1u) & 0x1FFFFFFu) < 3u) | (a - (TOP27_F8 - 1u) < 3u);
+}
+TG_HD uint32_t top27_code(uint32_t a) {
+  const uint32_t c = (TOP27_LUT >> ((a >> 22) & 0x18u)) & 0xFFu;
+  return a >= TOP27_F8 ? c ^ CODE_FLIP : c;
+}
 // the noisy step of a code: +2..+4 (DIR > 0: RIGHT / DOWN) or -4..-2 (LEFT / UP)
 TG_HD int code_step(uint32_t c, bool neg) {
   return neg ? (int)((c >> CODE_NEG_SHIFT) & 3u) - 4 : (int)(c & CODE_POS) + 2;

@@ -329,6 +329,17 @@ class TreasureGameVec:
     def stats_reset(self):
         check(self._L.tg_stats_reset(self.handle), "tg_stats_reset")
 
+    def kernel_info(self):
+        """{kernel: (workgroups per CU, VGPRs, LDS bytes)} of the step kernels (tg_kernel_info)"""
+        out = {}
+        for name, k in (("k_classify", 0), ("k_run", 1), ("k_regen", 2)):
+            v = [ctypes.c_int32() for _ in range(4)]
+            check(self._L.tg_kernel_info(self.handle, k, *[ctypes.byref(x) for x in v]),
+                  "tg_kernel_info")
+            out[name] = {"blocks_per_cu": v[0].value, "waves_per_simd": v[0].value,
+                         "vgprs": v[1].value, "lds_bytes": v[3].value}
+        return out
+
     # -- render('rgb_array') (TG/:98-105; DR/ draw_domain) ---------------------------------------
     def render_init(self, sprites=None):
         """Load the sprite sheet (uint8 [24, h, w, 4] RGBA, ``render.load_sprites`` /
@@ -577,8 +588,10 @@ class TreasureGame:
                          self._py.gauss_next if self._py.has_gauss else None))
 
     def _reset_py(self, obs):
-        st = random.getstate()
-        self._load_global()
+        st = self._load_global()
+        if st is None:  # in-place load: the replay's start state from the words just loaded
+            st = (3, self._WORDS.unpack_from(self._py, 0),
+                  self._py.gauss_next if self._py.has_gauss else None)
         check(self._vec._L.tg_reset1_py(self._vec.handle, ctypes.byref(self._py),
                                         obs.ctypes.data, self._vec._stream()), "tg_reset1_py")
         # The reset's draws (IM/:55-73): two uniform(), then gauss twice.  Their stream position

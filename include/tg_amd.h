@@ -221,6 +221,14 @@ int tg_predicate_table(tg_batch *h, int32_t x0, int32_t x1, int32_t y0, int32_t 
 /* Counters (host, synchronises). */
 int tg_get_stats(tg_batch *h, tg_stats *out);
 int tg_stats_reset(tg_batch *h);
+/* Resources of the step kernels as launched on this handle's device (no reference counterpart;
+ * for the measurement's notes): kernel TG_KERNEL_*; out: workgroups per CU by the occupancy
+ * API, VGPRs, SGPRs, static LDS bytes per 256-thread workgroup. */
+#define TG_KERNEL_CLASSIFY 0 /* k_classify, uniform policy given as actions, auto-reset */
+#define TG_KERNEL_RUN 1      /* k_run, auto-reset */
+#define TG_KERNEL_REGEN 2    /* k_regen */
+int tg_kernel_info(tg_batch *h, int kernel, int32_t *blocks_per_cu, int32_t *vgprs, int32_t *sgprs,
+                   int32_t *lds_bytes);
 
 /* Raw SoA state copy-out for checkpoints and tests (host buffers, synchronises; the MT
  * generations are gathered on the device and copied out in chunks of 64 Ki envs):

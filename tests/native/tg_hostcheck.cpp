@@ -175,6 +175,23 @@ int64_t hc_check_code_top27(int64_t* slow) {
   return bad;
 }
 
+// top27_code / top27_slow (the wave twist's code pass, tg_twist.h) against code_of_top27 for
+// every a: equal wherever top27_slow is false, and top27_slow covers every CODE_SLOW interval;
+// returns the mismatches and the number of slow intervals
+int64_t hc_check_code_lean(int64_t* slow) {
+  int64_t bad = 0, ns = 0;
+  for (uint32_t a = 0; a < (1u << 27); ++a) {
+    const uint32_t c = tg::code_of_top27(a);
+    if (tg::top27_slow(a)) {
+      ++ns;
+      continue;
+    }
+    bad += (c == tg::CODE_SLOW) + (tg::top27_code(a) != c);
+  }
+  *slow = ns;
+  return bad;
+}
+
 // the six collision predicates at a pixel position / door state (same bit order as the
 // oracle's tgo_predicates)
 unsigned hc_predicates(int px, int py, unsigned door_bits) {

@@ -177,3 +177,14 @@ def test_draw_code_from_the_top_27_bits(hostcheck):
     bad = hostcheck.hc_check_code_top27(ctypes.byref(slow))
     assert bad == 0
     assert slow.value == 9
+
+
+def test_lean_draw_code_equals_top27(hostcheck):
+    """top27_code / top27_slow (the wave twist's code pass, tg_twist.h: the class from a's top
+    two bits plus one compare) equal code_of_top27 on every a they decide, and the slow set
+    (a within one of a multiple of 2^25 or of floor(0.8 * 2^27)) covers every CODE_SLOW a"""
+    slow = ctypes.c_int64(0)
+    hostcheck.hc_check_code_lean.restype = ctypes.c_int64
+    bad = hostcheck.hc_check_code_lean(ctypes.byref(slow))
+    assert bad == 0
+    assert slow.value == 15  # 0, 1; 2^25 k - 1 .. 2^25 k + 1 (k = 1..3); 2^27 - 1; F8 - 1 .. F8 + 1

@@ -280,7 +280,7 @@ def test_modes_identical_full_outputs(tg):
 CORRIDOR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", "corridor")
 
 
-@pytest.mark.parametrize("level,n,steps", [(None, 1 << 16, 80), ("corridor", 192, 40)])
+@pytest.mark.parametrize("level,n,steps", [(None, 1 << 16, 80), (None, 192, 80), ("corridor", 192, 40)])
 def test_deferred_regeneration_is_invisible(tg, level, n, steps):
     """k_regen drains the listed stale MT halves every 16 compact steps; when it runs must not
     matter.  The same batch stepped with the automatic drains only, and with tg_regenerate
@@ -307,7 +307,10 @@ def test_deferred_regeneration_is_invisible(tg, level, n, steps):
     assert torch.equal(a, b)
     for k in sa:
         assert np.array_equal(sa[k], sb[k]), k
-    for k in ("steps", "valid_steps", "ticks", "draws", "episodes"):
+    # every half left stale is regenerated exactly once, by k_regen or by its lane: the counts
+    # agree unless a drain skipped listed halves (a k_regen grid below 8 workgroups
+    # left the regions of the missing XCD counters to the lanes)
+    for k in ("steps", "valid_steps", "ticks", "draws", "episodes", "regens"):
         assert ta[k] == tb[k], k
     assert tb["regen_launches"] >= steps and ta["regen_launches"] <= steps // 16 + 1
     assert ea == eb == (0 if level is None else ea)
