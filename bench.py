@@ -484,19 +484,28 @@ def load_pmc(path, envs, policy, mode, regens_per_step, burn_in):
 
 def step_line(args, runner, dt, st, node, world, total):
     """the bench line's roofline / counters for the c3 step measurement: the dominant kernel
-    (k_run; k_step in the direct mode) over its own HIP-event time, the step's kernels beside"""
+    (k_run; k_step in the direct mode) over its own duration, the step's kernels beside.
+
+    Durations: every --timing-every-th timed step is sampled (tg_set_timing): a HIP event pair on
+    the step's stream brackets its kernels (the step's event time), and each kernel's span, from
+    its first wave's start to its last wave's end, comes from in-kernel s_memrealtime stamps
+    (tg_amd.hip kst_end; no event between the kernels, so nothing is added to the stream
+    between them).  k_regen: its own event pair and span per launch.  The spans are the
+    kernels' durations; the rocprofv3 trace of the same command agrees with them
+    (profiles/<tag>_summary.json)."""
     env_steps = total * args.steps
     assert node["steps"] == env_steps, (node, env_steps)
     launches = max(st["launches"], 1)
     timed = max(st["timed_launches"], 1)
-    step_s = st["kernel_ms"] / 1e3 / timed      # k_classify + k_run of a timed launch
-    run_s = st["run_ms"] / 1e3 / timed          # k_run alone
-    cls_s = step_s - run_s
+    event_s = st["kernel_ms"] / 1e3 / timed     # a sampled step, event to event
+    run_s = st["run_ms"] / 1e3 / timed          # k_run's span (k_step's in the direct mode)
+    cls_s = st["classify_ms"] / 1e3 / timed     # k_classify's span
     cls_b, run_b, regen_b = (b / launches for b in alg_bytes(st, args.mode))
-    # k_regen: its own event pairs; per step = per launch x launches per step
     rl = st.get("regen_launches", 0)
-    regen_launch_s = st["regen_ms"] / 1e3 / st["regen_timed"] if st.get("regen_timed") else 0.0
-    regen_s = regen_launch_s * rl / launches
+    rt = st.get("regen_timed", 0)
+    regen_launch_s = st["regen_span_ms"] / 1e3 / rt if rt else 0.0
+    regen_event_s = st["regen_ms"] / 1e3 / rt if rt else 0.0
+    regen_s = regen_launch_s * rl / launches    # per step
     surv = survey_bytes(st) / launches
     d = node["draws"] / max(node["steps"], 1)
     regens = st["regens"] / launches
@@ -508,49 +517,77 @@ def step_line(args, runner, dt, st, node, world, total):
     kp = pmc.get("kernels", {}) if pmc else {}
     run_pmc = next((v for k, v in kp.items() if k.split("<")[0] == run_name), None)
     cls_pmc = next((v for k, v in kp.items() if k.split("<")[0] == "k_classify"), None)
+    info = runner.vec.kernel_info()
 
-    def kern(name, alg, sec, pm):
+    def kern(name, alg, sec, pm, traffic=None):
         ach = alg / sec / 1e9 if sec > 0 else None
         out = {"kernel": name, "alg_bytes_per_launch": alg, "kernel_ms": sec * 1e3,
                "achieved": ach, "frac": ach / HBM_PEAK_GBS if ach else None,
-               "traffic": pm["hbm_bytes"] if pm else None}
+               "traffic": traffic if traffic is not None else (pm["hbm_bytes"] if pm else None)}
         if pm:
-            out.update({"traffic_gbs": pm["hbm_bytes"] / sec / 1e9 if sec > 0 else None,
+            out.update({"traffic_gbs": out["traffic"] / sec / 1e9 if sec > 0 else None,
                         "valu_util": pm.get("valu_util"), "wait_frac": pm.get("wait_frac"),
-                        "limiter": pm.get("limiter")})
+                        "limiter": pm.get("limiter"), "rocprof_ms": (pm.get("avg_ns") or 0) / 1e6})
+        if name in info:
+            out["occupancy"] = info[name]
         return out
 
     run_k = kern(run_name, run_b, run_s, run_pmc)
+    # "bound" names the roofline the fraction is taken against: HBM, the only one this integer
+    # path has (no MFMA); what the counters say limits the kernel is "limiter"
     roof = {"bound": "hbm", "kernel": run_name + " (the step's dominant kernel)",
             "achieved": run_k["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": run_k["frac"], "traffic": run_k["traffic"],
             "traffic_source": pmc["source"] if pmc else None,
             "kernel_ms": run_s * 1e3, "alg_bytes_per_launch": run_b,
             "timed_launches": st["timed_launches"],
-            "timing": "HIP events around every %d-th step on the step's stream (start, "
-                      "between the kernels, end)" % args.timing_every,
+            "timing": "every %d-th timed step: the kernel's span from its first wave's start to "
+                      "its last wave's end (in-kernel s_memrealtime stamps), HIP events on the "
+                      "step's stream around the step" % args.timing_every,
+            "rocprof_ms": run_k.get("rocprof_ms"),
             "limiter": run_k.get("limiter"), "valu_util": run_k.get("valu_util"),
             "wait_frac": run_k.get("wait_frac"), "lane_efficiency": lane_eff,
+            "bound_basis": "the HBM roofline (no MFMA on this integer path); the kernel is "
+                           "limited by what `limiter` says (rocprofv3 counters)",
             "note": "dominant kernel by time; latency-bound option loops that move few bytes "
-                    "(the MT regeneration is k_regen's since round 3: step.kernels.regen; the "
-                    "whole step: step.frac) (DESIGN.md 3.6)"}
+                    "(the MT regeneration is k_regen's: step.kernels.regen; the whole step: "
+                    "step.frac) (DESIGN.md 3.6)"}
     kernels = {"run": run_k}
     if args.mode == "compact":
         kernels["classify"] = kern("k_classify", cls_b, cls_s, cls_pmc)
         if rl:
             regen_pmc = next((v for k, v in kp.items() if k.split("<")[0] == "k_regen"), None)
-            kernels["regen"] = kern("k_regen", regen_b * launches / rl, regen_launch_s, regen_pmc)
-            kernels["regen"].update({"launches": rl, "steps_per_launch": launches / rl})
-    all_b, all_s = cls_b + run_b + regen_b, step_s + regen_s
+            gens_launch = st["regens"] / rl  # MT generations regenerated per k_regen launch
+            # the PMC traffic per generation regenerated (its source run: 16 steps per launch),
+            # scaled to this run's launches
+            tr_gen = None
+            if regen_pmc and pmc.get("regens_per_step"):
+                tr_gen = regen_pmc["hbm_bytes"] / (pmc["regens_per_step"] * 16.0)
+            kernels["regen"] = kern("k_regen", regen_b * launches / rl, regen_launch_s, regen_pmc,
+                                    traffic=tr_gen * gens_launch if tr_gen else None)
+            kernels["regen"].update({
+                "launches": rl, "steps_per_launch": launches / rl,
+                "generations_per_launch": gens_launch,
+                "alg_bytes_per_generation": REGEN_GEN,
+                "traffic_per_generation": tr_gen,
+                "ms_per_1k_generations": regen_launch_s * 1e3 / gens_launch * 1e3
+                if gens_launch else None,
+                "event_ms": regen_event_s * 1e3})
+    all_b, all_s = cls_b + run_b + regen_b, cls_s + run_s + regen_s
+    ms_step = dt / args.steps * 1e3
     roof["step"] = {"kernel": "tg_step = " + (" + ".join(
-                        ["k_classify", "k_run", "k_regen / 16 steps"] if args.mode == "compact"
-                        else ["k_step"])),
+                        ["k_classify", "k_run", "k_regen / steps per launch"]
+                        if args.mode == "compact" else ["k_step"])),
                     "alg_bytes_per_launch": all_b, "kernel_ms": all_s * 1e3,
+                    "event_ms": event_s * 1e3,
+                    "gaps_ms": ms_step - all_s * 1e3,
                     "achieved": all_b / all_s / 1e9,
                     "frac": all_b / all_s / 1e9 / HBM_PEAK_GBS,
+                    "frac_wall": all_b / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS,
                     "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                     "alg_bytes_per_launch_survey": surv,
                     "frac_survey": surv / all_s / 1e9 / HBM_PEAK_GBS,
+                    "frac_survey_wall": surv / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS,
                     "kernels": kernels}
     return {
         "ticks_per_s": node["ticks"] / dt,

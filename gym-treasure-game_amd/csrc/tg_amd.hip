@@ -372,6 +372,30 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
+// In-kernel span stamps of the timed launches (tg_set_timing): each wave's lane 0 folds its
+// start and end (s_memrealtime: the 100 MHz constant clock) into one of KST_SLOTS
+// (min start, max end) pairs of the launch's record, with returnless atomics on 64 addresses;
+// flush_timing reduces them to the launch's span, first wave start to last wave end.  Null
+// record: not timed (a wave-uniform branch).
+constexpr int KST_SLOTS = 64;
+__device__ __forceinline__ unsigned long long kst_begin(const unsigned long long* ks) {
+  return ks ? __builtin_amdgcn_s_memrealtime() : 0ull;
+}
+__device__ __forceinline__ void kst_end(unsigned long long* ks, unsigned long long t0) {
+  if (ks && (threadIdx.x & 63) == 0) {
+    unsigned long long* const s = ks + 2 * (blockIdx.x % KST_SLOTS);
+    atomicMin(s, t0);
+    atomicMax(s + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+}
+__global__ void k_kst_init(unsigned long long* ks, int64_t pairs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < pairs) {
+    ks[2 * i] = ~0ull;
+    ks[2 * i + 1] = 0ull;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
@@ -609,7 +633,9 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
                                                  const uint32_t* __restrict__ grid, StepIO io,
                                                  EpQueue q, int64_t g0,
                                                  unsigned long long* __restrict__ stats,
-                                                 uint32_t* __restrict__ err_or) {
+                                                 uint32_t* __restrict__ err_or,
+                                                 unsigned long long* __restrict__ ks) {
+  const unsigned long long kt0 = kst_begin(ks);
   __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
   LEVEL_IN_LDS();
   lds_u8* const wscr = (lds_u8*)win + (threadIdx.x >> 6) * WIN_WAVE_BYTES;
@@ -656,6 +682,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
   }
   wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
               __popcll(need) + wave_sum(lregen), true);
+  kst_end(ks, kt0);
 }
 
 // ---- two-pass compacted step (TG_MODE_COMPACT) -------------------------------------------
@@ -720,7 +747,9 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      const uint32_t* __restrict__ grid,
                                                      StepIO io, EpQueue q, Work w, int64_t g0,
                                                      unsigned long long* __restrict__ stats,
-                                                     uint32_t* __restrict__ err_or) {
+                                                     uint32_t* __restrict__ err_or,
+                                                     unsigned long long* __restrict__ ks) {
+  const unsigned long long kt0 = kst_begin(ks);
   __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
   // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
   // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
@@ -848,6 +877,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   }
   wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
               AUTORESET ? (live && !runs && dn) : 0);
+  kst_end(ks, kt0);
 }
 
 #ifdef TG_DIAG_STAMPS
@@ -867,7 +897,9 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
                                                 const uint32_t* __restrict__ grid, StepIO io,
                                                 EpQueue q, Work w, int64_t g0,
                                                 unsigned long long* __restrict__ stats,
-                                                uint32_t* __restrict__ err_or) {
+                                                uint32_t* __restrict__ err_or,
+                                                unsigned long long* __restrict__ ks) {
+  const unsigned long long kt0 = kst_begin(ks);
   // the worklists in run order: pre[s] = envs listed before segment s (exclusive prefix of the
   // counters, two segments per thread), then per option (run order j) its first segment's
   // prefix and its start in the chunk space, where each option is padded to whole chunks
@@ -973,6 +1005,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   __builtin_amdgcn_s_setprio(0);
   wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
              regens + wave_sum(lregen), true);
+  kst_end(ks, kt0);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
   {
@@ -1032,11 +1065,14 @@ constexpr int REGEN_GRAB = 16;  // list regions a wave takes from its XCD's coun
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  const uint8_t* __restrict__ nrefill, int64_t n,
                                                  int slots, int32_t* __restrict__ ctr,
+                                                 int32_t* __restrict__ ctr_next,
                                                  unsigned long long* __restrict__ stats,
-                                                 int nstat) {
+                                                 int nstat, unsigned long long* __restrict__ ks) {
+  const unsigned long long kt0 = kst_begin(ks);
   __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   lds_u32* const scr = (lds_u32*)scratch[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x < 8) ctr_next[threadIdx.x * CTR_STRIDE] = 0;  // next launch's
   const int64_t nreg = (n + 63) >> 6;  // regions per slot
   const int64_t total = nreg * slots;
   // regions go out REGEN_GRAB at a time from one counter per XCD (blockIdx.x % 8: regions
@@ -1086,6 +1122,7 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
   if (lane == 0 && halves)
     atomicAdd(&stats[(size_t)(blockIdx.x % (unsigned)nstat) * ST_COUNT + ST_REGENS],
               (unsigned long long)halves);
+  kst_end(ks, kt0);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
@@ -1343,32 +1380,70 @@ int run_grid_for(int64_t n) { return grid_for(n) + (O_COUNT * 64 + BLOCK - 1) / 
 // one launch-counter slot per workgroup of the widest step launch (k_run)
 int stat_slots(int64_t n) { return run_grid_for(n); }
 
-int flush_timing(tg_batch* h) {
-  for (size_t k = 0; k + 3 <= h->ev_used; k += 3) {
-    HIP_TRY(hipEventSynchronize(h->ev[k + 2]));
-    float all = 0.f, second = 0.f;
-    HIP_TRY(hipEventElapsedTime(&all, h->ev[k], h->ev[k + 2]));
-    HIP_TRY(hipEventElapsedTime(&second, h->ev[k + 1], h->ev[k + 2]));
-    h->kernel_ms_done += all;
-    h->run_ms_done += second;
-    ++h->timed_launches;
-  }
+// Timing (tg_set_timing): a sampled step launch records a HIP event before its first kernel
+// and after its last, and its kernels fold their in-kernel span stamps into the sample's
+// record (kst_end); k_regen likewise.  Records: KST_MAX samples of step launches (two kernels
+// each) and KST_MAX of k_regen launches, KST_SLOTS (start, end) pairs per kernel.
+constexpr int KST_MAX = 512;
+constexpr int64_t KST_PAIRS = (int64_t)KST_MAX * 3 * KST_SLOTS;
+unsigned long long* kst_step(tg_batch* h, int k, int kernel) {
+  return h->kst + ((size_t)k * 2 + kernel) * 2 * KST_SLOTS;
+}
+unsigned long long* kst_regen(tg_batch* h, int k) {
+  return h->kst + ((size_t)KST_MAX * 2 + k) * 2 * KST_SLOTS;
+}
+int kst_reset(tg_batch* h) {  // every record to (no start, no end)
+  if (!h->kst && hipMalloc((void**)&h->kst, sizeof(unsigned long long) * 2 * KST_PAIRS) != hipSuccess)
+    return fail(TG_E_NOMEM, "timing records");
+  hipLaunchKernelGGL(k_kst_init, dim3((unsigned)((KST_PAIRS + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, 0,
+                     h->kst, KST_PAIRS);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
   h->ev_used = 0;
-  for (size_t k = 0; k + 2 <= h->rev_used; k += 2) {
-    HIP_TRY(hipEventSynchronize(h->rev[k + 1]));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, h->rev[k], h->rev[k + 1]));
-    h->regen_ms_done += ms;
-    ++h->regen_timed;
-  }
   h->rev_used = 0;
   return TG_OK;
 }
-// timing of one step launch (tg_set_timing): whether this launch is sampled, and its events
-bool timing_begin(tg_batch* h, hipStream_t st, int& rc) {
+// a kernel record's span in ms (first wave start to last wave end; 0 if it never ran)
+double kst_span_ms(const unsigned long long* rec) {
+  unsigned long long t0 = ~0ull, t1 = 0ull;
+  for (int j = 0; j < KST_SLOTS; ++j) {
+    if (rec[2 * j] < t0) t0 = rec[2 * j];
+    if (rec[2 * j + 1] > t1) t1 = rec[2 * j + 1];
+  }
+  return t1 > t0 ? (double)(t1 - t0) * 1e-5 : 0.0;  // 100 MHz ticks
+}
+int flush_timing(tg_batch* h) {
+  const size_t ns = h->ev_used / 2, nr = h->rev_used / 2;
+  if (!ns && !nr) return TG_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<unsigned long long> rec((size_t)2 * KST_PAIRS);
+  HIP_TRY(hipMemcpy(rec.data(), h->kst, sizeof(unsigned long long) * rec.size(), hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < ns; ++k) {
+    float all = 0.f;
+    HIP_TRY(hipEventElapsedTime(&all, h->ev[2 * k], h->ev[2 * k + 1]));
+    h->kernel_ms_done += all;
+    h->classify_ms_done += kst_span_ms(rec.data() + (k * 2 + 0) * 2 * KST_SLOTS);
+    h->run_ms_done += kst_span_ms(rec.data() + (k * 2 + 1) * 2 * KST_SLOTS);
+    ++h->timed_launches;
+  }
+  for (size_t k = 0; k < nr; ++k) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, h->rev[2 * k], h->rev[2 * k + 1]));
+    h->regen_ms_done += ms;
+    h->regen_span_ms_done += kst_span_ms(rec.data() + ((size_t)KST_MAX * 2 + k) * 2 * KST_SLOTS);
+    ++h->regen_timed;
+  }
+  return kst_reset(h);
+}
+// whether this step launch is sampled; if so its start event is recorded and ks0 / ks1 are
+// its kernels' records
+bool timing_begin(tg_batch* h, hipStream_t st, int& rc, unsigned long long*& ks0,
+                  unsigned long long*& ks1) {
   rc = TG_OK;
+  ks0 = ks1 = nullptr;
   if (!h->timing_every || (h->timing_calls++ % (uint64_t)h->timing_every) != 0) return false;
-  while (h->ev.size() < h->ev_used + 3) {
+  if (h->ev_used / 2 >= (size_t)KST_MAX && (rc = flush_timing(h))) return false;
+  while (h->ev.size() < h->ev_used + 2) {
     hipEvent_t ev;
     if (hipEventCreate(&ev) != hipSuccess) {
       rc = fail(TG_E_HIP, "hipEventCreate");
@@ -1376,15 +1451,15 @@ bool timing_begin(tg_batch* h, hipStream_t st, int& rc) {
     }
     h->ev.push_back(ev);
   }
+  const int k = (int)(h->ev_used / 2);
+  ks0 = kst_step(h, k, 0);
+  ks1 = kst_step(h, k, 1);
   if (hipEventRecord(h->ev[h->ev_used], st) != hipSuccess) rc = fail(TG_E_HIP, "hipEventRecord");
   return rc == TG_OK;
 }
-int timing_mark(tg_batch* h, hipStream_t st, int k) {  // k = 1: after the first kernel, 2: end
-  HIP_TRY(hipEventRecord(h->ev[h->ev_used + k], st));
-  if (k == 2) {
-    h->ev_used += 3;
-    if (h->ev_used >= 4095) return flush_timing(h);
-  }
+int timing_end(tg_batch* h, hipStream_t st) {
+  HIP_TRY(hipEventRecord(h->ev[h->ev_used + 1], st));
+  h->ev_used += 2;
   return TG_OK;
 }
 }  // namespace
@@ -1468,13 +1543,14 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
   ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63) * REGEN_STEPS);
   ALLOC(h->nrefill, (size_t)((n + 63) >> 6) * REGEN_STEPS);
-  ALLOC(h->regen_ctr, sizeof(int32_t) * 8 * CTR_STRIDE);
+  ALLOC(h->regen_ctr, sizeof(int32_t) * 2 * 8 * CTR_STRIDE);
 #undef ALLOC
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->gotab, gotab.data(), sizeof(uint32_t) * gotab.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
       hipMemset(h->wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE) != hipSuccess ||
+      hipMemset(h->regen_ctr, 0, sizeof(int32_t) * 2 * 8 * CTR_STRIDE) != hipSuccess ||
       hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)) != hipSuccess ||
       hipMemset(h->err, 0, sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail(TG_E_HIP, "tg_create: upload failed"));
@@ -1502,7 +1578,7 @@ void tg_destroy(tg_batch* h) {
   void* bufs[] = {h->grid,  h->genrand, h->gotab, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
                   h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
                   h->wst4,  h->wang,    h->wep,
-                  h->wctr,  h->refill,  h->nrefill,   h->obs_scratch, h->regen_ctr};
+                  h->wctr,  h->refill,  h->nrefill,   h->obs_scratch, h->regen_ctr, h->kst};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->one) (void)hipHostFree(h->one);
@@ -1525,20 +1601,26 @@ namespace {
 // k_regen over the pending refill-list slots (timed with its own event pair when timing is on)
 int launch_regen(tg_batch* h, hipStream_t st) {
   if (!h->rpend) return TG_OK;
-  const bool timed = h->timing_every != 0;
-  if (timed) {
+  unsigned long long* ks = nullptr;
+  if (h->timing_every) {
+    if (h->rev_used / 2 >= (size_t)KST_MAX) {
+      const int rc = flush_timing(h);
+      if (rc) return rc;
+    }
     while (h->rev.size() < h->rev_used + 2) {
       hipEvent_t ev;
       HIP_TRY(hipEventCreate(&ev));
       h->rev.push_back(ev);
     }
+    ks = kst_regen(h, (int)(h->rev_used / 2));
     HIP_TRY(hipEventRecord(h->rev[h->rev_used], st));
   }
   // Workgroups take list regions from the counter of their XCD (blockIdx.x % 8) until it runs
   // out, so the grid needs at least 8 of them (one per counter; fewer would leave the regions
   // of the missing counters undone) and no more than are resident at once (a second round
   // would find the counters exhausted and only pay its launch).  Block b adds its halves to
-  // stats slot b % stat_slots.
+  // stats slot b % stat_slots.  The counters alternate between two sets by launch parity: each
+  // launch zeroes the other set for the next one (no memset launch).
   if (!h->regen_per_cu) {
     int nb = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k_regen),
@@ -1549,16 +1631,17 @@ int launch_regen(tg_batch* h, hipStream_t st) {
   int64_t grid = (int64_t)h->cus * h->regen_per_cu;
   if (grid > (regions + 3) / 4) grid = (regions + 3) / 4;  // 4 waves per workgroup
   if (grid < 8) grid = 8;
-  HIP_TRY(hipMemsetAsync(h->regen_ctr, 0, sizeof(int32_t) * 8 * CTR_STRIDE, st));
+  int32_t* const cur = h->regen_ctr + h->regen_parity * 8 * CTR_STRIDE;
+  int32_t* const nxt = h->regen_ctr + (h->regen_parity ^ 1) * 8 * CTR_STRIDE;
+  h->regen_parity ^= 1;
   hipLaunchKernelGGL(k_regen, dim3((unsigned)grid), dim3(BLOCK), 0, st, h->S, h->refill, h->nrefill,
-                     h->n, h->rpend, h->regen_ctr, h->stats, stat_slots(h->n));
+                     h->n, h->rpend, cur, nxt, h->stats, stat_slots(h->n), ks);
   HIP_TRY(hipGetLastError());
   h->rpend = 0;
   ++h->regen_launches;
-  if (timed) {
+  if (ks) {
     HIP_TRY(hipEventRecord(h->rev[h->rev_used + 1], st));
     h->rev_used += 2;
-    if (h->rev_used >= 4094) return flush_timing(h);
   }
   return TG_OK;
 }
@@ -1568,7 +1651,8 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
   io.tstep = h->tstep++;
   const bool fo = io.final_obs != nullptr;
   int rc;
-  const bool timed = timing_begin(h, st, rc);
+  unsigned long long *ks0, *ks1;
+  const bool timed = timing_begin(h, st, rc, ks0, ks1);
   if (rc) return rc;
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   const dim3 grid(grid_for(h->n)), block(BLOCK);
@@ -1583,9 +1667,8 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
     else
       kern = ar ? (fo ? k_step<true, true> : k_step<true, false>)
                 : (fo ? k_step<false, true> : k_step<false, false>);
-    if (timed && (rc = timing_mark(h, st, 1))) return rc;
     hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, h->g0,
-                       h->stats, h->err);
+                       h->stats, h->err, ks1);
   } else {
     // counters double-buffered by step parity: k_classify zeroes the next step's set (the
     // previous k_run, which read it, has finished), so no memset launch per step
@@ -1609,14 +1692,13 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
     auto kr = ar ? (fo ? k_run<true, true> : k_run<true, false>)
                  : (fo ? k_run<false, true> : k_run<false, false>);
     hipLaunchKernelGGL(kc, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, w, h->g0,
-                       h->stats, h->err);
+                       h->stats, h->err, ks0);
     HIP_TRY(hipGetLastError());
-    if (timed && (rc = timing_mark(h, st, 1))) return rc;
     hipLaunchKernelGGL(kr, dim3(run_grid_for(h->n)), block, 0, st, h->S, h->n, h->L, h->grid, io,
-                       q, w, h->g0, h->stats, h->err);
+                       q, w, h->g0, h->stats, h->err, ks1);
   }
   HIP_TRY(hipGetLastError());
-  if (timed && (rc = timing_mark(h, st, 2))) return rc;
+  if (timed && (rc = timing_end(h, st))) return rc;
   if (h->mode != TG_MODE_DIRECT && ++h->rpend == REGEN_STEPS) return launch_regen(h, st);
   return TG_OK;
 }
@@ -1650,7 +1732,7 @@ int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t*
                   (uint64_t)(int64_t)action, 0, h->tstep++};
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   hipLaunchKernelGGL((k_step<false, false, POL_IMMEDIATE>), dim3(1), dim3(BLOCK), 0, st, h->S,
-                     h->n, h->L, h->grid, io, q, h->g0, h->stats, h->err);
+                     h->n, h->L, h->grid, io, q, h->g0, h->stats, h->err, nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st));
   memcpy(obs, h->one->obs, sizeof h->one->obs);
@@ -1818,6 +1900,10 @@ int tg_regenerate(tg_batch* h, void* stream) {
 int tg_set_timing(tg_batch* h, int every) {
   BIND(h);
   if (every < 0) return fail(TG_E_INVAL, "tg_set_timing: every %d < 0", every);
+  HIP_TRY(hipDeviceSynchronize());
+  int rc = flush_timing(h);  // records of the previous setting are kept in the sums
+  if (rc) return rc;
+  if (every && !h->kst && (rc = kst_reset(h))) return rc;
   h->timing_every = every;
   h->timing_calls = 0;
   return TG_OK;
@@ -1877,6 +1963,8 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   out->regen_ms = h->regen_ms_done;
   out->regen_timed = h->regen_timed;
   out->regen_launches = h->regen_launches;
+  out->classify_ms = h->classify_ms_done;
+  out->regen_span_ms = h->regen_span_ms_done;
   return TG_OK;
 }
 
@@ -1884,12 +1972,18 @@ int tg_stats_reset(tg_batch* h) {
   BIND(h);
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(h->n)));
+  if (h->kst) {
+    const int rc = kst_reset(h);  // drops the unflushed records (and their events)
+    if (rc) return rc;
+  }
   h->ev_used = 0;
   h->kernel_ms_done = 0.0;
   h->run_ms_done = 0.0;
+  h->classify_ms_done = 0.0;
   h->timed_launches = 0;
   h->rev_used = 0;
   h->regen_ms_done = 0.0;
+  h->regen_span_ms_done = 0.0;
   h->regen_timed = 0;
   h->regen_launches = 0;
   return TG_OK;

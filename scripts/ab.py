@@ -44,7 +44,7 @@ def time_one(path, policy, n, burn, steps):
         vec.regenerate()
     torch.cuda.synchronize()
     vec.stats_reset()
-    vec.set_timing(True)
+    vec.set_timing(int(os.environ.get("TIMING", "0")))  # 0: the wall clock only (no events / stamps)
     t0 = time.perf_counter()
     for j in range(steps):
         vec.step(acts[j] if acts is not None else vec.policy_actions(burn + j, ACTION_SEED, policy))
@@ -57,7 +57,7 @@ def time_one(path, policy, n, burn, steps):
     st = vec.stats()
     vec.close()
     return {"ms_step": dt / steps * 1e3,
-            "kernel_ms": st["kernel_ms"] / max(st.get("timed_launches") or steps, 1),
+            "kernel_ms": st["kernel_ms"] / max(st.get("timed_launches") or 1, 1),
             "lane_eff": st["ticks"] / max(64 * st["wave_ticks"], 1)}
 
 

@@ -14,6 +14,11 @@
 //              permutation: k_run's scattered st4 / ang stores of its listed envs)
 //   x2_env     8-B loads / stores, each lane a different env (ep, a draw's two MT words)
 //   code4      4-B stores, one per lane, contiguous (the twist's draw codes)
+//   gen_stores k_regen's store stream without its compute: per job (a random env's half of
+//              8 generations) 8 x 624 dword stores (256 B per instruction, generations 2,496 B
+//              apart: every other one not 128-B aligned) and 8 x 312 code bytes (64 B per
+//              instruction); gen_stores_aligned the same with generations 2,560 B apart.  Their
+//              rocprofv3 durations are the store-bound ceiling of k_regen's pattern.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -94,6 +99,33 @@ __global__ void k_env_store(uint8_t* __restrict__ base, const uint32_t* __restri
   }
 }
 
+// k_regen's stores alone (see the header): GSTRIDE words between generations
+template <int GSTRIDE>
+__global__ void k_gen_stores(uint32_t* __restrict__ mt, uint8_t* __restrict__ mc,
+                             const uint32_t* __restrict__ jobs, int njobs) {
+  const int lane = threadIdx.x & 63;
+  const int w = (int)((blockIdx.x * (uint64_t)BLOCK + threadIdx.x) >> 6);
+  const int nw = (int)(gridDim.x * (BLOCK / 64));
+  for (int j = w; j < njobs; j += nw) {
+    const uint32_t e = jobs[j];
+    const uint64_t env = e & 0x7FFFFFFFu, half = e >> 31;
+    uint32_t* const dst = mt + env * (16 * GSTRIDE) + half * (8 * GSTRIDE);
+    uint8_t* const dc = mc + env * 4992 + half * 2496;
+    for (int g = 0; g < 8; ++g) {
+#pragma unroll
+      for (int r = 0; r < 10; ++r) {
+        const int p = r * 64 + lane;
+        if (p < 624) dst[g * GSTRIDE + p] = (uint32_t)(p ^ j);
+      }
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        const int d = r * 64 + lane;
+        if (d < 312) dc[g * 312 + d] = (uint8_t)(d ^ j);
+      }
+    }
+  }
+}
+
 int main() {
   const uint64_t GiB = 1ull << 30;
   const uint64_t nenv = 1ull << 20;  // k_run's batch
@@ -131,7 +163,35 @@ int main() {
     hipLaunchKernelGGL(k_dword_store, dim3(grid), dim3(BLOCK), 0, 0, (uint32_t*)buf2, GiB / 4);
     hipLaunchKernelGGL(k_env_store<uint2>, dim3(grid), dim3(BLOCK), 0, 0, buf, perm, nenv, 1024u);
   }
+  // k_regen's store stream: 52,800 jobs (a uniform 1M-env launch's halves) over 262,144 envs
+  const int njobs = 52800;
+  const uint64_t genv = 1ull << 18;
+  uint32_t *gmt = nullptr, *gjobs = nullptr;
+  uint8_t* gmc = nullptr;
+  CHECK(hipMalloc(&gmt, genv * 16 * 640 * 4));
+  CHECK(hipMalloc(&gmc, genv * 4992));
+  {
+    std::vector<uint32_t> jb(njobs);
+    std::vector<char> used(genv, 0);
+    for (int j = 0; j < njobs; ++j) {
+      uint32_t v;
+      do v = (uint32_t)(((uint64_t)rand() * 65536 + rand()) % genv); while (used[v]);
+      used[v] = 1;
+      jb[j] = v | ((rand() & 1) ? 0x80000000u : 0u);
+    }
+    CHECK(hipMalloc(&gjobs, njobs * 4));
+    CHECK(hipMemcpy(gjobs, jb.data(), njobs * 4, hipMemcpyHostToDevice));
+  }
+  for (int r = 0; r < REPS; ++r) {
+    hipLaunchKernelGGL(k_dword_store, dim3(grid), dim3(BLOCK), 0, 0, (uint32_t*)buf2, GiB / 4);
+    hipLaunchKernelGGL(k_gen_stores<624>, dim3(2048), dim3(BLOCK), 0, 0, gmt, gmc, gjobs, njobs);
+    hipLaunchKernelGGL(k_dword_store, dim3(grid), dim3(BLOCK), 0, 0, (uint32_t*)buf2, GiB / 4);
+    hipLaunchKernelGGL(k_gen_stores<640>, dim3(2048), dim3(BLOCK), 0, 0, gmt, gmc, gjobs, njobs);
+  }
   CHECK(hipDeviceSynchronize());
+  CHECK(hipFree(gmt));
+  CHECK(hipFree(gmc));
+  CHECK(hipFree(gjobs));
   // bytes each dispatch requests (loads or stores)
   printf("  \"k_dword\": %llu,\n", (unsigned long long)GiB);
   printf("  \"k_dword_store\": %llu,\n", (unsigned long long)GiB);
@@ -140,7 +200,9 @@ int main() {
   printf("  \"k_env_load<uint4>\": %llu,\n", (unsigned long long)(16 * nenv));
   printf("  \"k_env_load<uint2>\": %llu,\n", (unsigned long long)(8 * nenv));
   printf("  \"k_env_store<uint4>\": %llu,\n", (unsigned long long)(16 * nenv));
-  printf("  \"k_env_store<uint2>\": %llu\n", (unsigned long long)(8 * nenv));
+  printf("  \"k_env_store<uint2>\": %llu,\n", (unsigned long long)(8 * nenv));
+  printf("  \"k_gen_stores<624>\": %llu,\n", (unsigned long long)njobs * 8 * (2496 + 312));
+  printf("  \"k_gen_stores<640>\": %llu\n", (unsigned long long)njobs * 8 * (2496 + 312));
   printf("}}\n");
   CHECK(hipFree(buf));
   CHECK(hipFree(buf2));
