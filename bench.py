@@ -139,9 +139,9 @@ def parse(argv=None):
                          "every K steps")
     ap.add_argument("--progress", action="store_true",
                     help="a line on stderr every 500 untimed steps (profiler runs)")
-    ap.add_argument("--timing-every", type=int, default=8,
-                    help="HIP-event timing of every k-th timed step (its kernels' durations for "
-                         "the roofline); an event record between kernels costs the stream ~5 us")
+    ap.add_argument("--timing-every", type=int, default=1,
+                    help="kernel spans of every k-th timed step (in-kernel s_memrealtime stamps: "
+                         "nothing goes on the stream) for the roofline")
     ap.add_argument("--secondary-steps", type=int, default=30,
                     help="N = 1, c3: steps of the masked-policy line (0 disables it)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -427,15 +427,21 @@ class Runner:
         if self.world > 1:
             dist.barrier()
         torch.cuda.synchronize(self.dev)
+        # HIP events on the step's stream (torch's current stream, which the steps use) around
+        # the whole timed region: two records, none between kernels
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        ev0.record()
         for _ in range(steps):
             self.step(t)
             t += 1
         self.tg._lib.check(self.L.tg_regenerate(self.h, self.stream), "tg_regenerate")
+        ev1.record()
         torch.cuda.synchronize(self.dev)
         if self.world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
+        self.events_ms = ev0.elapsed_time(ev1)
         self.timing = False
         vec.set_timing(0)
         st = vec.stats()
@@ -486,25 +492,21 @@ def step_line(args, runner, dt, st, node, world, total):
     """the bench line's roofline / counters for the c3 step measurement: the dominant kernel
     (k_run; k_step in the direct mode) over its own duration, the step's kernels beside.
 
-    Durations: every --timing-every-th timed step is sampled (tg_set_timing): a HIP event pair on
-    the step's stream brackets its kernels (the step's event time), and each kernel's span, from
-    its first wave's start to its last wave's end, comes from in-kernel s_memrealtime stamps
-    (tg_amd.hip kst_end; no event between the kernels, so nothing is added to the stream
-    between them).  k_regen: its own event pair and span per launch.  The spans are the
-    kernels' durations; the rocprofv3 trace of the same command agrees with them
-    (profiles/<tag>_summary.json)."""
+    Durations: the kernels of every --timing-every-th timed step (default every step) and every
+    k_regen launch record their span, from the first wave's start to the last wave's end, by
+    in-kernel s_memrealtime stamps (tg_amd.hip kst_end: two returnless atomics per wave, nothing
+    on the stream); a HIP event pair on the step's stream brackets the whole timed region.  The
+    rocprofv3 kernel trace of the same command agrees with the spans (profiles/<tag>*)."""
     env_steps = total * args.steps
     assert node["steps"] == env_steps, (node, env_steps)
     launches = max(st["launches"], 1)
     timed = max(st["timed_launches"], 1)
-    event_s = st["kernel_ms"] / 1e3 / timed     # a sampled step, event to event
     run_s = st["run_ms"] / 1e3 / timed          # k_run's span (k_step's in the direct mode)
     cls_s = st["classify_ms"] / 1e3 / timed     # k_classify's span
     cls_b, run_b, regen_b = (b / launches for b in alg_bytes(st, args.mode))
     rl = st.get("regen_launches", 0)
     rt = st.get("regen_timed", 0)
-    regen_launch_s = st["regen_span_ms"] / 1e3 / rt if rt else 0.0
-    regen_event_s = st["regen_ms"] / 1e3 / rt if rt else 0.0
+    regen_launch_s = st["regen_ms"] / 1e3 / rt if rt else 0.0
     regen_s = regen_launch_s * rl / launches    # per step
     surv = survey_bytes(st) / launches
     d = node["draws"] / max(node["steps"], 1)
@@ -542,8 +544,8 @@ def step_line(args, runner, dt, st, node, world, total):
             "kernel_ms": run_s * 1e3, "alg_bytes_per_launch": run_b,
             "timed_launches": st["timed_launches"],
             "timing": "every %d-th timed step: the kernel's span from its first wave's start to "
-                      "its last wave's end (in-kernel s_memrealtime stamps), HIP events on the "
-                      "step's stream around the step" % args.timing_every,
+                      "its last wave's end (in-kernel s_memrealtime stamps); HIP events on the "
+                      "step's stream around the timed region (events_ms)" % args.timing_every,
             "rocprof_ms": run_k.get("rocprof_ms"),
             "limiter": run_k.get("limiter"), "valu_util": run_k.get("valu_util"),
             "wait_frac": run_k.get("wait_frac"), "lane_efficiency": lane_eff,
@@ -571,15 +573,14 @@ def step_line(args, runner, dt, st, node, world, total):
                 "alg_bytes_per_generation": REGEN_GEN,
                 "traffic_per_generation": tr_gen,
                 "ms_per_1k_generations": regen_launch_s * 1e3 / gens_launch * 1e3
-                if gens_launch else None,
-                "event_ms": regen_event_s * 1e3})
+                if gens_launch else None})
     all_b, all_s = cls_b + run_b + regen_b, cls_s + run_s + regen_s
     ms_step = dt / args.steps * 1e3
     roof["step"] = {"kernel": "tg_step = " + (" + ".join(
                         ["k_classify", "k_run", "k_regen / steps per launch"]
                         if args.mode == "compact" else ["k_step"])),
                     "alg_bytes_per_launch": all_b, "kernel_ms": all_s * 1e3,
-                    "event_ms": event_s * 1e3,
+                    "events_ms_per_step": runner.events_ms / args.steps,
                     "gaps_ms": ms_step - all_s * 1e3,
                     "achieved": all_b / all_s / 1e9,
                     "frac": all_b / all_s / 1e9 / HBM_PEAK_GBS,

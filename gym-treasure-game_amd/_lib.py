@@ -60,7 +60,7 @@ class Stats(ctypes.Structure):
                 ("wave_ticks", ctypes.c_int64), ("timed_launches", ctypes.c_int64),
                 ("run_ms", ctypes.c_double), ("regen_ms", ctypes.c_double),
                 ("regen_timed", ctypes.c_int64), ("regen_launches", ctypes.c_int64),
-                ("classify_ms", ctypes.c_double), ("regen_span_ms", ctypes.c_double)]
+                ("classify_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -378,21 +378,22 @@ __device__ __forceinline__ int wave_max(int v) {
 // flush_timing reduces them to the launch's span, first wave start to last wave end.  Null
 // record: not timed (a wave-uniform branch).
 constexpr int KST_SLOTS = 64;
+constexpr int KST_STRIDE = 16;  // u64 per slot: each slot's pair in a 128-B line of its own
 __device__ __forceinline__ unsigned long long kst_begin(const unsigned long long* ks) {
   return ks ? __builtin_amdgcn_s_memrealtime() : 0ull;
 }
 __device__ __forceinline__ void kst_end(unsigned long long* ks, unsigned long long t0) {
   if (ks && (threadIdx.x & 63) == 0) {
-    unsigned long long* const s = ks + 2 * (blockIdx.x % KST_SLOTS);
+    unsigned long long* const s = ks + KST_STRIDE * (blockIdx.x % KST_SLOTS);
     atomicMin(s, t0);
     atomicMax(s + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 }
-__global__ void k_kst_init(unsigned long long* ks, int64_t pairs) {
+__global__ void k_kst_init(unsigned long long* ks, int64_t slots) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < pairs) {
-    ks[2 * i] = ~0ull;
-    ks[2 * i + 1] = 0ull;
+  if (i < slots) {
+    ks[KST_STRIDE * i] = ~0ull;
+    ks[KST_STRIDE * i + 1] = 0ull;
   }
 }
 
@@ -1380,87 +1381,68 @@ int run_grid_for(int64_t n) { return grid_for(n) + (O_COUNT * 64 + BLOCK - 1) / 
 // one launch-counter slot per workgroup of the widest step launch (k_run)
 int stat_slots(int64_t n) { return run_grid_for(n); }
 
-// Timing (tg_set_timing): a sampled step launch records a HIP event before its first kernel
-// and after its last, and its kernels fold their in-kernel span stamps into the sample's
-// record (kst_end); k_regen likewise.  Records: KST_MAX samples of step launches (two kernels
-// each) and KST_MAX of k_regen launches, KST_SLOTS (start, end) pairs per kernel.
+// Timing (tg_set_timing): the kernels of a sampled step launch (and every k_regen launch while
+// timing is on) fold their in-kernel span stamps into the launch's record (kst_end): no event or
+// other packet goes on the stream.  Records: KST_MAX step samples (two kernels each) and KST_MAX
+// k_regen launches, KST_SLOTS slots per kernel.
 constexpr int KST_MAX = 512;
-constexpr int64_t KST_PAIRS = (int64_t)KST_MAX * 3 * KST_SLOTS;
+constexpr int64_t KST_KSLOTS = (int64_t)KST_MAX * 3 * KST_SLOTS;  // slots of all records
 unsigned long long* kst_step(tg_batch* h, int k, int kernel) {
-  return h->kst + ((size_t)k * 2 + kernel) * 2 * KST_SLOTS;
+  return h->kst + ((size_t)k * 2 + kernel) * KST_STRIDE * KST_SLOTS;
 }
 unsigned long long* kst_regen(tg_batch* h, int k) {
-  return h->kst + ((size_t)KST_MAX * 2 + k) * 2 * KST_SLOTS;
+  return h->kst + ((size_t)KST_MAX * 2 + k) * KST_STRIDE * KST_SLOTS;
 }
 int kst_reset(tg_batch* h) {  // every record to (no start, no end)
-  if (!h->kst && hipMalloc((void**)&h->kst, sizeof(unsigned long long) * 2 * KST_PAIRS) != hipSuccess)
+  if (!h->kst && hipMalloc((void**)&h->kst, sizeof(unsigned long long) * KST_STRIDE * KST_KSLOTS) !=
+                     hipSuccess)
     return fail(TG_E_NOMEM, "timing records");
-  hipLaunchKernelGGL(k_kst_init, dim3((unsigned)((KST_PAIRS + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, 0,
-                     h->kst, KST_PAIRS);
+  hipLaunchKernelGGL(k_kst_init, dim3((unsigned)((KST_KSLOTS + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, 0,
+                     h->kst, KST_KSLOTS);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipDeviceSynchronize());
-  h->ev_used = 0;
-  h->rev_used = 0;
+  h->kst_steps = 0;
+  h->kst_regens = 0;
   return TG_OK;
 }
 // a kernel record's span in ms (first wave start to last wave end; 0 if it never ran)
 double kst_span_ms(const unsigned long long* rec) {
   unsigned long long t0 = ~0ull, t1 = 0ull;
   for (int j = 0; j < KST_SLOTS; ++j) {
-    if (rec[2 * j] < t0) t0 = rec[2 * j];
-    if (rec[2 * j + 1] > t1) t1 = rec[2 * j + 1];
+    if (rec[KST_STRIDE * j] < t0) t0 = rec[KST_STRIDE * j];
+    if (rec[KST_STRIDE * j + 1] > t1) t1 = rec[KST_STRIDE * j + 1];
   }
   return t1 > t0 ? (double)(t1 - t0) * 1e-5 : 0.0;  // 100 MHz ticks
 }
 int flush_timing(tg_batch* h) {
-  const size_t ns = h->ev_used / 2, nr = h->rev_used / 2;
-  if (!ns && !nr) return TG_OK;
+  if (!h->kst_steps && !h->kst_regens) return TG_OK;
   HIP_TRY(hipDeviceSynchronize());
-  std::vector<unsigned long long> rec((size_t)2 * KST_PAIRS);
+  std::vector<unsigned long long> rec((size_t)KST_STRIDE * KST_KSLOTS);
   HIP_TRY(hipMemcpy(rec.data(), h->kst, sizeof(unsigned long long) * rec.size(), hipMemcpyDeviceToHost));
-  for (size_t k = 0; k < ns; ++k) {
-    float all = 0.f;
-    HIP_TRY(hipEventElapsedTime(&all, h->ev[2 * k], h->ev[2 * k + 1]));
-    h->kernel_ms_done += all;
-    h->classify_ms_done += kst_span_ms(rec.data() + (k * 2 + 0) * 2 * KST_SLOTS);
-    h->run_ms_done += kst_span_ms(rec.data() + (k * 2 + 1) * 2 * KST_SLOTS);
+  const size_t kr = (size_t)KST_STRIDE * KST_SLOTS;  // u64 per kernel record
+  for (int k = 0; k < h->kst_steps; ++k) {
+    const double c = kst_span_ms(rec.data() + (k * 2 + 0) * kr), r = kst_span_ms(rec.data() + (k * 2 + 1) * kr);
+    h->classify_ms_done += c;
+    h->run_ms_done += r;
+    h->kernel_ms_done += c + r;
     ++h->timed_launches;
   }
-  for (size_t k = 0; k < nr; ++k) {
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, h->rev[2 * k], h->rev[2 * k + 1]));
-    h->regen_ms_done += ms;
-    h->regen_span_ms_done += kst_span_ms(rec.data() + ((size_t)KST_MAX * 2 + k) * 2 * KST_SLOTS);
+  for (int k = 0; k < h->kst_regens; ++k) {
+    h->regen_ms_done += kst_span_ms(rec.data() + ((size_t)KST_MAX * 2 + k) * kr);
     ++h->regen_timed;
   }
   return kst_reset(h);
 }
-// whether this step launch is sampled; if so its start event is recorded and ks0 / ks1 are
-// its kernels' records
-bool timing_begin(tg_batch* h, hipStream_t st, int& rc, unsigned long long*& ks0,
-                  unsigned long long*& ks1) {
+// whether this step launch is sampled; if so ks0 / ks1 are its kernels' records
+bool timing_begin(tg_batch* h, int& rc, unsigned long long*& ks0, unsigned long long*& ks1) {
   rc = TG_OK;
   ks0 = ks1 = nullptr;
   if (!h->timing_every || (h->timing_calls++ % (uint64_t)h->timing_every) != 0) return false;
-  if (h->ev_used / 2 >= (size_t)KST_MAX && (rc = flush_timing(h))) return false;
-  while (h->ev.size() < h->ev_used + 2) {
-    hipEvent_t ev;
-    if (hipEventCreate(&ev) != hipSuccess) {
-      rc = fail(TG_E_HIP, "hipEventCreate");
-      return false;
-    }
-    h->ev.push_back(ev);
-  }
-  const int k = (int)(h->ev_used / 2);
-  ks0 = kst_step(h, k, 0);
-  ks1 = kst_step(h, k, 1);
-  if (hipEventRecord(h->ev[h->ev_used], st) != hipSuccess) rc = fail(TG_E_HIP, "hipEventRecord");
-  return rc == TG_OK;
-}
-int timing_end(tg_batch* h, hipStream_t st) {
-  HIP_TRY(hipEventRecord(h->ev[h->ev_used + 1], st));
-  h->ev_used += 2;
-  return TG_OK;
+  if (h->kst_steps >= KST_MAX && (rc = flush_timing(h))) return false;
+  ks0 = kst_step(h, h->kst_steps, 0);
+  ks1 = kst_step(h, h->kst_steps, 1);
+  ++h->kst_steps;
+  return true;
 }
 }  // namespace
 
@@ -1572,8 +1554,6 @@ void tg_destroy(tg_batch* h) {
   if (!h) return;
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
-  for (auto ev : h->ev) (void)hipEventDestroy(ev);
-  for (auto ev : h->rev) (void)hipEventDestroy(ev);
   render_free(h->rs);
   void* bufs[] = {h->grid,  h->genrand, h->gotab, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
                   h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
@@ -1603,17 +1583,11 @@ int launch_regen(tg_batch* h, hipStream_t st) {
   if (!h->rpend) return TG_OK;
   unsigned long long* ks = nullptr;
   if (h->timing_every) {
-    if (h->rev_used / 2 >= (size_t)KST_MAX) {
+    if (h->kst_regens >= KST_MAX) {
       const int rc = flush_timing(h);
       if (rc) return rc;
     }
-    while (h->rev.size() < h->rev_used + 2) {
-      hipEvent_t ev;
-      HIP_TRY(hipEventCreate(&ev));
-      h->rev.push_back(ev);
-    }
-    ks = kst_regen(h, (int)(h->rev_used / 2));
-    HIP_TRY(hipEventRecord(h->rev[h->rev_used], st));
+    ks = kst_regen(h, h->kst_regens++);
   }
   // Workgroups take list regions from the counter of their XCD (blockIdx.x % 8) until it runs
   // out, so the grid needs at least 8 of them (one per counter; fewer would leave the regions
@@ -1639,10 +1613,6 @@ int launch_regen(tg_batch* h, hipStream_t st) {
   HIP_TRY(hipGetLastError());
   h->rpend = 0;
   ++h->regen_launches;
-  if (ks) {
-    HIP_TRY(hipEventRecord(h->rev[h->rev_used + 1], st));
-    h->rev_used += 2;
-  }
   return TG_OK;
 }
 // one step's kernels on `st`, timed with HIP events when enabled
@@ -1652,7 +1622,7 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
   const bool fo = io.final_obs != nullptr;
   int rc;
   unsigned long long *ks0, *ks1;
-  const bool timed = timing_begin(h, st, rc, ks0, ks1);
+  timing_begin(h, rc, ks0, ks1);
   if (rc) return rc;
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   const dim3 grid(grid_for(h->n)), block(BLOCK);
@@ -1698,7 +1668,6 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
                        q, w, h->g0, h->stats, h->err, ks1);
   }
   HIP_TRY(hipGetLastError());
-  if (timed && (rc = timing_end(h, st))) return rc;
   if (h->mode != TG_MODE_DIRECT && ++h->rpend == REGEN_STEPS) return launch_regen(h, st);
   return TG_OK;
 }
@@ -1964,7 +1933,6 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   out->regen_timed = h->regen_timed;
   out->regen_launches = h->regen_launches;
   out->classify_ms = h->classify_ms_done;
-  out->regen_span_ms = h->regen_span_ms_done;
   return TG_OK;
 }
 
@@ -1973,17 +1941,14 @@ int tg_stats_reset(tg_batch* h) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(h->n)));
   if (h->kst) {
-    const int rc = kst_reset(h);  // drops the unflushed records (and their events)
+    const int rc = kst_reset(h);  // drops the unflushed records
     if (rc) return rc;
   }
-  h->ev_used = 0;
   h->kernel_ms_done = 0.0;
   h->run_ms_done = 0.0;
   h->classify_ms_done = 0.0;
   h->timed_launches = 0;
-  h->rev_used = 0;
   h->regen_ms_done = 0.0;
-  h->regen_span_ms_done = 0.0;
   h->regen_timed = 0;
   h->regen_launches = 0;
   return TG_OK;

@@ -81,21 +81,17 @@ struct tg_batch {
   int64_t shard_cap = 0;
   int timing_every = 0;        // HIP-event timing of every k-th step launch (0: off)
   uint64_t timing_calls = 0;   // step launches since timing was enabled
-  std::vector<hipEvent_t> ev;  // (before the first kernel, after the last) pairs
-  size_t ev_used = 0;
   unsigned long long* kst = nullptr;  // in-kernel span records of the timed launches (tg_amd.hip)
-  double kernel_ms_done = 0.0;  // the timed step launches, by their event pairs
-  double classify_ms_done = 0.0;  // their k_classify spans (in-kernel stamps)
-  double run_ms_done = 0.0;     //   and k_run (or k_step) spans
+  int kst_steps = 0, kst_regens = 0;  // records in use
+  double kernel_ms_done = 0.0;  // the timed step launches' kernel spans (in-kernel stamps)
+  double classify_ms_done = 0.0;  //   of which k_classify
+  double run_ms_done = 0.0;     //   and k_run (or k_step)
   int64_t timed_launches = 0;
   int rpend = 0;                    // compact steps whose refill lists k_regen has not drained
   int regen_per_cu = 0;             // k_regen workgroups resident per CU (occupancy API, first use)
   int32_t* regen_ctr = nullptr;     // k_regen's per-XCD region counters, two sets (k_regen
                                     // zeroes the other set for the next launch)
-  std::vector<hipEvent_t> rev;      // k_regen's (start, stop) pairs while timing is on
-  size_t rev_used = 0;
-  double regen_ms_done = 0.0;       // the timed k_regen launches (events)
-  double regen_span_ms_done = 0.0;  //   (in-kernel stamps)
+  double regen_ms_done = 0.0;       // the timed k_regen launches' spans (in-kernel stamps)
   int regen_parity = 0;             // which set of regen_ctr the next k_regen counts in
   int64_t regen_launches = 0;       // k_regen launches (timed or not)
   int64_t regen_timed = 0;

@@ -94,22 +94,21 @@ typedef struct {
   int64_t episodes;     /* completed episodes (auto-reset) */
   int64_t episodes_dropped; /* records lost because the queue (max(4N, 65536)) was full */
   int64_t launches;     /* step-kernel launches */
-  double kernel_ms;     /* summed time of the timed step launches (tg_set_timing): HIP events
-                           on the step's stream before its first kernel and after its last */
+  double kernel_ms;     /* summed kernel time of the timed step launches (tg_set_timing): each
+                           kernel's span from its first wave's start to its last wave's end, by
+                           in-kernel s_memrealtime stamps (100 MHz); nothing goes on the stream */
   int64_t regens;       /* MT19937 generations regenerated by the step kernels (624 words +
                            312 random() values each) */
   int64_t wave_ticks;   /* sum over the tick loops' wavefronts of their longest lane's ticks:
                            lane efficiency = ticks / (64 * wave_ticks) (an upper bound for the
                            go loops, whose lanes may also wait for the others' plain ticks) */
   int64_t timed_launches; /* launches timed (tg_set_timing) */
-  double run_ms;        /* the timed launches' second kernel (k_run in the compact mode; the single
-                           kernel of the direct launches): its span from the first wave's start
-                           to the last wave's end, by in-kernel s_memrealtime stamps (100 MHz) */
-  double regen_ms;      /* summed k_regen time of the timed k_regen launches (HIP events) */
+  double run_ms;        /* of kernel_ms, the second kernel (k_run in the compact mode; the single
+                           kernel of the direct launches) */
+  double regen_ms;      /* summed span of the k_regen launches while timing is on */
   int64_t regen_timed;  /* k_regen launches timed (while tg_set_timing is on) */
   int64_t regen_launches; /* k_regen launches (deferred MT regenerations, tg_regenerate) */
-  double classify_ms;   /* the timed launches' k_classify spans (in-kernel stamps, as run_ms) */
-  double regen_span_ms; /* the timed k_regen launches' spans (in-kernel stamps) */
+  double classify_ms;   /* of kernel_ms, k_classify */
 } tg_stats;
 
 /* Create N envs on `device`: env i is `random.seed(seed_base + global_offset + i);
