@@ -74,10 +74,12 @@ struct LdsLevel {
   uint32_t grid[MAX_CELLS / 4];
 };
 __device__ __forceinline__ void stage_level(LdsLevel& lv, const uint32_t* __restrict__ grid,
-                                            const Level& L) {
+                                            const Level& L, uint32_t* masks = nullptr) {
   const int nwords = ((L.W + 2 * PAD) * (L.H + 2 * PAD) + 3) / 4;
   for (int i = threadIdx.x; i < nwords; i += BLOCK) lv.grid[i] = grid[i];
   if (threadIdx.x < 12) lv.trig[threadIdx.x] = L.trig[threadIdx.x >> 1][threadIdx.x & 1];
+  if (masks && L.masks)
+    for (int i = threadIdx.x; i < mk_words(L.W, L.H); i += BLOCK) masks[i] = L.masks[i];
   __syncthreads();
 }
 #define LEVEL_IN_LDS()                   \
@@ -85,6 +87,13 @@ __device__ __forceinline__ void stage_level(LdsLevel& lv, const uint32_t* __rest
   stage_level(lv, grid, L);              \
   const uint32_t* const trig = lv.trig;  \
   const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H}
+// the same with the level bitmasks (Map::mk) staged too: the option loops' kernels
+#define LEVEL_IN_LDS_MK()                                                      \
+  __shared__ LdsLevel lv;                                                      \
+  __shared__ uint32_t lmk[MK_MAX_WORDS];                                       \
+  stage_level(lv, grid, L, lmk);                                               \
+  const uint32_t* const trig = lv.trig;                                        \
+  const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H, L.masks ? lmk : nullptr}
 
 __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o[9]) {
   double* p = out + i * 9;
@@ -938,7 +947,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     oraw[O_COUNT] = pre[NSEG];
   }
   __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
-  LEVEL_IN_LDS();  // includes the barrier
+  LEVEL_IN_LDS_MK();  // includes the barrier
   const int total = ostart[O_COUNT];
   const int base = (blockIdx.x * BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
   int oj = 0;  // ostart[oj] <= base < ostart[oj + 1] (wave-uniform)
@@ -1506,6 +1515,9 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   const std::vector<uint32_t> gotab = build_gotab(L, grid);
   ALLOC(h->gotab, sizeof(uint32_t) * gotab.size());
   L.gotab = h->gotab;
+  const std::vector<uint32_t> masks = build_masks(L, grid);
+  if (!masks.empty()) ALLOC(h->masks, sizeof(uint32_t) * masks.size());
+  L.masks = h->masks;
   h->L = L;
   ALLOC(h->S.st4, sizeof(uint4) * n);
   ALLOC(h->S.ang, sizeof(double2) * n);
@@ -1530,6 +1542,8 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->gotab, gotab.data(), sizeof(uint32_t) * gotab.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      (h->masks && hipMemcpy(h->masks, masks.data(), sizeof(uint32_t) * masks.size(),
+                             hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
       hipMemset(h->wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE) != hipSuccess ||
       hipMemset(h->regen_ctr, 0, sizeof(int32_t) * 2 * 8 * CTR_STRIDE) != hipSuccess ||
@@ -1555,7 +1569,7 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   render_free(h->rs);
-  void* bufs[] = {h->grid,  h->genrand, h->gotab, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
+  void* bufs[] = {h->grid,  h->genrand, h->gotab, h->masks, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
                   h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
                   h->wst4,  h->wang,    h->wep,
                   h->wctr,  h->refill,  h->nrefill,   h->obs_scratch, h->regen_ctr, h->kst};

@@ -61,6 +61,7 @@ struct tg_batch {
   uint32_t* genrand = nullptr;
   // GoTable (tg_core.h go_lookup): W * H * 32 entries
   uint32_t* gotab = nullptr;
+  uint32_t* masks = nullptr;  // the level bitmasks (tg_core.h Map::mk), or null
   int cus = 0;  // compute units
   tg::Soa S{};
   tg_episode* eps = nullptr;

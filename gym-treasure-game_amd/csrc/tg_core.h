@@ -80,6 +80,9 @@ struct Level {
   // go_left / go_right can_run and target per (cell, door state, key home?, gold home?)
   // (GoTable; device global memory, built at tg_create; null: computed directly)
   const uint32_t* gotab;
+  // the level bitmasks (Map::mk; mk_words(W, H) words, device global memory, staged into LDS
+  // by the kernels that use them; null: the level is too large, cell probes)
+  const uint32_t* masks;
 };
 
 // ---- per-env state (registers) -------------------------------------------------------------
@@ -386,12 +389,19 @@ struct AirCells {
     const uint32_t r = rows_open(px - HALFW + 2, px + HALFW - 2);
     return ((r >> ri2(py)) & (r >> ri2(py + S + 2)) & 1u) != 0;
   }
-  TG_HD uint32_t can_fall4(int px, int py) const {  // Map::can_fall4
+  // the distance of a downward move of yd <= 4 px from (px, py) (IM/:341-348, Map::fall): the
+  // probes at py + k and py + 50 + k (k < 4) cross at most one row boundary each, at k = ka / kb
+  TG_HD int fall(int px, int py, int yd) const {
     const uint32_t r = rows_open(px - HALFW + 2, px + HALFW - 2);
-    uint32_t b = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) b |= ((r >> ri2(py + k)) & (r >> ri2(py + S + 2 + k)) & 1u) << k;
-    return b;
+    const int ya = py, yb = py + S + 2;
+    const uint32_t ra = ri2(ya), rb = ri2(yb);
+    if (!((r >> ra) & (r >> rb) & 1u)) return yd;
+    const int ka = ya < by1 ? by1 - ya : ya < by2 ? by2 - ya : 4;  // (no boundary in reach: 4)
+    const int kb = yb < by1 ? by1 - yb : yb < by2 ? by2 - yb : 4;
+    int d = yd;
+    if (!((r >> (ra + 2u)) & 1u)) d = min(d, ka);
+    if (!((r >> (rb + 2u)) & 1u)) d = min(d, kb);
+    return d;
   }
   TG_HD bool side(int px, int py, int dir) const {  // can_go_side
     const uint32_t c = ci(px + dir * (HALFW + INCR));
@@ -403,11 +413,32 @@ struct AirCells {
   }
 };
 
+// ---- level bitmasks (Map::mk) -------------------------------------------------------------------
+// For levels of at most MK_DIM - 2 PAD cells a side (the default 14 x 13 is 18 x 17 bordered):
+// per bordered column (index c + PAD) the rows holding a LADDER (bit r + PAD); per door state and
+// column the OPEN rows; per door state and bordered row the OPEN columns and the WALL-or-closed-
+// door columns (bit c + PAD).  Built on the host from the grid (tg_level.h build_masks) and
+// staged with it; a predicate that would read several cells of one column or row reads one word
+// and tests bits (the ladder and go loops' span limits).  Null: the cell probes.
+constexpr int MK_DIM = 32;
+constexpr int MK_MAX_WORDS = 25 * MK_DIM;  // 9 column tables + 16 row tables
+TG_HD int mk_words(int W, int H) { return 9 * (W + 2 * PAD) + 16 * (H + 2 * PAD); }
+
 struct Map {
   const uint8_t* g;  // LDS on device: (H + 2*PAD) rows of (W + 2*PAD) cells
   int W, H;
+  const uint32_t* mk = nullptr;  // the level bitmasks (LDS on device), or null
 
   TG_HD int pw() const { return W + 2 * PAD; }
+  TG_HD int ph() const { return H + 2 * PAD; }
+  // mask words: c / r are clamped column / row indices (colx / rowy)
+  TG_HD uint32_t mk_lad(int c) const { return mk[c + PAD]; }
+  TG_HD uint32_t mk_colopen(uint32_t dc, int c) const { return mk[pw() * (1 + (int)dc) + c + PAD]; }
+  TG_HD uint32_t mk_rowopen(uint32_t dc, int r) const { return mk[9 * pw() + ph() * (int)dc + r + PAD]; }
+  TG_HD uint32_t mk_rowblk(uint32_t dc, int r) const {
+    return mk[9 * pw() + ph() * (8 + (int)dc) + r + PAD];
+  }
+  TG_HD uint32_t rbit(int y) const { return (uint32_t)(rowy(y) + PAD); }  // row bit of pixel y
   // object_type_at_cell (IM/:227-230) as cell bits; anything outside the grid is WALL
   TG_HD uint32_t cellb(int cx, int cy) const {
     cx = clampi(cx, -PAD, W + PAD - 1);
@@ -491,9 +522,13 @@ struct Map {
     }
     return AirCells{op, bl, (c0 + 1) * S, (r0 + 1) * S, (r0 + 2) * S, dc};
   }
-  // can_fall at (px, py + k) for k = 0..3 as bits 0..3: the probes (px -+ 10 at py + k and
-  // py + 50 + k) span at most two rows each, so 8 lookups instead of 16
-  TG_HD uint32_t can_fall4(uint32_t dc, int px, int py) const {
+  // integrate y on a downward move of yd <= 4 px (IM/:341-348): with can_fall at py the player
+  // falls pixel by pixel while can_fall holds, so the distance is the first k in 1..yd-1 with
+  // !can_fall(py + k), else yd.  The probes (px -+ 10 at py + k and py + 50 + k, k < 4) span at
+  // most two rows each, entering the second at k = ka / kb: 8 lookups instead of 16, and the
+  // first failing k in closed form (rows past the border clamp to the same WALL row, where
+  // both lookups agree anyway)
+  TG_HD int fall(uint32_t dc, int px, int py, int yd) const {
     const int ca = colx(px - HALFW + 2), cb = colx(px + HALFW - 2);
     const int ya = py, yb = py + S + 2;
     const int ra0 = rowy(ya), ra1 = rowy(ya + 3), rb0 = rowy(yb), rb1 = rowy(yb + 3);
@@ -501,14 +536,46 @@ struct Map {
     const bool a1 = is_open(cellb(ca, ra1), dc) & is_open(cellb(cb, ra1), dc);
     const bool b0 = is_open(cellb(ca, rb0), dc) & is_open(cellb(cb, rb0), dc);
     const bool b1 = is_open(cellb(ca, rb1), dc) & is_open(cellb(cb, rb1), dc);
-    // y + k lies in the second row from k = 48 - (y mod 48) on (rows past the border clamp to
-    // the same WALL row, where both lookups agree anyway)
+    if (!(a0 & b0)) return yd;
     const int ka = S - (ya - floordiv48(ya) * S), kb = S - (yb - floordiv48(yb) * S);
-    uint32_t r = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      r |= (uint32_t)((k < ka ? a0 : a1) & (k < kb ? b0 : b1)) << k;
-    return r;
+    int d = yd;
+    if (!a1) d = min(d, ka);
+    if (!b1) d = min(d, kb);
+    return d;
+  }
+};
+
+// The ladder options' probes from the level bitmasks: px is fixed while a ladder option runs
+// (its primitives UP / DOWN / NOP and the gravity move only py), and so are the door states, so
+// the columns of every probe are: LADDER rows at px -+ 12 (can_go_up / can_go_down), OPEN rows at
+// both px -+ 10 (can_fall) and at both px -+ 4 (up_clear, for a leftover jump ticker).
+struct LadMasks {
+  uint32_t lad, fall, up;
+  TG_HD LadMasks(const Map& m, uint32_t dc, int px)
+      : lad(m.mk_lad(m.colx(px - HALFW)) | m.mk_lad(m.colx(px + HALFW))),
+        fall(m.mk_colopen(dc, m.colx(px - HALFW + 2)) & m.mk_colopen(dc, m.colx(px + HALFW - 2))),
+        up(m.mk_colopen(dc, m.colx(px - INCR)) & m.mk_colopen(dc, m.colx(px + INCR))) {}
+  // Map::can_go_up / can_go_down / can_fall_at / up_clear / fall at (px, py)
+  TG_HD bool can_go_up(const Map& m, int py) const {
+    return (py > 1) & ((((lad >> m.rbit(py - INCR)) | (lad >> m.rbit(py)) | (lad >> m.rbit(py + S - INCR))) & 1u) != 0);
+  }
+  TG_HD bool can_go_down(const Map& m, int py) const {
+    return (((lad >> m.rbit(py)) | (lad >> m.rbit(py + S / 2)) | (lad >> m.rbit(py + S + INCR - 1))) & 1u) != 0;
+  }
+  TG_HD bool can_fall(const Map& m, int py) const {
+    return ((fall >> m.rbit(py)) & (fall >> m.rbit(py + S + 2)) & 1u) != 0;
+  }
+  TG_HD bool up_clear(const Map& m, int py) const {
+    return ((up >> m.rbit(py - INCR)) & (up >> m.rbit(py - 1)) & 1u) != 0;
+  }
+  TG_HD int fall_dist(const Map& m, int py, int yd) const {
+    const int ya = py, yb = py + S + 2;
+    if (!((fall >> m.rbit(ya)) & (fall >> m.rbit(yb)) & 1u)) return yd;
+    const int ka = S - (ya - floordiv48(ya) * S), kb = S - (yb - floordiv48(yb) * S);
+    int d = yd;
+    if (!((fall >> m.rbit(ya + 3)) & 1u)) d = min(d, ka);
+    if (!((fall >> m.rbit(yb + 3)) & 1u)) d = min(d, kb);
+    return d;
   }
 };
 
@@ -630,8 +697,13 @@ TG_HD void flip(const uint32_t* trig, Env& e, int h, R& rng) {
   }
 }
 
-// pickups in object order: key then goldcoin (IM/:350-354)
+// pickups in object order: key then goldcoin (IM/:350-354).  near_cell needs |dx| < 24 for
+// r = 24, so a tick whose player is 24 px or more from both objects' centres in x (nearly every
+// tick) skips the rest with one combined test.
 TG_HD void pickups(const Level& L, Env& e) {
+  const int dkx = e.px - (e.kx * S + S / 2), dgx = e.px - (e.gx * S + S / 2);
+  if (((uint32_t)(dkx + (S / 2 - 1)) >= (uint32_t)(S - 1)) & ((uint32_t)(dgx + (S / 2 - 1)) >= (uint32_t)(S - 1)))
+    return;
   if (near_cell(e, e.kx, e.ky, R2_OBJ)) {
     e.kx = L.W - 1 - bag_len(e.f);
     e.ky = L.H - 1;
@@ -698,15 +770,7 @@ TG_HD int tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, int p
   e.px += xd;
   // integrate y (IM/:341-348): with yd > 0 and can_fall, fall pixel by pixel while can_fall
   // holds: the distance is the first k in 1..yd-1 with !can_fall(py + k), else yd (yd <= 4)
-  if (yd > 0) {
-    const uint32_t cf = m.can_fall4(Map::dc_of(e.f), e.px, e.py);
-    if (cf & 1u) {
-      int dist = yd;
-      for (int k = yd - 1; k >= 1; --k)
-        if (!((cf >> k) & 1u)) dist = k;
-      yd = dist;
-    }
-  }
+  if (yd > 0) yd = m.fall(Map::dc_of(e.f), e.px, e.py, yd);
   e.py += yd;
   pickups(L, e);
   return may<PM>(prim, P_JUMP) ? -5 : -1;  // JUMP_REWARD / STEP_REWARD (IM/:15-16)
@@ -1020,6 +1084,40 @@ TG_HD int go_plain_limit(const Map& m, const Env& e, int tx) {
   const uint32_t dc = Map::dc_of(e.f);
   const int rs1 = m.rowy(e.py + INCR), rs2 = m.rowy(e.py + S - INCR);  // can_go_side
   const int rf1 = m.rowy(e.py), rf2 = m.rowy(e.py + S + 2);            // can_fall
+  if (m.mk) {  // the same two scans as bit scans over the rows' column masks (below)
+    const int off = DIR * (HALFW + INCR);
+    const int c0 = m.colx(P + off) + PAD, c1 = m.colx(lim + off) + PAD;  // bit indices
+    const uint32_t blk = m.mk_rowblk(dc, rs1) | m.mk_rowblk(dc, rs2);
+    // columns strictly ahead of c0 up to c1
+    const uint32_t ahead = DIR > 0 ? ~((2u << c0) - 1u) & ((2u << c1) - 1u)
+                                   : ((1u << c0) - 1u) & ~((1u << c1) - 1u);
+    const uint32_t hit = blk & ahead;
+    if (hit) {
+      const int c = (DIR > 0 ? __builtin_ctz(hit) : 31 - __builtin_clz(hit)) - PAD;
+      lim = DIR > 0 ? min(lim, c * S - off - 1) : max(lim, c * S + S - 1 - off + 1);
+    }
+    // can_fall: F(c) = both probed cells of column c OPEN; F(lead0) bounds the span at once
+    // (the trailing probe reaches lead0); else the first F column ahead, up to lead1, does
+    // when the trailing probe reaches it (the loop below: an F column right after an F lead0
+    // would bound it later than lead0 already has)
+    const int d = HALFW - 2;  // 10
+    const int l0 = m.colx(P + DIR * d) + PAD, l1 = m.colx(lim + DIR * d) + PAD;
+    const uint32_t F = m.mk_rowopen(dc, rf1) & m.mk_rowopen(dc, rf2);
+    int cf = -1000;
+    if ((F >> l0) & 1u) {
+      cf = l0;
+    } else {
+      const uint32_t fa = F & (DIR > 0 ? ~((2u << l0) - 1u) & ((2u << l1) - 1u)
+                                       : ((1u << l0) - 1u) & ~((1u << l1) - 1u));
+      if (fa) cf = DIR > 0 ? __builtin_ctz(fa) : 31 - __builtin_clz(fa);
+    }
+    if (cf != -1000) {
+      const int c = cf - PAD;
+      const int p_both = DIR > 0 ? c * S + d : c * S + S - 1 - d;
+      lim = DIR > 0 ? min(lim, p_both - 1) : max(lim, p_both + 1);
+    }
+    return lim;
+  }
   // can_go_side(p) reads column colx(p + 16*dir): the span ends before the first column ahead
   // whose two cells hold a WALL or a closed door
   {
@@ -1078,8 +1176,25 @@ TG_HD int isqrt_below(int v) {  // largest t >= 0 with t * t < v (v >= 1)
   while ((t + 1) * (t + 1) < v) ++t;
   return t;
 }
-template <int DIR>  // -1: up_ladder (py decreases), +1: down_ladder
-TG_HD int ladder_plain_limit(const Map& m, const Env& e) {
+// (the predicates at px for a start position py: the cell probes, or the level bitmasks)
+struct LadProbe {
+  const Map& m;
+  const Env& e;
+  TG_HD bool lad(int dir, int y) const {
+    Env p = e;
+    p.py = y;
+    return dir < 0 ? m.can_go_up(p) : m.can_go_down(p);
+  }
+  TG_HD bool fall(uint32_t dc, int y) const { return m.can_fall_at(dc, e.px, y); }
+};
+struct LadProbeMk {
+  const Map& m;
+  const LadMasks& lm;
+  TG_HD bool lad(int dir, int y) const { return dir < 0 ? lm.can_go_up(m, y) : lm.can_go_down(m, y); }
+  TG_HD bool fall(uint32_t, int y) const { return lm.can_fall(m, y); }
+};
+template <int DIR, class P = LadProbe>  // -1: up_ladder (py decreases), +1: down_ladder
+TG_HD int ladder_plain_limit(const Map& m, const Env& e, const P& pr) {
   constexpr int NONE = DIR > 0 ? -0x40000000 : 0x40000000;
   if (e.f & F_JT) return NONE;
   const uint32_t dc = Map::dc_of(e.f);
@@ -1099,10 +1214,7 @@ TG_HD int ladder_plain_limit(const Map& m, const Env& e) {
   int y = e.py, lim = NONE;
   for (int it = 0; it < LADDER_SPAN_INTERVALS; ++it) {
     if (DIR < 0 ? y < bound : y > bound) break;
-    Env p = e;
-    p.py = y;
-    const bool lad = DIR < 0 ? m.can_go_up(p) : m.can_go_down(p);
-    if (!lad || m.can_fall_at(dc, e.px, y)) break;
+    if (!pr.lad(DIR, y) || pr.fall(dc, y)) break;
     // the interval of start positions whose probes (rows of y + o) all stay in their rows
     int end;
     if (DIR < 0) {  // can_go_up: y - 4, y, y + 44; can_fall: y, y + 50
@@ -1160,18 +1272,32 @@ TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng, AirCell
     yd = INCR;
   }
   e.px += xd;
-  if (yd > 0) {  // IM/:341-348 (e.px moved by <= 4: still inside the AirCells)
-    const uint32_t cf = ac.can_fall4(e.px, e.py);
-    if (cf & 1u) {
-      int dist = yd;
-      for (int k = yd - 1; k >= 1; --k)
-        if (!((cf >> k) & 1u)) dist = k;
-      yd = dist;
-    }
-  }
+  if (yd > 0) yd = ac.fall(e.px, e.py, yd);  // (e.px moved by <= 4: still inside the AirCells)
   e.py += yd;
   pickups(L, e);
   return -1;  // STEP_REWARD (no JUMP after the first tick)
+}
+
+// A ladder option's full tick from the level bitmasks: policy<K> (MO/:168-173, 184-189) and
+// tick<prims_of(K)> (IM/:290-359) fused — UP / DOWN when the ladder predicate holds (the tick
+// re-tests it at the same state: the same answer), else NOP and done; then the jump ticker /
+// gravity, the fall integration and the pickups, as tick<>.  Same outcomes and draws.
+template <int DIR, class R>
+TG_HD int ladder_tick(const Level& L, const Map& m, const LadMasks& lm, Env& e, Opt& o, R& rng) {
+  int yd = 0;
+  if (DIR < 0 ? lm.can_go_up(m, e.py) : lm.can_go_down(m, e.py)) yd = code_step(rng.code(), DIR < 0);
+  else o.done = true;
+  const uint32_t jt = e.f & F_JT;  // IM/:331-337
+  if (jt > 0) {
+    if (lm.up_clear(m, e.py)) yd = -INCR;
+    e.f = (e.f & ~F_JT) | (jt - 1);
+  } else if (lm.can_fall(m, e.py)) {
+    yd = INCR;
+  }
+  if (yd > 0) yd = lm.fall_dist(m, e.py, yd);
+  e.py += yd;
+  pickups(L, e);
+  return -1;  // STEP_REWARD
 }
 
 // the while-not-done loop of _Option.run (OP/:28-31) for option K, whose can_run held
@@ -1221,6 +1347,37 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
   if constexpr (K == O_UP_LADDER || K == O_DOWN_LADDER) {
     constexpr int DIR = K == O_UP_LADDER ? -1 : 1;
     int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
+    if (m.mk) {  // the level bitmasks: full ticks and span limits test bits, no cell probes
+      const LadMasks lm(m, Map::dc_of(e.f), e.px);
+      const LadProbeMk pr{m, lm};
+      do {
+        rng.phase(0);
+        bool capped = false;
+        while ((DIR > 0 ? e.py <= lim : e.py >= lim) && rng.has(TICK_DRAWS)) {
+          e.py += code_step(rng.code(), DIR < 0);
+          r.reward += -1;
+          if (DIR > 0 ? e.py > lim : e.py < lim) pickups(L, e);
+          if (++r.ticks >= TICK_CAP) {
+            e.f |= E_TICKCAP;
+            capped = true;
+            lim = DIR > 0 ? -0x40000000 : 0x40000000;
+          }
+        }
+        if (capped) break;
+        rng.phase(1);
+        rng.reserve(TICK_DRAWS);
+        rng.phase(2);
+        r.reward += ladder_tick<DIR>(L, m, lm, e, o, rng);
+        if (!o.done) lim = ladder_plain_limit<DIR>(m, e, pr);
+        rng.phase(3);
+        if (++r.ticks >= TICK_CAP) {
+          e.f |= E_TICKCAP;
+          break;
+        }
+      } while (!o.done);
+      return;
+    }
+    const LadProbe pr{m, e};
     do {
       // plain phase (ladder_plain_limit), then one full tick: as the go loops
       // per tick (a batched walk here, RngCodes::walk, took k_run from 82 to 98 VGPRs: 4
@@ -1243,7 +1400,7 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
       rng.phase(2);
       const int prim = policy<K>(L, m, e, o);
       r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
-      if (!o.done) lim = ladder_plain_limit<DIR>(m, e);
+      if (!o.done) lim = ladder_plain_limit<DIR>(m, e, pr);
       rng.phase(3);
       if (++r.ticks >= TICK_CAP) {
         e.f |= E_TICKCAP;

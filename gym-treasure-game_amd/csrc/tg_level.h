@@ -243,4 +243,25 @@ inline std::vector<uint32_t> build_gotab(const Level& Lin, const std::vector<uin
   return tab;
 }
 
+// The level bitmasks (tg_core.h Map::mk) of a parsed level's bordered grid, or empty when a
+// bordered side exceeds MK_DIM cells.
+inline std::vector<uint32_t> build_masks(const Level& L, const std::vector<uint8_t>& grid) {
+  const int PW = L.W + 2 * PAD, PH = L.H + 2 * PAD;
+  if (PW > MK_DIM || PH > MK_DIM) return {};
+  std::vector<uint32_t> mk((size_t)mk_words(L.W, L.H), 0u);
+  for (int ri = 0; ri < PH; ++ri)
+    for (int ci = 0; ci < PW; ++ci) {
+      const uint32_t c = grid[(size_t)ri * PW + ci];
+      if (Map::is_ladder(c)) mk[ci] |= 1u << ri;
+      for (uint32_t dc = 0; dc < 8; ++dc) {
+        if (Map::is_open(c, dc)) {
+          mk[PW * (1 + dc) + ci] |= 1u << ri;
+          mk[9 * PW + PH * dc + ri] |= 1u << ci;
+        }
+        if (Map::is_wall(c) | Map::is_door(c, dc)) mk[9 * PW + PH * (8 + dc) + ri] |= 1u << ci;
+      }
+    }
+  return mk;
+}
+
 }  // namespace tg

@@ -213,11 +213,12 @@ def render_summary(a):
                         "frame_bytes_algorithmic": 1257984 * envs,
                         "avg_ns": ks["k_render"]["avg_ns"]},
            "fetch_calibration": cal}
-    with open(os.path.join(ROOT, "profiles", "%s_summary.json" % tag), "w") as f:
+    os.makedirs(a.dest, exist_ok=True)
+    with open(os.path.join(a.dest, "%s_summary.json" % tag), "w") as f:
         json.dump(res, f, indent=1)
     tj = {"envs": envs, "kernel": "k_render", "hbm_bytes_per_launch": fr * cal + wr,
           "avg_ns": ks["k_render"]["avg_ns"], "source": "profiles/%s_summary.json" % tag}
-    with open(os.path.join(ROOT, "profiles", "traffic_render.json"), "w") as f:
+    with open(os.path.join(a.dest, "traffic_render.json"), "w") as f:
         json.dump(tj, f, indent=1)
     print(json.dumps(res["k_render"], indent=1))
 

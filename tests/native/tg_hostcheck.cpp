@@ -38,6 +38,10 @@ extern "C" {
 // go_left / go_right answered from the GoTable as on the device (1, default) or directly (0)
 static int g_gotab = 1;
 void hc_set_gotab(int on) { g_gotab = on; }
+// the level bitmasks (tg_core.h Map::mk) as on the device's option loops (1, default) or not (0)
+static int g_masks = 1;
+void hc_set_masks(int on) { g_masks = on; }
+static std::vector<uint32_t> g_mk;  // the last loaded level's masks
 
 static bool load_level(const char* dom, const char* objs, const char* inter, Level& L,
                        std::vector<uint8_t>& grid, std::vector<uint32_t>& tab) {
@@ -52,6 +56,8 @@ static bool load_level(const char* dom, const char* objs, const char* inter, Lev
     tab = build_gotab(L, grid);
     L.gotab = tab.data();
   }
+  g_mk = g_masks ? build_masks(L, grid) : std::vector<uint32_t>();
+  L.masks = g_mk.empty() ? nullptr : g_mk.data();
   return true;
 }
 
@@ -69,7 +75,7 @@ int hc_run(const char* dom, const char* objs, const char* inter, uint64_t seed_b
   uint32_t gen[MT_N];
   gen[0] = 19650218u;
   for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
-  const Map m{grid.data(), L->W, L->H};
+  const Map m{grid.data(), L->W, L->H, L->masks};
   const uint32_t* trig = &L->trig[0][0];
   const int64_t T1 = (int64_t)steps + 1;
   std::vector<uint32_t> mt(MT_WORDS);

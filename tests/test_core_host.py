@@ -167,6 +167,24 @@ def test_core_gotable_matches_direct(hostcheck, level, policy):
     np.testing.assert_array_equal(direct["ticks"], table["ticks"])
 
 
+@pytest.mark.parametrize("level", [None, "corridor", "gen1", "gen2", "gen3", "exit", "cascade"])
+@pytest.mark.parametrize("policy", [0, 1])
+def test_core_level_masks_match_cell_probes(hostcheck, level, policy):
+    """The level bitmasks (tg_core.h Map::mk: the ladder options' fused full tick and span
+    limits, the go options' span limits as bit scans; the device's path) against the cell
+    probes they replace, over whole auto-reset trajectories on seven levels, and both against
+    the oracle (the other host tests run with the masks on)."""
+    ld = None if level is None else os.path.join(LEVELS, level)
+    try:
+        hostcheck.hc_set_masks(0)
+        probes = hc_run(hostcheck, 13, 0, 512, 80, 0xFACE, policy, True, level_dir=ld)
+    finally:
+        hostcheck.hc_set_masks(1)
+    masks = hc_run(hostcheck, 13, 0, 512, 80, 0xFACE, policy, True, level_dir=ld)
+    assert_same(probes, masks)
+    np.testing.assert_array_equal(probes["ticks"], masks["ticks"])
+
+
 def test_draw_code_from_the_top_27_bits(hostcheck):
     """code_of_top27 (k_regen's code pass: one tempered word, integer compares) equals
     draw_code(random()) at both ends of every interval of 2^26 draws it decides; draw_code's
