@@ -1518,6 +1518,9 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   const std::vector<uint32_t> masks = build_masks(L, grid);
   if (!masks.empty()) ALLOC(h->masks, sizeof(uint32_t) * masks.size());
   L.masks = h->masks;
+  const std::vector<double> obs_q = build_obs_q(L);
+  ALLOC(h->obs_q, sizeof(double) * obs_q.size());
+  L.obs_q = h->obs_q;
   h->L = L;
   ALLOC(h->S.st4, sizeof(uint4) * n);
   ALLOC(h->S.ang, sizeof(double2) * n);
@@ -1544,6 +1547,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
       hipMemcpy(h->gotab, gotab.data(), sizeof(uint32_t) * gotab.size(), hipMemcpyHostToDevice) != hipSuccess ||
       (h->masks && hipMemcpy(h->masks, masks.data(), sizeof(uint32_t) * masks.size(),
                              hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemcpy(h->obs_q, obs_q.data(), sizeof(double) * obs_q.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
       hipMemset(h->wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE) != hipSuccess ||
       hipMemset(h->regen_ctr, 0, sizeof(int32_t) * 2 * 8 * CTR_STRIDE) != hipSuccess ||
@@ -1569,7 +1573,7 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   render_free(h->rs);
-  void* bufs[] = {h->grid,  h->genrand, h->gotab, h->masks, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
+  void* bufs[] = {h->grid,  h->genrand, h->gotab, h->masks, h->obs_q, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
                   h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
                   h->wst4,  h->wang,    h->wep,
                   h->wctr,  h->refill,  h->nrefill,   h->obs_scratch, h->regen_ctr, h->kst};

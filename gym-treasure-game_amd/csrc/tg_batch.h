@@ -62,6 +62,7 @@ struct tg_batch {
   // GoTable (tg_core.h go_lookup): W * H * 32 entries
   uint32_t* gotab = nullptr;
   uint32_t* masks = nullptr;  // the level bitmasks (tg_core.h Map::mk), or null
+  double* obs_q = nullptr;    // get_state's quotient table (tg_core.h Level::obs_q)
   int cus = 0;  // compute units
   tg::Soa S{};
   tg_episode* eps = nullptr;

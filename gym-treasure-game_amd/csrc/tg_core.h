@@ -83,7 +83,13 @@ struct Level {
   // the level bitmasks (Map::mk; mk_words(W, H) words, device global memory, staged into LDS
   // by the kernels that use them; null: the level is too large, cell probes)
   const uint32_t* masks;
+  // get_state's quotients (observe): obs_q[i] = (double)(Q_MIN + i) / (W * 48) for
+  // i < qx_n, then obs_q[qx_n + i] = (double)(Q_MIN + i) / (H * 48) for i < qy_n, each the IEEE
+  // quotient the division would give (built on the host, tg_level.h build_obs_q); null: divide
+  const double* obs_q;
+  int32_t qx_n, qy_n;
 };
+constexpr int Q_MIN = -2 * S;  // the smallest pixel coordinate the quotient table covers
 
 // ---- per-env state (registers) -------------------------------------------------------------
 struct Env {
@@ -953,17 +959,23 @@ TG_HD int policy(const Level& L, const Map& m, const Env& e, Opt& o) {
 // ==========================================================================================
 // Observation (IM/:368-378 + OB/:157-158,186-190,202-203,215-216) and done (TG/:95)
 // ==========================================================================================
+// v / d, from the level's quotient table when v is inside it (the table holds the same IEEE
+// quotients: an f64 division is ~11 VALU instructions on the device, the reciprocal among them)
+TG_HD double obs_div(const Level& L, int v, int base, int n, double d) {
+  const uint32_t i = (uint32_t)(v - Q_MIN);
+  return (L.obs_q && i < (uint32_t)n) ? L.obs_q[base + (int)i] : (double)v / d;
+}
 TG_HD void observe(const Level& L, const Env& e, double o[9]) {
   const double w = (double)(L.W * S), h = (double)(L.H * S);
-  o[0] = (double)e.px / w;
-  o[1] = (double)e.py / h;
+  o[0] = obs_div(L, e.px, 0, L.qx_n, w);
+  o[1] = obs_div(L, e.py, L.qx_n, L.qy_n, h);
   o[2] = e.ang0;
   o[3] = e.ang1;
-  o[4] = (double)(e.kx * S) / w;
-  o[5] = (double)(e.ky * S) / h;
+  o[4] = obs_div(L, e.kx * S, 0, L.qx_n, w);
+  o[5] = obs_div(L, e.ky * S, L.qx_n, L.qy_n, h);
   o[6] = ((e.f >> (F_OBJ + 5)) & 1u) ? 1.0 : 0.0;
-  o[7] = (double)(e.gx * S) / w;
-  o[8] = (double)(e.gy * S) / h;
+  o[7] = obs_div(L, e.gx * S, 0, L.qx_n, w);
+  o[8] = obs_div(L, e.gy * S, L.qx_n, L.qy_n, h);
 }
 TG_HD bool is_done(const Env& e) {
   int xc, yc;

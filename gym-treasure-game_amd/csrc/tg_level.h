@@ -243,6 +243,20 @@ inline std::vector<uint32_t> build_gotab(const Level& Lin, const std::vector<uin
   return tab;
 }
 
+// get_state's quotient table (tg_core.h Level::obs_q): pixel coordinates Q_MIN .. (W + 2) * 48
+// over W * 48 and Q_MIN .. (H + 2) * 48 over H * 48 (every player and object coordinate the
+// level can produce, with margin; outside it observe divides), each the IEEE double quotient
+// (the host's division: correctly rounded, as the device's).  Sets L.qx_n / L.qy_n.
+inline std::vector<double> build_obs_q(Level& L) {
+  L.qx_n = (L.W + 2) * S - Q_MIN + 1;
+  L.qy_n = (L.H + 2) * S - Q_MIN + 1;
+  std::vector<double> q((size_t)(L.qx_n + L.qy_n));
+  const double w = (double)(L.W * S), h = (double)(L.H * S);
+  for (int i = 0; i < L.qx_n; ++i) q[(size_t)i] = (double)(Q_MIN + i) / w;
+  for (int i = 0; i < L.qy_n; ++i) q[(size_t)(L.qx_n + i)] = (double)(Q_MIN + i) / h;
+  return q;
+}
+
 // The level bitmasks (tg_core.h Map::mk) of a parsed level's bordered grid, or empty when a
 // bordered side exceeds MK_DIM cells.
 inline std::vector<uint32_t> build_masks(const Level& L, const std::vector<uint8_t>& grid) {

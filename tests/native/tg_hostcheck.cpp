@@ -42,6 +42,7 @@ void hc_set_gotab(int on) { g_gotab = on; }
 static int g_masks = 1;
 void hc_set_masks(int on) { g_masks = on; }
 static std::vector<uint32_t> g_mk;  // the last loaded level's masks
+static std::vector<double> g_q;     // and quotient table
 
 static bool load_level(const char* dom, const char* objs, const char* inter, Level& L,
                        std::vector<uint8_t>& grid, std::vector<uint32_t>& tab) {
@@ -58,6 +59,8 @@ static bool load_level(const char* dom, const char* objs, const char* inter, Lev
   }
   g_mk = g_masks ? build_masks(L, grid) : std::vector<uint32_t>();
   L.masks = g_mk.empty() ? nullptr : g_mk.data();
+  g_q = build_obs_q(L);  // observe's quotient table, as on the device
+  L.obs_q = g_q.data();
   return true;
 }
 
