@@ -130,6 +130,10 @@ def parse(argv=None):
                     help="K > 0: tg_rollout, K steps per call with the policy evaluated inside "
                          "the step kernels (episodes drained / gathered every K steps); 0: the "
                          "per-step API (tg_policy_actions + tg_step per step)")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="with --rollout: step the batch as G groups on G streams (tg_set_groups)")
+    ap.add_argument("--stagger", action="store_true",
+                    help="with --groups: group g + 1 starts after group g's first k_classify")
     ap.add_argument("--actions-in-loop", action="store_true",
                     help="generate the uniform policy's actions inside the timed loop "
                          "(tg_policy_actions before every tg_step) instead of before it")
@@ -340,10 +344,13 @@ class Runner:
                 and args.steps * count * 4 <= PREGEN_BYTES):
             self.pre = torch.empty((max(args.steps, 1), count), dtype=torch.int32, device=dev)
         if self.K:
-            if args.workload == "c5" or args.steps % self.K or args.warmup % self.K:
-                raise SystemExit("--rollout K: c3 only, with --steps and --warmup multiples of K")
+            if args.workload == "c5":
+                raise SystemExit("--rollout K: c3 only")
             self.roll = [torch.empty((self.K, count), dtype=d, device=dev)
                          for d in (torch.int32, torch.uint8, torch.uint8)]
+            if args.groups > 1:
+                tg._lib.check(L.tg_set_groups(h, args.groups, 1 if args.stagger else 0),
+                              "tg_set_groups")
         self.frames, self.rev, self.timing, self.render_on = None, [], False, True
         if args.workload == "c5":  # ObservationWrapper.step: render every env after its step
             vec.render_init(tg.synthetic_sprites(seed=1))
@@ -369,15 +376,32 @@ class Runner:
             if int(cnt.sum().item()) == 0:
                 return
 
+    def roll_steps(self, t, k):
+        """steps t .. t+k-1 in one tg_rollout call (k <= K), then the episode drain"""
+        p = self.p
+        self.tg._lib.check(self.L.tg_rollout(self.h, k, ACTION_SEED, t, self.pol, self.flags,
+                                             None, None, p(self.roll[0]), p(self.roll[1]),
+                                             p(self.roll[2]), self.stream), "rollout")
+        self.drain()
+
+    def advance(self, t, nsteps):
+        """nsteps steps from t: rollout calls of K steps (the last one shorter), or per step"""
+        if self.K:
+            done = 0
+            while done < nsteps:
+                k = min(self.K, nsteps - done)
+                self.roll_steps(t + done, k)
+                done += k
+        else:
+            for j in range(nsteps):
+                self.step(t + j)
+        return t + nsteps
+
     def step(self, t):
         chk, L, p = self.tg._lib.check, self.L, self.p
         K = self.K
-        if K:  # steps t .. t+K-1 in one call
-            if t % K:
-                return
-            chk(L.tg_rollout(self.h, K, ACTION_SEED, t, self.pol, self.flags, None, None,
-                             p(self.roll[0]), p(self.roll[1]), p(self.roll[2]), self.stream),
-                "rollout")
+        if K:
+            raise AssertionError("rollout mode steps through advance()")
         elif self.timing and self.pre is not None:  # actions generated before timing
             a = self.pre[t - self.pre_t0]
             chk(L.tg_step(self.h, p(a), *self.args_step[2:]), "tg_step")
@@ -385,7 +409,7 @@ class Runner:
             chk(L.tg_policy_actions(self.h, ACTION_SEED, t, self.pol, p(self.vec._act),
                                     self.stream), "actions")
             chk(L.tg_step(*self.args_step), "tg_step")
-        if (t + 1) % self.G == 0 or K:
+        if (t + 1) % self.G == 0:
             self.drain()
         if self.frames is not None and self.render_on:
             if self.timing:  # k_render alone, on the stream it is launched on
@@ -400,7 +424,14 @@ class Runner:
         """warm-up + burn-in (untimed), then EXACTLY ``steps`` timed steps between barriers;
         returns the max-over-ranks wall time and this rank's stats."""
         t = 0
-        for j in range(warmup + burn_in):
+        if self.K:
+            t = self.advance(t, warmup)
+            for j in range(0, burn_in, 500):
+                t = self.advance(t, min(500, burn_in - j))
+                if self.args.progress:
+                    print("untimed step %d of %d" % (t, warmup + burn_in), file=sys.stderr,
+                          flush=True)
+        for j in range(warmup + burn_in if not self.K else 0):
             self.render_on = j < warmup  # c5: the burn-in only advances the envs
             self.step(t)
             t += 1
@@ -432,9 +463,12 @@ class Runner:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record()
-        for _ in range(steps):
-            self.step(t)
-            t += 1
+        if self.K:
+            t = self.advance(t, steps)
+        else:
+            for _ in range(steps):
+                self.step(t)
+                t += 1
         self.tg._lib.check(self.L.tg_regenerate(self.h, self.stream), "tg_regenerate")
         ev1.record()
         torch.cuda.synchronize(self.dev)
@@ -504,6 +538,8 @@ def step_line(args, runner, dt, st, node, world, total):
     run_s = st["run_ms"] / 1e3 / timed          # k_run's span (k_step's in the direct mode)
     cls_s = st["classify_ms"] / 1e3 / timed     # k_classify's span
     cls_b, run_b, regen_b = (b / launches for b in alg_bytes(st, args.mode))
+    if args.rollout and args.groups > 1:  # the spans are group 0's kernels: its share
+        cls_b, run_b, regen_b = cls_b / args.groups, run_b / args.groups, regen_b / args.groups
     rl = st.get("regen_launches", 0)
     rt = st.get("regen_timed", 0)
     regen_launch_s = st["regen_ms"] / 1e3 / rt if rt else 0.0
@@ -686,7 +722,11 @@ def main():
             "config": {"workload": workload,
                        "envs_per_gpu": args.envs, "total_envs": total, "policy": args.policy,
                        "autoreset": autoreset, "step_mode": args.mode,
-                       "api": ("tg_rollout x%d (policy inside the step kernels)" % args.rollout
+                       "api": ("tg_rollout x%d (policy inside the step kernels%s)"
+                               % (args.rollout, ", %d groups on %d streams%s" % (
+                                   args.groups, args.groups,
+                                   ", staggered" if args.stagger else "")
+                                  if args.groups > 1 else "")
                                if args.rollout else
                                "tg_step per step, the timed steps' actions generated in HBM "
                                "before timing (tg_policy_actions)" if run.pre is not None else

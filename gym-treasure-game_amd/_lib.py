@@ -29,7 +29,7 @@ NUM_ACTIONS = 9
 
 # every symbol include/tg_amd.h declares (tests check the library exports all of them)
 EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_step1", "tg_step1_py",
-           "tg_reset1_py", "tg_rollout",
+           "tg_reset1_py", "tg_rollout", "tg_set_groups",
            "tg_available_mask",
            "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing", "tg_regenerate",
            "tg_set_episode_capacity", "tg_predicate_table",
@@ -103,6 +103,7 @@ def load():
         "tg_predicate_table": (i32, [P, i32, i32, i32, i32, u32, P, P]),
         "tg_get_stats": (i32, [P, ctypes.POINTER(Stats)]),
         "tg_stats_reset": (i32, [P]),
+        "tg_set_groups": (i32, [P, i32, i32]),
         "tg_kernel_info": (i32, [P, i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                  ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
         "tg_read_state": (i32, [P, P, P, P, P, P, P, P]),

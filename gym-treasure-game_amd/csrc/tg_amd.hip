@@ -1453,6 +1453,40 @@ bool timing_begin(tg_batch* h, int& rc, unsigned long long*& ks0, unsigned long 
   ++h->kst_steps;
   return true;
 }
+
+
+// a stepper's buffers for envs [off, off + n) (StepCtx)
+int alloc_ctx(StepCtx& c, int64_t off, int64_t n) {
+  c.off = off;
+  c.n = n;
+#define ALLOC_C(ptr, bytes)                                             \
+  if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess)                \
+    return fail(TG_E_NOMEM, "hipMalloc %zu B for " #ptr, (size_t)(bytes));
+  ALLOC_C(c.stats, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n));
+  // a shard holds the envs of every SHARDS-th workgroup
+  c.shard_cap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK;
+  ALLOC_C(c.wl, sizeof(int32_t) * NSEG * (size_t)c.shard_cap);
+  ALLOC_C(c.wst4, sizeof(uint4) * NSEG * (size_t)c.shard_cap);
+  ALLOC_C(c.wang, sizeof(double2) * NSEG * (size_t)c.shard_cap);
+  ALLOC_C(c.wep, sizeof(int2) * NSEG * (size_t)c.shard_cap);
+  ALLOC_C(c.wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
+  ALLOC_C(c.refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63) * REGEN_STEPS);
+  ALLOC_C(c.nrefill, (size_t)((n + 63) >> 6) * REGEN_STEPS);
+  ALLOC_C(c.regen_ctr, sizeof(int32_t) * 2 * 8 * CTR_STRIDE);
+#undef ALLOC_C
+  HIP_TRY(hipMemset(c.stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)));
+  HIP_TRY(hipMemset(c.wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE));
+  HIP_TRY(hipMemset(c.regen_ctr, 0, sizeof(int32_t) * 2 * 8 * CTR_STRIDE));
+  return TG_OK;
+}
+void free_ctx(StepCtx& c) {
+  void* bufs[] = {c.stats, c.wl, c.wst4, c.wang, c.wep, c.wctr, c.refill, c.nrefill, c.regen_ctr};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c.ev) (void)hipEventDestroy(c.ev);
+  if (c.st) (void)hipStreamDestroy(c.st);
+  c = StepCtx{};
+}
 }  // namespace
 
 extern "C" {
@@ -1529,19 +1563,9 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->S.mc, sizeof(uint8_t) * MT_CODES * (size_t)n);
   ALLOC(h->eps, sizeof(tg_episode) * (size_t)h->eps_cap);
   ALLOC(h->eps_count, sizeof(int32_t));
-  ALLOC(h->stats, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n));
   ALLOC(h->err, sizeof(uint32_t));
-  // a shard holds the envs of every SHARDS-th workgroup
-  h->shard_cap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK;
-  ALLOC(h->wl, sizeof(int32_t) * NSEG * (size_t)h->shard_cap);
-  ALLOC(h->wst4, sizeof(uint4) * NSEG * (size_t)h->shard_cap);
-  ALLOC(h->wang, sizeof(double2) * NSEG * (size_t)h->shard_cap);
-  ALLOC(h->wep, sizeof(int2) * NSEG * (size_t)h->shard_cap);
-  ALLOC(h->wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
-  ALLOC(h->refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63) * REGEN_STEPS);
-  ALLOC(h->nrefill, (size_t)((n + 63) >> 6) * REGEN_STEPS);
-  ALLOC(h->regen_ctr, sizeof(int32_t) * 2 * 8 * CTR_STRIDE);
 #undef ALLOC
+  if (const int rc = alloc_ctx(h->main, 0, n)) return cleanup(rc);
   if (hipMemcpy(h->grid, grid.data(), grid.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->genrand, gen, sizeof gen, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->gotab, gotab.data(), sizeof(uint32_t) * gotab.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -1549,9 +1573,6 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
                              hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemcpy(h->obs_q, obs_q.data(), sizeof(double) * obs_q.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->eps_count, 0, sizeof(int32_t)) != hipSuccess ||
-      hipMemset(h->wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE) != hipSuccess ||
-      hipMemset(h->regen_ctr, 0, sizeof(int32_t) * 2 * 8 * CTR_STRIDE) != hipSuccess ||
-      hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)) != hipSuccess ||
       hipMemset(h->err, 0, sizeof(uint32_t)) != hipSuccess)
     return cleanup(fail(TG_E_HIP, "tg_create: upload failed"));
   // seed -> generation 1 (first half) -> generation 2 (second half) -> the constructor's draws
@@ -1573,12 +1594,13 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   render_free(h->rs);
-  void* bufs[] = {h->grid,  h->genrand, h->gotab, h->masks, h->obs_q, h->S.st4,     h->S.ang, h->S.ep, h->S.mt,
-                  h->S.mc,  h->eps,     h->eps_count, h->stats, h->err,  h->wl,
-                  h->wst4,  h->wang,    h->wep,
-                  h->wctr,  h->refill,  h->nrefill,   h->obs_scratch, h->regen_ctr, h->kst};
+  void* bufs[] = {h->grid, h->genrand, h->gotab, h->masks, h->obs_q, h->S.st4, h->S.ang, h->S.ep,
+                  h->S.mt, h->S.mc, h->eps, h->eps_count, h->err, h->obs_scratch, h->kst};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  free_ctx(h->main);
+  for (auto& c : h->grp) free_ctx(c);
+  if (h->fork) (void)hipEventDestroy(h->fork);
   if (h->one) (void)hipHostFree(h->one);
   if (h->py) (void)hipHostFree(h->py);
   if (h->pyc) (void)hipFree(h->pyc);
@@ -1597,10 +1619,15 @@ int tg_reset(tg_batch* h, const uint8_t* mask, double* obs, void* stream) {
 
 namespace {
 // k_regen over the pending refill-list slots (timed with its own event pair when timing is on)
-int launch_regen(tg_batch* h, hipStream_t st) {
-  if (!h->rpend) return TG_OK;
+// a stepper's envs as a Soa view (StepCtx: envs [off, off + n) of the handle)
+Soa soa_of(const tg_batch* h, const StepCtx& c) {
+  return Soa{h->S.st4 + c.off, h->S.ang + c.off, h->S.ep + c.off, h->S.mt + c.off * (int64_t)MT_WORDS,
+             h->S.mc + c.off * (int64_t)MT_CODES};
+}
+int launch_regen(tg_batch* h, StepCtx& c, hipStream_t st) {
+  if (!c.rpend) return TG_OK;
   unsigned long long* ks = nullptr;
-  if (h->timing_every) {
+  if (h->timing_every && &c == &h->main) {
     if (h->kst_regens >= KST_MAX) {
       const int rc = flush_timing(h);
       if (rc) return rc;
@@ -1619,31 +1646,43 @@ int launch_regen(tg_batch* h, hipStream_t st) {
                                                          BLOCK, 0));
     h->regen_per_cu = nb > 0 ? nb : 1;
   }
-  const int64_t regions = ((h->n + 63) >> 6) * h->rpend;
+  const int64_t regions = ((c.n + 63) >> 6) * c.rpend;
   int64_t grid = (int64_t)h->cus * h->regen_per_cu;
   if (grid > (regions + 3) / 4) grid = (regions + 3) / 4;  // 4 waves per workgroup
   if (grid < 8) grid = 8;
-  int32_t* const cur = h->regen_ctr + h->regen_parity * 8 * CTR_STRIDE;
-  int32_t* const nxt = h->regen_ctr + (h->regen_parity ^ 1) * 8 * CTR_STRIDE;
-  h->regen_parity ^= 1;
-  hipLaunchKernelGGL(k_regen, dim3((unsigned)grid), dim3(BLOCK), 0, st, h->S, h->refill, h->nrefill,
-                     h->n, h->rpend, cur, nxt, h->stats, stat_slots(h->n), ks);
+  int32_t* const cur = c.regen_ctr + c.regen_parity * 8 * CTR_STRIDE;
+  int32_t* const nxt = c.regen_ctr + (c.regen_parity ^ 1) * 8 * CTR_STRIDE;
+  c.regen_parity ^= 1;
+  hipLaunchKernelGGL(k_regen, dim3((unsigned)grid), dim3(BLOCK), 0, st, soa_of(h, c), c.refill,
+                     c.nrefill, c.n, c.rpend, cur, nxt, c.stats, stat_slots(c.n), ks);
   HIP_TRY(hipGetLastError());
-  h->rpend = 0;
+  c.rpend = 0;
   ++h->regen_launches;
   return TG_OK;
 }
-// one step's kernels on `st`, timed with HIP events when enabled
-int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
+// one step's kernels for a stepper's envs on `st` (io: the whole handle's arrays; the stepper's
+// rows start at c.off), their spans sampled when timing is on (the handle's own stepper only)
+int launch_step(tg_batch* h, StepCtx& c, const StepIO& io_in, bool ar, hipStream_t st,
+                uint32_t tstep, hipEvent_t mid = nullptr) {
   StepIO io = io_in;
-  io.tstep = h->tstep++;
+  io.tstep = tstep;
+  if (c.off) {
+    if (io.actions) io.actions += c.off;
+    io.obs += c.off * 9;
+    io.reward += c.off;
+    io.valid += c.off;
+    io.done += c.off;
+    if (io.final_obs) io.final_obs += c.off * 9;
+  }
   const bool fo = io.final_obs != nullptr;
-  int rc;
-  unsigned long long *ks0, *ks1;
-  timing_begin(h, rc, ks0, ks1);
+  int rc = TG_OK;
+  unsigned long long *ks0 = nullptr, *ks1 = nullptr;
+  if (&c == &h->main || &c == h->grp.data()) timing_begin(h, rc, ks0, ks1);
   if (rc) return rc;
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
-  const dim3 grid(grid_for(h->n)), block(BLOCK);
+  const dim3 grid(grid_for(c.n)), block(BLOCK);
+  const Soa S = soa_of(h, c);
+  const int64_t g0 = h->g0 + c.off;
   if (h->mode == TG_MODE_DIRECT) {
     decltype(&k_step<true, true>) kern;
     if (io.policy == TG_POLICY_UNIFORM)
@@ -1655,18 +1694,18 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
     else
       kern = ar ? (fo ? k_step<true, true> : k_step<true, false>)
                 : (fo ? k_step<false, true> : k_step<false, false>);
-    hipLaunchKernelGGL(kern, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, h->g0,
-                       h->stats, h->err, ks1);
+    hipLaunchKernelGGL(kern, grid, block, 0, st, S, c.n, h->L, h->grid, io, q, g0, c.stats, h->err,
+                       ks1);
   } else {
     // counters double-buffered by step parity: k_classify zeroes the next step's set (the
     // previous k_run, which read it, has finished), so no memset launch per step
-    int32_t* const cur = h->wctr + (h->parity ? NCTR * CTR_STRIDE : 0);
-    int32_t* const nxt = h->wctr + (h->parity ? 0 : NCTR * CTR_STRIDE);
-    h->parity ^= 1;
+    int32_t* const cur = c.wctr + (c.parity ? NCTR * CTR_STRIDE : 0);
+    int32_t* const nxt = c.wctr + (c.parity ? 0 : NCTR * CTR_STRIDE);
+    c.parity ^= 1;
     // this step's refill-list slot (k_regen drains the pending slots every REGEN_STEPS steps)
-    const int64_t nreg = (h->n + 63) >> 6;
-    const Work w{h->wl,  h->wst4, h->wang, h->wep, cur, nxt, h->refill + h->rpend * nreg * 64,
-                 h->nrefill + h->rpend * nreg, h->shard_cap};
+    const int64_t nreg = (c.n + 63) >> 6;
+    const Work w{c.wl,  c.wst4, c.wang, c.wep, cur, nxt, c.refill + c.rpend * nreg * 64,
+                 c.nrefill + c.rpend * nreg, c.shard_cap};
     decltype(&k_classify<true, true>) kc;
     if (io.policy == TG_POLICY_UNIFORM)
       kc = ar ? (fo ? k_classify<true, true, 0> : k_classify<true, false, 0>)
@@ -1679,17 +1718,25 @@ int launch_step(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st) {
               : (fo ? k_classify<false, true> : k_classify<false, false>);
     auto kr = ar ? (fo ? k_run<true, true> : k_run<true, false>)
                  : (fo ? k_run<false, true> : k_run<false, false>);
-    hipLaunchKernelGGL(kc, grid, block, 0, st, h->S, h->n, h->L, h->grid, io, q, w, h->g0,
-                       h->stats, h->err, ks0);
+    hipLaunchKernelGGL(kc, grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w, g0, c.stats, h->err,
+                       ks0);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(kr, dim3(run_grid_for(h->n)), block, 0, st, h->S, h->n, h->L, h->grid, io,
-                       q, w, h->g0, h->stats, h->err, ks1);
+    if (mid) HIP_TRY(hipEventRecord(mid, st));  // (tg_rollout's stagger between groups)
+    hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n)), block, 0, st, S, c.n, h->L, h->grid, io, q, w,
+                       g0, c.stats, h->err, ks1);
   }
   HIP_TRY(hipGetLastError());
-  if (h->mode != TG_MODE_DIRECT && ++h->rpend == REGEN_STEPS) return launch_regen(h, st);
+  if (h->mode != TG_MODE_DIRECT && ++c.rpend == REGEN_STEPS) return launch_regen(h, c, st);
   return TG_OK;
 }
-
+// every stepper's pending refill lists drained on `st` (the groups' lists name halves the
+// handle's own k_classify will not list again, and the reverse)
+int regen_all(tg_batch* h, hipStream_t st) {
+  int rc = launch_regen(h, h->main, st);
+  for (auto& c : h->grp)
+    if (!rc) rc = launch_regen(h, c, st);
+  return rc;
+}
 }  // namespace
 
 extern "C" {
@@ -1700,7 +1747,8 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
   if (!actions || !obs || !reward || !valid || !done)
     return fail(TG_E_INVAL, "tg_step: actions/obs/reward/valid/done are required");
   const StepIO io{const_cast<int32_t*>(actions), obs, reward, valid, done, final_obs, -1, 0, 0};
-  return launch_step(h, io, (flags & TG_STEP_AUTORESET) != 0, (hipStream_t)stream);
+  return launch_step(h, h->main, io, (flags & TG_STEP_AUTORESET) != 0, (hipStream_t)stream,
+                     h->tstep++);
 }
 
 int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t* valid,
@@ -1719,7 +1767,7 @@ int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t*
                   (uint64_t)(int64_t)action, 0, h->tstep++};
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   hipLaunchKernelGGL((k_step<false, false, POL_IMMEDIATE>), dim3(1), dim3(BLOCK), 0, st, h->S,
-                     h->n, h->L, h->grid, io, q, h->g0, h->stats, h->err, nullptr);
+                     h->n, h->L, h->grid, io, q, h->g0, h->main.stats, h->err, nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st));
   memcpy(obs, h->one->obs, sizeof h->one->obs);
@@ -1762,7 +1810,7 @@ int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) 
   h->py_warm = false;  // until the call has returned
   hipLaunchKernelGGL(k_py1<RESET>, dim3(1), dim3(64), 0, stream, h->S, h->L, h->grid, (int)action,
                      h->py_dev, warm ? h->pyc : nullptr, h->pyc, st->index, (int)st->has_gauss,
-                     st->gauss_next, h->one_dev, tstep, h->stats, h->err);
+                     st->gauss_next, h->one_dev, tstep, h->main.stats, h->err);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(stream));
   memcpy(st, h->py, sizeof(tg_pystate));
@@ -1808,13 +1856,86 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
     if (hipMalloc((void**)&h->obs_scratch, sizeof(double) * 9 * (size_t)n) != hipSuccess)
       return fail(TG_E_NOMEM, "tg_rollout: obs scratch");
   const bool ar = (flags & TG_STEP_AUTORESET) != 0;
-  for (int32_t s = 0; s < steps; ++s) {
-    const StepIO io{actions ? actions + (size_t)s * n : nullptr,
-                    obs ? obs + (size_t)s * n * 9 : h->obs_scratch,
-                    reward + (size_t)s * n, valid + (size_t)s * n, done + (size_t)s * n,
-                    nullptr, policy, action_seed, t0 + s};
-    const int rc = launch_step(h, io, ar, (hipStream_t)stream);
-    if (rc) return rc;
+  hipStream_t cs = (hipStream_t)stream;
+  const uint32_t tb = h->tstep;
+  h->tstep += (uint32_t)steps;
+  auto io_of = [&](int32_t s) {
+    return StepIO{actions ? actions + (size_t)s * n : nullptr,
+                  obs ? obs + (size_t)s * n * 9 : h->obs_scratch,
+                  reward + (size_t)s * n, valid + (size_t)s * n, done + (size_t)s * n,
+                  nullptr, policy, action_seed, t0 + s};
+  };
+  if (h->grp.empty() || h->mode == TG_MODE_DIRECT) {
+    for (int32_t s = 0; s < steps; ++s) {
+      const int rc = launch_step(h, h->main, io_of(s), ar, cs, tb + (uint32_t)s);
+      if (rc) return rc;
+    }
+    return TG_OK;
+  }
+  // Groups (tg_set_groups): each steps its envs on a stream of its own, so one group's
+  // latency-bound k_run tail overlaps the others' bandwidth-bound k_classify / k_regen.  The
+  // handle's own pending refill lists go first (the groups' k_classify would not list those
+  // halves again), each group drains its own at the end, then the caller's stream joins.
+  int rc = launch_regen(h, h->main, cs);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(h->fork, cs));
+  for (auto& c : h->grp) HIP_TRY(hipStreamWaitEvent(c.st, h->fork, 0));
+  for (int32_t s = 0; s < steps; ++s)
+    for (size_t g = 0; g < h->grp.size(); ++g) {
+      StepCtx& c = h->grp[g];
+      // stagger: group g + 1 starts after group g's first k_classify (half a step apart)
+      hipEvent_t mid = (s == 0 && h->stagger && g + 1 < h->grp.size()) ? h->grp[g + 1].ev : nullptr;
+      if ((rc = launch_step(h, c, io_of(s), ar, c.st, tb + (uint32_t)s, mid))) return rc;
+      if (mid) HIP_TRY(hipStreamWaitEvent(h->grp[g + 1].st, mid, 0));
+    }
+  for (auto& c : h->grp) {
+    if ((rc = launch_regen(h, c, c.st))) return rc;
+    HIP_TRY(hipEventRecord(c.ev, c.st));
+    HIP_TRY(hipStreamWaitEvent(cs, c.ev, 0));
+  }
+  return TG_OK;
+}
+
+int tg_set_groups(tg_batch* h, int32_t groups, int32_t stagger) {
+  BIND(h);
+  if (groups < 1 || groups > 16 || (int64_t)groups * 4096 > h->n)
+    return fail(TG_E_INVAL, "tg_set_groups: %d groups of %lld envs (1..16, >= 4096 envs each)",
+                groups, (long long)h->n);
+  HIP_TRY(hipDeviceSynchronize());
+  int rc = regen_all(h, 0);  // the old groups' pending lists
+  if (rc) return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  if (!h->grp.empty()) {  // the old groups' launch counters go on with the handle's own
+    std::vector<unsigned long long> slot0(ST_COUNT);
+    HIP_TRY(hipMemcpy(slot0.data(), h->main.stats, sizeof(unsigned long long) * ST_COUNT,
+                      hipMemcpyDeviceToHost));
+    for (auto& c : h->grp) {
+      std::vector<unsigned long long> part((size_t)stat_slots(c.n) * ST_COUNT);
+      HIP_TRY(hipMemcpy(part.data(), c.stats, sizeof(unsigned long long) * part.size(),
+                        hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < part.size(); ++i) slot0[i % ST_COUNT] += part[i];
+    }
+    HIP_TRY(hipMemcpy(h->main.stats, slot0.data(), sizeof(unsigned long long) * ST_COUNT,
+                      hipMemcpyHostToDevice));
+  }
+  for (auto& c : h->grp) free_ctx(c);
+  h->grp.clear();
+  h->stagger = stagger != 0;
+  if (groups == 1) return TG_OK;
+  if (!h->fork) HIP_TRY(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
+  // contiguous groups of whole 256-env workgroups
+  const int64_t per = ((h->n + groups - 1) / groups + BLOCK - 1) / BLOCK * BLOCK;
+  h->grp.resize((size_t)groups);
+  for (int g = 0; g < groups; ++g) {
+    const int64_t off = per * g, cnt = std::min(per, h->n - off);
+    StepCtx& c = h->grp[(size_t)g];
+    if (cnt <= 0 || (rc = alloc_ctx(c, off, cnt))) {
+      for (auto& x : h->grp) free_ctx(x);
+      h->grp.clear();
+      return rc ? rc : fail(TG_E_INVAL, "tg_set_groups: empty group");
+    }
+    HIP_TRY(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
   }
   return TG_OK;
 }
@@ -1881,7 +2002,7 @@ int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
 
 int tg_regenerate(tg_batch* h, void* stream) {
   BIND(h);
-  return launch_regen(h, (hipStream_t)stream);
+  return regen_all(h, (hipStream_t)stream);
 }
 
 int tg_set_timing(tg_batch* h, int every) {
@@ -1928,13 +2049,17 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
   HIP_TRY(hipDeviceSynchronize());
   int rc = flush_timing(h);
   if (rc) return rc;
-  const size_t nb = (size_t)stat_slots(h->n);
-  std::vector<unsigned long long> part(nb * ST_COUNT);
-  HIP_TRY(hipMemcpy(part.data(), h->stats, sizeof(unsigned long long) * part.size(),
-                    hipMemcpyDeviceToHost));
   unsigned long long s[ST_COUNT] = {};
-  for (size_t b = 0; b < nb; ++b)
-    for (int k = 0; k < ST_COUNT; ++k) s[k] += part[b * ST_COUNT + k];
+  std::vector<StepCtx*> ctxs{&h->main};
+  for (auto& c : h->grp) ctxs.push_back(&c);
+  for (StepCtx* c : ctxs) {
+    const size_t nb = (size_t)stat_slots(c->n);
+    std::vector<unsigned long long> part(nb * ST_COUNT);
+    HIP_TRY(hipMemcpy(part.data(), c->stats, sizeof(unsigned long long) * part.size(),
+                      hipMemcpyDeviceToHost));
+    for (size_t b = 0; b < nb; ++b)
+      for (int k = 0; k < ST_COUNT; ++k) s[k] += part[b * ST_COUNT + k];
+  }
   out->steps = (int64_t)s[ST_STEPS];
   out->valid_steps = (int64_t)s[ST_VALID];
   out->ticks = (int64_t)s[ST_TICKS];
@@ -1957,7 +2082,9 @@ int tg_get_stats(tg_batch* h, tg_stats* out) {
 int tg_stats_reset(tg_batch* h) {
   BIND(h);
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemset(h->stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(h->n)));
+  HIP_TRY(hipMemset(h->main.stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(h->n)));
+  for (auto& c : h->grp)
+    HIP_TRY(hipMemset(c.stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(c.n)));
   if (h->kst) {
     const int rc = kst_reset(h);  // drops the unflushed records
     if (rc) return rc;
@@ -2087,7 +2214,8 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
   }
   HIP_TRY(hipDeviceSynchronize());
   // validated: the pending refill lists name the old states' halves, and every ring is rebuilt
-  h->rpend = 0;
+  h->main.rpend = 0;
+  for (auto& c : h->grp) c.rpend = 0;
   HIP_TRY(hipMemcpy(h->S.st4, st.data(), sizeof(uint4) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->S.ang, ang, sizeof(double2) * n, hipMemcpyHostToDevice));
   {  // (return, length) -> (return, start step)

@@ -48,6 +48,29 @@ struct TgOne {
 struct RenderState;  // tg_render.hip
 void render_free(RenderState* rs);
 
+// One stepper over envs [off, off + n) of the handle: its worklists, counters, refill lists and
+// launch counters.  The handle's own covers every env (tg_step, tg_rollout); with tg_set_groups
+// each group has one, and tg_rollout steps the groups on streams of their own (tg_amd.hip).
+struct StepCtx {
+  int64_t off = 0, n = 0;
+  unsigned long long* stats = nullptr;  // [stat_slots(n)][ST_COUNT] launch counters
+  int32_t* wl = nullptr;   // per-(option, shard) worklists (compact mode)
+  uint4* wst4 = nullptr;   // the listed envs' state in worklist order (k_classify -> k_run)
+  double2* wang = nullptr;
+  int2* wep = nullptr;
+  int32_t* wctr = nullptr; // sharded counters, two sets (step parity)
+  uint32_t* refill = nullptr;  // stale MT halves listed by k_classify: REGEN_STEPS slots (k_regen)
+  uint8_t* nrefill = nullptr;
+  int64_t shard_cap = 0;
+  int parity = 0;  // which half of wctr this compact step counts in
+  int rpend = 0;   // compact steps whose refill lists k_regen has not drained
+  int32_t* regen_ctr = nullptr;  // k_regen's per-XCD region counters, two sets (k_regen zeroes
+                                 // the other set for the next launch)
+  int regen_parity = 0;          // which set the next k_regen counts in
+  hipStream_t st = nullptr;      // a group's stream (groups only)
+  hipEvent_t ev = nullptr;       //   and its join event
+};
+
 }  // namespace tg
 
 // the handle (tg_amd.h tg_batch)
@@ -68,19 +91,13 @@ struct tg_batch {
   tg_episode* eps = nullptr;
   int32_t* eps_count = nullptr;
   int32_t eps_cap = 0;
-  unsigned long long* stats = nullptr;  // ST_COUNT
   uint32_t* err = nullptr;
   int mode = TG_MODE_COMPACT;
-  int32_t* wl = nullptr;   // per-(option, shard) worklists (compact mode)
-  uint4* wst4 = nullptr;   // the listed envs' state in worklist order (k_classify -> k_run)
-  double2* wang = nullptr;
-  int2* wep = nullptr;
-  int32_t* wctr = nullptr; // sharded counters
-  uint32_t* refill = nullptr;  // stale MT halves listed by k_classify: REGEN_STEPS slots (k_regen)
-  uint8_t* nrefill = nullptr;
-  int parity = 0;  // which half of wctr this compact step counts in
+  tg::StepCtx main;                // the stepper over every env
+  std::vector<tg::StepCtx> grp;    // tg_set_groups: the groups' steppers (tg_rollout)
+  hipEvent_t fork = nullptr;       //   the groups' fork event
+  bool stagger = false;            //   group g + 1 starts after group g's first k_classify
   uint32_t tstep = 0;  // steps taken by the handle (mod 2^32): S.ep holds each episode's start step
-  int64_t shard_cap = 0;
   int timing_every = 0;        // HIP-event timing of every k-th step launch (0: off)
   uint64_t timing_calls = 0;   // step launches since timing was enabled
   unsigned long long* kst = nullptr;  // in-kernel span records of the timed launches (tg_amd.hip)
@@ -89,12 +106,8 @@ struct tg_batch {
   double classify_ms_done = 0.0;  //   of which k_classify
   double run_ms_done = 0.0;     //   and k_run (or k_step)
   int64_t timed_launches = 0;
-  int rpend = 0;                    // compact steps whose refill lists k_regen has not drained
   int regen_per_cu = 0;             // k_regen workgroups resident per CU (occupancy API, first use)
-  int32_t* regen_ctr = nullptr;     // k_regen's per-XCD region counters, two sets (k_regen
-                                    // zeroes the other set for the next launch)
   double regen_ms_done = 0.0;       // the timed k_regen launches' spans (in-kernel stamps)
-  int regen_parity = 0;             // which set of regen_ctr the next k_regen counts in
   int64_t regen_launches = 0;       // k_regen launches (timed or not)
   int64_t regen_timed = 0;
   std::string domain;              // domain.txt text (the renderer's cell sprites)

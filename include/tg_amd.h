@@ -167,6 +167,14 @@ int tg_rollout(tg_batch *h, int32_t steps, uint64_t action_seed, int64_t t0, int
                uint32_t flags, int32_t *actions, double *obs, int32_t *reward, uint8_t *valid,
                uint8_t *done, void *stream);
 
+/* Step the batch as `groups` contiguous groups (1..16, each >= 4096 envs; 1 = off, the default)
+ * in tg_rollout: each group's steps go on a stream of its own, forked from and joined back to
+ * the caller's, so one group's latency-bound option loops overlap another's bandwidth-bound
+ * passes.  Results are identical (the envs share nothing); counters and timing are unchanged
+ * in meaning (timing samples group 0's kernels).  stagger != 0: group g + 1 starts after group
+ * g's first k_classify.  Synchronises.  (No reference counterpart: batching is new.) */
+int tg_set_groups(tg_batch *h, int32_t groups, int32_t stagger);
+
 /* available_mask for every env: u16 [N], bit k == option k can run. */
 int tg_available_mask(tg_batch *h, uint16_t *mask, void *stream);
 
