@@ -236,6 +236,13 @@ class TreasureGameVec:
                                  self._stream()), "tg_rollout")
         return out
 
+    def set_groups(self, groups=1, stagger=False):
+        """rollout() steps the batch as ``groups`` contiguous groups, each on a stream of its
+        own (tg_set_groups: overlaps one group's option loops with another's bandwidth-bound
+        passes; results identical).  1: off."""
+        check(self._L.tg_set_groups(self.handle, int(groups), 1 if stagger else 0),
+              "tg_set_groups")
+
     def available_mask(self):
         """available_mask (TG/:83-89) as bits: int16 [N], bit k == option k can run."""
         check(self._L.tg_available_mask(self.handle, _ptr(self._mask), self._stream()),

@@ -21,7 +21,8 @@ def episodes_sorted(vec):
     return e[np.lexsort((e[:, 2], e[:, 1], e[:, 0]))] if len(e) else e
 
 
-def run_pair(tg, n, k, policy, pre_steps=0, level=None, seed=5, a0=0xA5A5, chunks=(None,)):
+def run_pair(tg, n, k, policy, pre_steps=0, level=None, seed=5, a0=0xA5A5, chunks=(None,),
+             groups=1, stagger=False, post_steps=0):
     """the same batch through K x (tg_policy_actions + tg_step) and through tg_rollout (in
     `chunks` calls); returns both sides' outputs, final states and sorted episodes"""
     ld = None if level is None else os.path.join(LEVELS, level)
@@ -40,6 +41,8 @@ def run_pair(tg, n, k, policy, pre_steps=0, level=None, seed=5, a0=0xA5A5, chunk
                              "done": d.clone(), "actions": act})
             out = {key: torch.stack([x[key] for x in outs]) for key in outs[0]}
         else:
+            if groups > 1:
+                v.set_groups(groups, stagger)
             t0, parts = pre_steps, []
             sizes = [k] if chunks == (None,) else list(chunks)
             assert sum(sizes) == k
@@ -47,6 +50,9 @@ def run_pair(tg, n, k, policy, pre_steps=0, level=None, seed=5, a0=0xA5A5, chunk
                 parts.append(v.rollout(c, t0=t0, action_seed=a0, policy=policy))
                 t0 += c
             out = {key: torch.cat([p[key] for p in parts]) for key in parts[0]}
+        # the per-step API afterwards (the grouped steppers' lists were drained)
+        for t in range(pre_steps + k, pre_steps + k + post_steps):
+            v.step(v.policy_actions(t, a0, policy))
         torch.cuda.synchronize()
         sides.append((out, v.read_state(mt=True), episodes_sorted(v), v.stats(), v.errors()))
         v.close()
@@ -123,3 +129,26 @@ def test_rollout_1m_envs(tg, policy):
     """the bench's size: 1M envs"""
     n, k = 1 << 20, 24
     check_pair(run_pair(tg, n, k, policy), n, k)
+
+
+@pytest.mark.parametrize("n,groups,stagger,policy", [(20000, 3, True, "masked"),
+                                                     (70001, 2, False, "uniform"),
+                                                     (1 << 20, 2, True, "uniform"),
+                                                     (1 << 20, 4, True, "masked")])
+def test_grouped_rollout(tg, n, groups, stagger, policy):
+    """tg_set_groups: the batch stepped as contiguous groups on their own streams (forked from and
+    joined to the caller's) equals the per-step API: every output row, states, MT streams,
+    episodes and counters; rollouts over several calls, envs entering with stale MT halves,
+    and per-step calls after the grouped rollouts"""
+    k = 30
+    check_pair(run_pair(tg, n, k, policy, pre_steps=5, chunks=(10, 3, 17), groups=groups,
+                        stagger=stagger, post_steps=6), n, k)
+
+
+@pytest.mark.parametrize("level", ["corridor", "cascade"])
+def test_grouped_rollout_levels(tg, level):
+    """groups on levels whose go options cross MT generations inside one step (corridor) and
+    whose INTERACT ticks draw 10 times (cascade)"""
+    n, k = 12288, 25
+    check_pair(run_pair(tg, n, k, "uniform", level=level, groups=3, stagger=True), n, k,
+               errors=(1 << 24) if level == "corridor" else 0)
