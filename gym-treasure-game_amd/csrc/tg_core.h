@@ -378,44 +378,54 @@ TG_HD void init_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed,
 // compares against the column / row starts instead of a clamped pixel -> cell division and an
 // LDS read; past the border the compares select the clamped cell, as colx / rowy do.
 struct AirCells {
-  uint32_t open, block;  // is_open; is_wall | is_door (can_go_side's blockers)
-  int bx, by1, by2;      // first pixel of column c0 + 1, of rows r0 + 1 and r0 + 2
-  uint32_t dc;           // the door state the masks were built for
+  // per window column (A: c0, B: c0 + 1) the rows r0 .. r0 + 2 (bits 0..2) that are OPEN /
+  // hold a WALL or a closed door (can_go_side's blockers)
+  uint32_t oA, oB, bA, bB;
+  int bx, by1;   // first pixel of column c0 + 1 and of row r0 + 1
+  uint32_t dc;   // the door state the masks were built for
   // still the window of (dc, px, py): colx(px - 16) == c0 and rowy(py - 4) == r0 (at a clamped
-  // border this is false, and the caller rebuilds every tick)
+  // border this is false even right after a rebuild: the caller then takes the full tick)
   TG_HD bool holds(uint32_t d, int px, int py) const {
     return (d == dc) & (px - (HALFW + INCR) < bx) & (px - (HALFW + INCR) >= bx - S) &
            (py - INCR < by1) & (py - INCR >= by1 - S);
   }
-  TG_HD uint32_t ci(int x) const { return (uint32_t)(x >= bx); }
-  TG_HD uint32_t ri2(int y) const { return (uint32_t)((y >= by1) + (y >= by2)) * 2u; }
-  // bit 2*ri: the cells of xa and of xb in row ri are both open
-  TG_HD uint32_t rows_open(int xa, int xb) const { return (open >> ci(xa)) & (open >> ci(xb)) & 0x15u; }
-  TG_HD bool can_fall(int px, int py) const {  // can_fall_at
-    const uint32_t r = rows_open(px - HALFW + 2, px + HALFW - 2);
-    return ((r >> ri2(py)) & (r >> ri2(py + S + 2)) & 1u) != 0;
+};
+
+// The air tick's predicates inside its window.  With s = bx - px and t = by1 - py the window
+// holds iff s in (-16, 32] and t in [-3, 44], so a probe at px + o lies in column B iff o >= s,
+// and one at py + o in row (o >= t) + (o >= t + 48): row 0 for o = -4, row 1 for o = 44, row 1 +
+// (t <= 2) for o = 50; each predicate is a few compares and selects of 3-bit row masks
+// (AirCells: every probe of the tick, the moved player's fall included, lies in the window).
+struct AirProbe {
+  const AirCells& ac;
+  int s, t;
+  TG_HD AirProbe(const AirCells& a, int px, int py) : ac(a), s(a.bx - px), t(a.by1 - py) {}
+  static TG_HD uint32_t bit(uint32_t m, uint32_t r) { return (m >> r) & 1u; }
+  TG_HD uint32_t open_col(int o) const { return o >= s ? ac.oB : ac.oA; }
+  TG_HD uint32_t block_col(int o) const { return o >= s ? ac.bB : ac.bA; }
+  TG_HD bool can_fall() const {  // can_fall_at: px -+ 10 at py and py + 50
+    const uint32_t c = open_col(-(HALFW - 2)) & open_col(HALFW - 2);
+    return (bit(c, (uint32_t)(t <= 0)) & bit(c, 1u + (uint32_t)(t <= 2))) != 0;
   }
-  // the distance of a downward move of yd <= 4 px from (px, py) (IM/:341-348, Map::fall): the
-  // probes at py + k and py + 50 + k (k < 4) cross at most one row boundary each, at k = ka / kb
-  TG_HD int fall(int px, int py, int yd) const {
-    const uint32_t r = rows_open(px - HALFW + 2, px + HALFW - 2);
-    const int ya = py, yb = py + S + 2;
-    const uint32_t ra = ri2(ya), rb = ri2(yb);
-    if (!((r >> ra) & (r >> rb) & 1u)) return yd;
-    const int ka = ya < by1 ? by1 - ya : ya < by2 ? by2 - ya : 4;  // (no boundary in reach: 4)
-    const int kb = yb < by1 ? by1 - yb : yb < by2 ? by2 - yb : 4;
+  TG_HD bool side(int dir) const {  // can_go_side: px + 16 dir at py + 4 and py + 44
+    const uint32_t c = block_col(dir * (HALFW + INCR));
+    return (bit(c, (uint32_t)(t <= INCR)) | bit(c, 1u)) == 0;
+  }
+  TG_HD bool up_clear() const {  // px -+ 4 at py - 4 and py - 1
+    const uint32_t c = open_col(-INCR) & open_col(INCR);
+    return (bit(c, 0u) & bit(c, (uint32_t)(t <= -1))) != 0;
+  }
+  // the distance of a downward move of yd <= 4 px (IM/:341-348, Map::fall) after the player's
+  // x moved to px2 (by <= 4: still in the window): the probes at py + k and py + 50 + k (k < 4)
+  // enter their next row at k = t (if t > 0) / t - 2 (if t > 2); the others at >= 43
+  TG_HD int fall(int px2, int yd) const {
+    const int s2 = ac.bx - px2;
+    const uint32_t c = (-(HALFW - 2) >= s2 ? ac.oB : ac.oA) & ((HALFW - 2) >= s2 ? ac.oB : ac.oA);
+    if (!(bit(c, (uint32_t)(t <= 0)) & bit(c, 1u + (uint32_t)(t <= 2)))) return yd;
     int d = yd;
-    if (!((r >> (ra + 2u)) & 1u)) d = min(d, ka);
-    if (!((r >> (rb + 2u)) & 1u)) d = min(d, kb);
+    if (!bit(c, (uint32_t)(t <= 3))) d = min(d, t > 0 ? t : t + S);
+    if (!bit(c, 1u + (uint32_t)(t <= 5))) d = min(d, t > 2 ? t - 2 : t + S - 2);
     return d;
-  }
-  TG_HD bool side(int px, int py, int dir) const {  // can_go_side
-    const uint32_t c = ci(px + dir * (HALFW + INCR));
-    return (((block >> (ri2(py + INCR) + c)) | (block >> (ri2(py + S - INCR) + c))) & 1u) == 0;
-  }
-  TG_HD bool up_clear(int px, int py) const {  // Map::up_clear
-    const uint32_t r = rows_open(px - INCR, px + INCR);
-    return ((r >> ri2(py - INCR)) & (r >> ri2(py - 1)) & 1u) != 0;
   }
 };
 
@@ -516,17 +526,18 @@ struct Map {
   TG_HD AirCells air_cells(uint32_t dc, int px, int py) const {
     const int c0 = colx(px - (HALFW + INCR)), r0 = rowy(py - INCR);
     const uint32_t x0 = (uint32_t)(c0 + PAD), x1 = (uint32_t)(c0 + 1 < W + PAD ? c0 + 1 + PAD : c0 + PAD);
-    uint32_t op = 0, bl = 0;
+    uint32_t oa = 0, ob = 0, ba = 0, bb = 0;
 #pragma unroll
     for (int ri = 0; ri < 3; ++ri) {
       const int r = r0 + ri < H + PAD ? r0 + ri : H + PAD - 1;
       const uint8_t* const row = g + mul24((uint32_t)(r + PAD), (uint32_t)pw());
       const uint32_t ca = row[x0], cb = row[x1];
-      op |= ((uint32_t)is_open(ca, dc) | (uint32_t)is_open(cb, dc) << 1) << (2 * ri);
-      bl |= ((uint32_t)(is_wall(ca) | is_door(ca, dc)) | (uint32_t)(is_wall(cb) | is_door(cb, dc)) << 1)
-            << (2 * ri);
+      oa |= (uint32_t)is_open(ca, dc) << ri;
+      ob |= (uint32_t)is_open(cb, dc) << ri;
+      ba |= (uint32_t)(is_wall(ca) | is_door(ca, dc)) << ri;
+      bb |= (uint32_t)(is_wall(cb) | is_door(cb, dc)) << ri;
     }
-    return AirCells{op, bl, (c0 + 1) * S, (r0 + 1) * S, (r0 + 2) * S, dc};
+    return AirCells{oa, ob, ba, bb, (c0 + 1) * S, (r0 + 1) * S, dc};
   }
   // integrate y on a downward move of yd <= 4 px (IM/:341-348): with can_fall at py the player
   // falls pixel by pixel while can_fall holds, so the distance is the first k in 1..yd-1 with
@@ -1257,14 +1268,21 @@ TG_HD int ladder_plain_limit(const Map& m, const Env& e, const P& pr) {
 // ac: the option loop's AirCells, rebuilt only when the player leaves its window (a jump
 // changes cell column or row every ~12 ticks)
 template <int K, class R>
-TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng, AirCells& ac) {
+TG_HD int air_tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, Opt& o, R& rng,
+                   AirCells& ac) {
   constexpr int DIR = (K == O_JUMP_LEFT || K == O_DOWN_LEFT) ? -1 : 1;
   constexpr bool JUMP = K == O_JUMP_LEFT || K == O_JUMP_RIGHT;
-  if (!ac.holds(Map::dc_of(e.f), e.px, e.py)) ac = m.air_cells(Map::dc_of(e.f), e.px, e.py);
-  const bool cf0 = ac.can_fall(e.px, e.py);
-  const bool fwd = ac.side(e.px, e.py, DIR);
-  const bool bwd = JUMP ? ac.side(e.px, e.py, -DIR) : false;
-  const bool uc = ac.up_clear(e.px, e.py);
+  const uint32_t dc = Map::dc_of(e.f);
+  if (!ac.holds(dc, e.px, e.py)) {
+    ac = m.air_cells(dc, e.px, e.py);
+    if (!ac.holds(dc, e.px, e.py)) {  // a clamped window (a player past the border): full tick
+      const int prim = policy<K>(L, m, e, o);
+      return tick<prims_of(K), R>(L, trig, m, e, prim, rng);
+    }
+  }
+  const AirProbe ap(ac, e.px, e.py);
+  const bool cf0 = ap.can_fall();
+  const bool fwd = ap.side(DIR);
   int mv = 0;  // the primitive: -1 LEFT, +1 RIGHT, 0 NOP
   if (close_x(e, o.tx)) {
     if (!cf0) o.done = true;
@@ -1272,19 +1290,21 @@ TG_HD int air_tick(const Level& L, const Map& m, Env& e, Opt& o, R& rng, AirCell
     mv = (JUMP && !cf0 && !fwd) ? -DIR : DIR;  // MO/:311-314: back off when blocked on the floor
   }
   int xd = 0, yd = 0;
-  if (mv != 0 && (mv == DIR ? fwd : bwd)) {  // can_go_left / can_go_right (IM/:303-311)
+  // can_go_left / can_go_right (IM/:303-311): forward is fwd; backward only after !fwd, when
+  // it is the other side's blockers
+  if (mv != 0 && (mv == DIR ? fwd : ap.side(-DIR))) {
     xd = code_step(rng.code(), mv < 0);
     e.f = mv > 0 ? (e.f | F_FACING) : (e.f & ~F_FACING);
   }
   const uint32_t jt = e.f & F_JT;  // IM/:331-337, at the pre-move x
   if (jt > 0) {
-    if (uc) yd = -INCR;
+    if (ap.up_clear()) yd = -INCR;
     e.f = (e.f & ~F_JT) | (jt - 1);
   } else if (cf0) {
     yd = INCR;
   }
   e.px += xd;
-  if (yd > 0) yd = ac.fall(e.px, e.py, yd);  // (e.px moved by <= 4: still inside the AirCells)
+  if (yd > 0) yd = ap.fall(e.px, yd);  // IM/:341-348
   e.py += yd;
   pickups(L, e);
   return -1;  // STEP_REWARD (no JUMP after the first tick)
@@ -1422,14 +1442,14 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
     return;
   }
   if constexpr (K == O_JUMP_LEFT || K == O_JUMP_RIGHT || K == O_DOWN_LEFT || K == O_DOWN_RIGHT) {
-    AirCells ac{0u, 0u, -0x40000000, 0, 0, 0u};  // holds nothing: built on the first air tick
+    AirCells ac{0u, 0u, 0u, 0u, -0x40000000, 0, 0u};  // holds nothing: built on the first air tick
     do {
       rng.phase(0);
       rng.phase(1);
       rng.reserve(TICK_DRAWS);
       rng.phase(2);
       if (o.init) {
-        r.reward += air_tick<K>(L, m, e, o, rng, ac);
+        r.reward += air_tick<K>(L, trig, m, e, o, rng, ac);
       } else {  // the first tick (the jump itself; the drop's target)
         const int prim = policy<K>(L, m, e, o);
         r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
