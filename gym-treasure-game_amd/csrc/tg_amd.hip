@@ -947,7 +947,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     oraw[O_COUNT] = pre[NSEG];
   }
   __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
-  LEVEL_IN_LDS_MK();  // includes the barrier
+  __syncthreads();  // ostart / oraw
   const int total = ostart[O_COUNT];
   const int base = (blockIdx.x * BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
   int oj = 0;  // ostart[oj] <= base < ostart[oj + 1] (wave-uniform)
@@ -966,7 +966,19 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     }
   }
   const int idx = qraw - pre[seg];
+  // the chunk's rows, loaded before the level staging so that their latency overlaps it
   int64_t i = 0;
+  uint4 s4w = make_uint4(0u, 0u, 0u, 0u);
+  double2 a2w = make_double2(0.0, 0.0);
+  int2 epw = make_int2(0, 0);
+  if (live) {
+    const int64_t at = (int64_t)seg * w.shard_cap + idx;
+    i = w.lists[at];
+    s4w = w.wst4[at];
+    a2w = w.wang[at];
+    epw = w.wep[at];
+  }
+  LEVEL_IN_LDS_MK();  // includes the barrier
   StepResult r{0, 0, 0, 0};
   Env e;
   e.mti = 0u;
@@ -986,10 +998,8 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   uint32_t prounds = 0;
 #endif
   if (live) {
-    const int64_t at = (int64_t)seg * w.shard_cap + idx;
-    i = w.lists[at];
-    unpack(w.wst4[at], w.wang[at], e);
-    ep = w.wep[at];
+    unpack(s4w, a2w, e);
+    ep = epw;
     RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
     rng.prime();  // issue the code loads now; the first draw comes after the policy setup
     TG_STAMP(t1);
