@@ -34,6 +34,13 @@ using namespace tg;
 namespace {
 
 constexpr int BLOCK = 256;
+// k_run's workgroup: a workgroup holds its CU slot (LDS, wave slots) until its slowest wave
+// ends, and k_run's waves differ in length by up to ~3x
+#ifndef TG_RUN_BLOCK
+#define TG_RUN_BLOCK 256
+#endif
+constexpr int RUN_BLOCK = TG_RUN_BLOCK;
+static_assert(RUN_BLOCK % 64 == 0 && BLOCK % RUN_BLOCK == 0, "whole waves, whole k_classify blocks");
 // issue priority of the option waves whose ticks are slow (ladders, drops, jumps), which share
 // SIMDs with the go waves (0.153 vs 0.156 ms per step)
 constexpr int PRIO_SLOW = 3;
@@ -73,13 +80,14 @@ struct LdsLevel {
   uint32_t trig[12];
   uint32_t grid[MAX_CELLS / 4];
 };
+template <int NT = BLOCK>  // NT: the workgroup's threads
 __device__ __forceinline__ void stage_level(LdsLevel& lv, const uint32_t* __restrict__ grid,
                                             const Level& L, uint32_t* masks = nullptr) {
   const int nwords = ((L.W + 2 * PAD) * (L.H + 2 * PAD) + 3) / 4;
-  for (int i = threadIdx.x; i < nwords; i += BLOCK) lv.grid[i] = grid[i];
+  for (int i = threadIdx.x; i < nwords; i += NT) lv.grid[i] = grid[i];
   if (threadIdx.x < 12) lv.trig[threadIdx.x] = L.trig[threadIdx.x >> 1][threadIdx.x & 1];
   if (masks && L.masks)
-    for (int i = threadIdx.x; i < mk_words(L.W, L.H); i += BLOCK) masks[i] = L.masks[i];
+    for (int i = threadIdx.x; i < mk_words(L.W, L.H); i += NT) masks[i] = L.masks[i];
   __syncthreads();
 }
 #define LEVEL_IN_LDS()                   \
@@ -91,7 +99,7 @@ __device__ __forceinline__ void stage_level(LdsLevel& lv, const uint32_t* __rest
 #define LEVEL_IN_LDS_MK()                                                      \
   __shared__ LdsLevel lv;                                                      \
   __shared__ uint32_t lmk[MK_MAX_WORDS];                                       \
-  stage_level(lv, grid, L, lmk);                                               \
+  stage_level<RUN_BLOCK>(lv, grid, L, lmk);                                    \
   const uint32_t* const trig = lv.trig;                                        \
   const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H, L.masks ? lmk : nullptr}
 
@@ -572,12 +580,13 @@ __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, 
 // wave_ticks: the wave's longest lane's ticks (the tick loop's trip count, lane efficiency).
 __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ part, int steps,
                                            int valid, int ticks, int draws, int episodes,
-                                           int regens = 0, bool wave_ticks = false) {
+                                           int regens = 0, bool wave_ticks = false,
+                                           int64_t sl = -1) {  // slot: blockIdx.x by default
   const int v[5] = {wave_sum(steps), wave_sum(valid), wave_sum(ticks), wave_sum(draws),
                     wave_sum(episodes)};
   const int wt = wave_ticks ? wave_max(ticks) : 0;
   if ((threadIdx.x & 63) == 0) {
-    unsigned long long* const slot = part + (size_t)blockIdx.x * ST_COUNT;
+    unsigned long long* const slot = part + (size_t)(sl < 0 ? (int64_t)blockIdx.x : sl) * ST_COUNT;
 #pragma unroll
     for (int c = 0; c < 5; ++c)
       if (v[c]) atomicAdd(&slot[c], (unsigned long long)v[c]);
@@ -721,7 +730,7 @@ constexpr RunPos make_runpos() {
 }
 constexpr RunPos kRunPos = make_runpos();
 constexpr int NSEG = O_COUNT * SHARDS;  // segment = run position * SHARDS + shard
-static_assert(NSEG <= 2 * BLOCK, "k_run's prefix: two segments per thread");
+static_assert(NSEG <= 2 * RUN_BLOCK, "k_run's prefix: two segments per thread");
 constexpr int NCTR = NSEG;      // the worklist counters
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
 struct Work {
@@ -903,7 +912,7 @@ __device__ unsigned long long g_stamps[NSTAMP_WAVES * NSTAMP];
 #endif
 
 template <bool AUTORESET, bool FINAL>
-__global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
+__global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
                                                 const uint32_t* __restrict__ grid, StepIO io,
                                                 EpQueue q, Work w, int64_t g0,
                                                 unsigned long long* __restrict__ stats,
@@ -914,7 +923,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   // counters, two segments per thread), then per option (run order j) its first segment's
   // prefix and its start in the chunk space, where each option is padded to whole chunks
   __shared__ int pre[NSEG + 1];
-  __shared__ int wtot[BLOCK / 64];
+  __shared__ int wtot[RUN_BLOCK / 64];
   __shared__ int ostart[O_COUNT + 1], oraw[O_COUNT + 1];
   {
     const int s0 = 2 * (int)threadIdx.x, ln = threadIdx.x & 63;
@@ -932,7 +941,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     const int excl = v - c0 - c1;
     if (s0 < NSEG) pre[s0] = excl;
     if (s0 + 1 < NSEG) pre[s0 + 1] = excl + c0;
-    if (threadIdx.x == BLOCK - 1) pre[NSEG] = v;
+    if (threadIdx.x == RUN_BLOCK - 1) pre[NSEG] = v;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -946,10 +955,10 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     ostart[O_COUNT] = acc;
     oraw[O_COUNT] = pre[NSEG];
   }
-  __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t win[(RUN_BLOCK / 64) * WIN_WAVE_BYTES];
   __syncthreads();  // ostart / oraw
   const int total = ostart[O_COUNT];
-  const int base = (blockIdx.x * BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
+  const int base = (blockIdx.x * RUN_BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
   int oj = 0;  // ostart[oj] <= base < ostart[oj + 1] (wave-uniform)
   while (oj + 1 < O_COUNT && ostart[oj + 1] <= base) ++oj;
   oj = __builtin_amdgcn_readfirstlane(oj);
@@ -1024,7 +1033,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
   }
   __builtin_amdgcn_s_setprio(0);
   wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
-             regens + wave_sum(lregen), true);
+             regens + wave_sum(lregen), true, (int64_t)blockIdx.x / (BLOCK / RUN_BLOCK));
   kst_end(ks, kt0);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
@@ -1036,7 +1045,7 @@ __global__ __launch_bounds__(BLOCK) void k_run(Soa S, int64_t n, Level L,
     const int src = bl ? __ffsll((long long)bl) - 1 : 0;
     const unsigned long long a1 = __shfl(t1, src, 64);
     const unsigned long long a2 = __shfl(t2, src, 64);
-    const int wv = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    const int wv = (blockIdx.x * RUN_BLOCK + threadIdx.x) >> 6;
     const unsigned long long rt3 = __builtin_amdgcn_s_memrealtime();
     // the phases of the lane whose option loop ran longest (the wave's own time)
     int lmax = src;
@@ -1732,7 +1741,8 @@ int launch_step(tg_batch* h, StepCtx& c, const StepIO& io_in, bool ar, hipStream
                        ks0);
     HIP_TRY(hipGetLastError());
     if (mid) HIP_TRY(hipEventRecord(mid, st));  // (tg_rollout's stagger between groups)
-    hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n)), block, 0, st, S, c.n, h->L, h->grid, io, q, w,
+    hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n) * (BLOCK / RUN_BLOCK)), dim3(RUN_BLOCK), 0, st, S,
+                       c.n, h->L, h->grid, io, q, w,
                        g0, c.stats, h->err, ks1);
   }
   HIP_TRY(hipGetLastError());
@@ -2120,7 +2130,8 @@ int tg_kernel_info(tg_batch* h, int kernel, int32_t* blocks_per_cu, int32_t* vgp
   hipFuncAttributes fa;
   HIP_TRY(hipFuncGetAttributes(&fa, k));
   int nb = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, BLOCK, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kernel == TG_KERNEL_RUN ? RUN_BLOCK : BLOCK,
+                                                       0));
   if (blocks_per_cu) *blocks_per_cu = nb;
   if (vgprs) *vgprs = fa.numRegs;
   if (sgprs) *sgprs = -1;  // not reported by hipFuncGetAttributes

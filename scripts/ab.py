@@ -46,8 +46,9 @@ def time_one(path, policy, n, burn, steps):
     vec.stats_reset()
     vec.set_timing(int(os.environ.get("TIMING", "0")))  # 0: the wall clock only (no events / stamps)
     t0 = time.perf_counter()
+    out = None
     for j in range(steps):
-        vec.step(acts[j] if acts is not None else vec.policy_actions(burn + j, ACTION_SEED, policy))
+        out = vec.step(acts[j] if acts is not None else vec.policy_actions(burn + j, ACTION_SEED, policy))
         if j % 10 == 9:
             vec.drain_episodes(rec, cnt)
     if regen:
@@ -55,8 +56,13 @@ def time_one(path, policy, n, burn, steps):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     st = vec.stats()
+    # the last step's rows and the run's counts: equal for every variant (same results)
+    obs = out[0].contiguous().view(torch.int64)
+    digest = "%x/%d/%d" % (int((obs * torch.arange(1, obs.numel() + 1, device=obs.device,
+                                                       dtype=torch.int64).view_as(obs)).sum()) & (2**64 - 1),
+                          st["ticks"], st["draws"])
     vec.close()
-    return {"ms_step": dt / steps * 1e3,
+    return {"digest": digest, "ms_step": dt / steps * 1e3,
             "kernel_ms": st["kernel_ms"] / max(st.get("timed_launches") or 1, 1),
             "lane_eff": st["ticks"] / max(64 * st["wave_ticks"], 1)}
 
@@ -78,6 +84,10 @@ def main():
                 best = out.get(key)
                 if best is None or res["ms_step"] < best["ms_step"]:
                     out[key] = res
+    for pol in policies:
+        ds = {name: out["%s/%s" % (pol, name)]["digest"] for name, _ in variants}
+        if len(set(ds.values())) > 1:
+            print("DIGEST MISMATCH", pol, json.dumps(ds), flush=True)
     print(json.dumps({"best": out, "n": n, "steps": steps}), flush=True)
 
 
