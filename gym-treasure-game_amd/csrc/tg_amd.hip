@@ -80,28 +80,43 @@ struct LdsLevel {
   uint32_t trig[12];
   uint32_t grid[MAX_CELLS / 4];
 };
-template <int NT = BLOCK>  // NT: the workgroup's threads
-__device__ __forceinline__ void stage_level(LdsLevel& lv, const uint32_t* __restrict__ grid,
-                                            const Level& L, uint32_t* masks = nullptr) {
-  const int nwords = ((L.W + 2 * PAD) * (L.H + 2 * PAD) + 3) / 4;
-  for (int i = threadIdx.x; i < nwords; i += NT) lv.grid[i] = grid[i];
-  if (threadIdx.x < 12) lv.trig[threadIdx.x] = L.trig[threadIdx.x >> 1][threadIdx.x & 1];
+TG_HD int grid_words(int W, int H) { return ((W + 2 * PAD) * (H + 2 * PAD) + 3) / 4; }
+// grid words, trigger table and (masks: non-null) the level bitmasks into LDS; NT: the
+// workgroup's threads
+template <int NT = BLOCK>
+__device__ __forceinline__ void stage_cells(uint32_t* lgrid, uint32_t* ltrig,
+                                            const uint32_t* __restrict__ grid, const Level& L,
+                                            uint32_t* masks = nullptr) {
+  const int nwords = grid_words(L.W, L.H);
+  for (int i = threadIdx.x; i < nwords; i += NT) lgrid[i] = grid[i];
+  if (threadIdx.x < 12) ltrig[threadIdx.x] = L.trig[threadIdx.x >> 1][threadIdx.x & 1];
   if (masks && L.masks)
     for (int i = threadIdx.x; i < mk_words(L.W, L.H); i += NT) masks[i] = L.masks[i];
   __syncthreads();
+}
+__device__ __forceinline__ void stage_level(LdsLevel& lv, const uint32_t* __restrict__ grid,
+                                            const Level& L) {
+  stage_cells(lv.grid, lv.trig, grid, L);
 }
 #define LEVEL_IN_LDS()                   \
   __shared__ LdsLevel lv;                \
   stage_level(lv, grid, L);              \
   const uint32_t* const trig = lv.trig;  \
   const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H}
-// the same with the level bitmasks (Map::mk) staged too: the option loops' kernels
-#define LEVEL_IN_LDS_MK()                                                      \
-  __shared__ LdsLevel lv;                                                      \
-  __shared__ uint32_t lmk[MK_MAX_WORDS];                                       \
-  stage_level<RUN_BLOCK>(lv, grid, L, lmk);                                    \
-  const uint32_t* const trig = lv.trig;                                        \
-  const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H, L.masks ? lmk : nullptr}
+// k_run's LDS beyond its few static words: the waves' code windows (WIN_WAVE_BYTES each, at
+// offset 0: 16-B aligned for the LDS-DMA), then the level's grid words and bitmasks (Map::mk),
+// sized for the handle's level at launch instead of for the largest level (MAX_CELLS + 25 *
+// MK_DIM words: 5.5 KB against ~2 KB for the default level), so that a 64-thread workgroup
+// still fits 5 waves per SIMD
+#define RUN_LEVEL_IN_LDS()                                                                \
+  extern __shared__ uint4 run_lds[];                                                      \
+  __shared__ uint32_t ltrig[12];                                                          \
+  uint8_t* const win = reinterpret_cast<uint8_t*>(run_lds);                                \
+  uint32_t* const lgrid = reinterpret_cast<uint32_t*>(win + (RUN_BLOCK / 64) * WIN_WAVE_BYTES); \
+  uint32_t* const lmk = lgrid + grid_words(L.W, L.H);                                     \
+  stage_cells<RUN_BLOCK>(lgrid, ltrig, grid, L, lmk);                                     \
+  const uint32_t* const trig = ltrig;                                                     \
+  const Map m{reinterpret_cast<const uint8_t*>(lgrid), L.W, L.H, L.masks ? lmk : nullptr}
 
 __device__ __forceinline__ void store_obs(double* out, int64_t i, const double o[9]) {
   double* p = out + i * 9;
@@ -146,6 +161,11 @@ constexpr int WIN_WAVE_BYTES = WIN_SLOTS * WIN_SLOT_BYTES;  // 4 KB per wave
 constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
 static_assert(WIN_WAVE_BYTES >= WAVE_SCRATCH, "wave_refill reuses the window as scratch");
 static_assert(WIN_DRAWS - WIN_UNIT + 1 >= (int)MAX_TICK_DRAWS, "a refilled window holds a tick's draws");
+// k_run's dynamic LDS for a level (RUN_LEVEL_IN_LDS)
+TG_HD size_t run_lds_bytes(int W, int H, bool masks) {
+  return (size_t)(RUN_BLOCK / 64) * WIN_WAVE_BYTES +
+         4 * (size_t)(grid_words(W, H) + (masks ? mk_words(W, H) : 0));
+}
 
 // LDS-DMA of one WIN_UNIT-byte unit per active lane into LDS [m0 + lane * WIN_UNIT]; M0 is
 // saved/restored
@@ -955,7 +975,6 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     ostart[O_COUNT] = acc;
     oraw[O_COUNT] = pre[NSEG];
   }
-  __shared__ __attribute__((aligned(16))) uint8_t win[(RUN_BLOCK / 64) * WIN_WAVE_BYTES];
   __syncthreads();  // ostart / oraw
   const int total = ostart[O_COUNT];
   const int base = (blockIdx.x * RUN_BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
@@ -987,7 +1006,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     a2w = w.wang[at];
     epw = w.wep[at];
   }
-  LEVEL_IN_LDS_MK();  // includes the barrier
+  RUN_LEVEL_IN_LDS();  // includes the barrier
   StepResult r{0, 0, 0, 0};
   Env e;
   e.mti = 0u;
@@ -1741,8 +1760,9 @@ int launch_step(tg_batch* h, StepCtx& c, const StepIO& io_in, bool ar, hipStream
                        ks0);
     HIP_TRY(hipGetLastError());
     if (mid) HIP_TRY(hipEventRecord(mid, st));  // (tg_rollout's stagger between groups)
-    hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n) * (BLOCK / RUN_BLOCK)), dim3(RUN_BLOCK), 0, st, S,
-                       c.n, h->L, h->grid, io, q, w,
+    hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n) * (BLOCK / RUN_BLOCK)), dim3(RUN_BLOCK),
+                       run_lds_bytes(h->L.W, h->L.H, h->L.masks != nullptr), st, S, c.n, h->L,
+                       h->grid, io, q, w,
                        g0, c.stats, h->err, ks1);
   }
   HIP_TRY(hipGetLastError());
@@ -2130,12 +2150,13 @@ int tg_kernel_info(tg_batch* h, int kernel, int32_t* blocks_per_cu, int32_t* vgp
   hipFuncAttributes fa;
   HIP_TRY(hipFuncGetAttributes(&fa, k));
   int nb = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kernel == TG_KERNEL_RUN ? RUN_BLOCK : BLOCK,
-                                                       0));
+  const bool run = kernel == TG_KERNEL_RUN;
+  const size_t dyn = run ? run_lds_bytes(h->L.W, h->L.H, h->L.masks != nullptr) : 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, run ? RUN_BLOCK : BLOCK, dyn));
   if (blocks_per_cu) *blocks_per_cu = nb;
   if (vgprs) *vgprs = fa.numRegs;
   if (sgprs) *sgprs = -1;  // not reported by hipFuncGetAttributes
-  if (lds_bytes) *lds_bytes = (int32_t)fa.sharedSizeBytes;
+  if (lds_bytes) *lds_bytes = (int32_t)(fa.sharedSizeBytes + dyn);
   return TG_OK;
 }
 
