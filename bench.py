@@ -66,16 +66,31 @@ EP_CAP = 4096          # episode records gathered per rank per step of a drain i
 #   k_run, valid env: the worklist row 44 read; state 16 + angles 16 + episode 8 + obs 72 +
 #     rows 6 written (118); random() draw: its 1-B code (tg_core.h draw_code)
 #   k_regen (every 16 compact steps, tg_regenerate), per MT generation regenerated (tg_core.h:
-#     halves of MT_HALF_GENS = 8 generations, chained in LDS): 624 words + 312 codes written,
-#     an eighth of the source generation's 624 words, of the 4-B list entry and of the env's
-#     4-B state word read and written
+#     halves of MT_HALF_GENS = 8 generations, chained in LDS): 312 codes + the words the build
+#     stores (round 4: the even generations, so 624 words every other generation; tg_mt_layout)
+#     written, an eighth of the source generation's 624 words, of the 4-B list entry and of the
+#     env's 4-B state word read and written
 #   k_step (direct mode): one kernel, the same without the worklist round trip
 MT_HALF_GENS = 8
 CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 78, 44, 4 / MT_HALF_GENS
 RUN_VALID, RUN_DRAW = 162, 1
-REGEN_GEN = 2496 + 312 + (2496 + 4 + 8) / MT_HALF_GENS
 DIRECT_ENV, DIRECT_INVALID, DIRECT_VALID = 44, 78, 118
-DIRECT_REGEN = 2496 + 312 + 2496 / MT_HALF_GENS
+# per generation regenerated, set by set_layout from the loaded library (round 3's layout, which
+# stored every generation's words, lacks tg_mt_layout)
+REGEN_GEN = DIRECT_REGEN = 0.0
+
+
+def set_layout(L):
+    """REGEN_GEN / DIRECT_REGEN for the loaded library's MT storage."""
+    global REGEN_GEN, DIRECT_REGEN
+    stored = 1.0
+    if hasattr(L, "tg_mt_layout"):
+        ring, kept = ctypes.c_int32(), ctypes.c_int32()
+        L.tg_mt_layout(ctypes.byref(ring), ctypes.byref(kept), None)
+        stored = kept.value / ring.value
+    REGEN_GEN = 2496 * stored + 312 + (2496 + 4 + 8) / MT_HALF_GENS
+    DIRECT_REGEN = 2496 * stored + 312 + 2496 / MT_HALF_GENS
+    return stored
 BYTES_DRAW = RUN_DRAW
 # SURVEY.md §8(d)'s layout-independent count per env-step: action 4 + obs 72 + reward 4 +
 # valid 1 + done 1 + state read/write 2 x 40 = 162, plus 24 per random() draw (8 B of MT words
@@ -330,6 +345,7 @@ class Runner:
         self.log = D.EpisodeLog(drains, world, self.ep_cap, dev, keep=keep_log)
         L, h = vec._L, vec.handle
         self.L, self.h = L, h
+        self.mt_stored = set_layout(L)
         self.flags = tg._lib.TG_STEP_AUTORESET if self.autoreset else 0
         p = self.p
         self.stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)

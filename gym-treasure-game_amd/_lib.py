@@ -33,7 +33,7 @@ EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_
            "tg_available_mask",
            "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing", "tg_regenerate",
            "tg_set_episode_capacity", "tg_predicate_table",
-           "tg_get_stats", "tg_stats_reset", "tg_kernel_info", "tg_read_state", "tg_write_state", "tg_render_init", "tg_frame_shape",
+           "tg_get_stats", "tg_stats_reset", "tg_kernel_info", "tg_mt_layout", "tg_read_state", "tg_write_state", "tg_render_init", "tg_frame_shape",
            "tg_render", "tg_last_error", "tg_version")
 
 
@@ -104,6 +104,7 @@ def load():
         "tg_get_stats": (i32, [P, ctypes.POINTER(Stats)]),
         "tg_stats_reset": (i32, [P]),
         "tg_set_groups": (i32, [P, i32, i32]),
+        "tg_mt_layout": (i32, [ctypes.POINTER(ctypes.c_int32)] * 3),
         "tg_kernel_info": (i32, [P, i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                  ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
         "tg_read_state": (i32, [P, P, P, P, P, P, P, P]),

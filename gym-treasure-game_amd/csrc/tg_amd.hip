@@ -182,15 +182,29 @@ __device__ __forceinline__ void glds_unit(uint32_t m0, const void* gptr) {
       : "memory");
 }
 
-// the rare second crossing (RngCodes::fill), out of line so that the draw sites stay small
+// the rare second crossing (RngCodes::fill), out of line so that the draw sites stay small, its
+// generation loops out of line too: a callee's registers add to its caller's allocation (k_run
+// 104 VGPRs, 4 waves per SIMD, with them inline)
+__device__ __noinline__ void twist_gen_call(const uint32_t* src, uint32_t* dst) { twist_gen(src, dst); }
+__device__ __noinline__ void gen_codes_call(const uint32_t* w, uint8_t* c) { gen_codes(w, c); }
+struct GenCalls {
+  __device__ void twist(const uint32_t* src, uint32_t* dst) const { twist_gen_call(src, dst); }
+  __device__ void codes(const uint32_t* w, uint8_t* c) const { gen_codes_call(w, c); }
+};
+// a double's two words (RngCodes::random), out of line for the same reason
+__device__ __noinline__ uint2 mt_pair_call(const uint32_t* mt, uint32_t p) {
+  uint2 w;
+  mt_pair(mt, p, w.x, w.y);
+  return w;
+}
 __device__ __noinline__ void regen_half(uint32_t* mt, uint8_t* mc, uint32_t h) {
-  twist_half(mt, h, mc);
+  twist_half(mt, h, mc, false, GenCalls());
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
 }
 
 struct RngCodes {
   static constexpr uint32_t NONE = 0xFFFFFFFFu;
-  uint32_t* mt;      // this env's MT_WORDS words (HBM)
+  uint32_t* mt;      // this env's MT_STORE stored words (HBM)
   uint8_t* mc;       // this env's MT_CODES code bytes (HBM)
   lds_u8* cell;      // this lane's unit in slot 0 of the wave's window
   uint32_t m0;       // LDS address of slot 0 of the wave's window (wave-uniform)
@@ -349,11 +363,12 @@ struct RngCodes {
     return c;
   }
   // one draw as its double (rare): the code is consumed too, the value built from the words
+  // (an odd generation's twisted from the stored one before it, tg_core.h mt_pair)
   __device__ __forceinline__ double random() {
     uint32_t p = (pos >> 1) + n;
     p = 2u * (p >= (uint32_t)MT_CODES ? p - (uint32_t)MT_CODES : p);
     (void)code();
-    const uint2 w = *reinterpret_cast<const uint2*>(mt + p);
+    const uint2 w = mt_pair_call(mt, p);
     return mt_double(w.x, w.y);
   }
   __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
@@ -380,15 +395,16 @@ __device__ __forceinline__ void wave_refill(unsigned long long need, uint32_t* e
                                             uint32_t state, lds_u32* scratch) {
   const uint32_t pos = state & MT_POS_MASK;
   const uint32_t dst = (uint32_t)MT_HALF - mt_half(pos);
-  const uint64_t src_l = (uint64_t)(uintptr_t)(env_mt + mt_prev_gen(dst));
-  const uint64_t dst_l = (uint64_t)(uintptr_t)(env_mt + dst);
-  const uint64_t dc_l = (uint64_t)(uintptr_t)(env_mc + dst / 2);
+  const uint64_t src_l = (uint64_t)(uintptr_t)(env_mt + regen_src_off(dst));
+  const uint64_t w_l = (uint64_t)(uintptr_t)env_mt;
+  const uint64_t c_l = (uint64_t)(uintptr_t)env_mc;
+  const int g0_l = (int)(dst / (uint32_t)MT_N);
   while (need) {
     const int L = __ffsll((long long)need) - 1;
     need &= need - 1;
     wave_twist_gens((const glb_u32*)(uintptr_t)readlane64(src_l, L),
-                    (glb_u32*)(uintptr_t)readlane64(dst_l, L),
-                    (uint8_t*)(uintptr_t)readlane64(dc_l, L), MT_HALF_GENS, scratch);
+                    (glb_u32*)(uintptr_t)readlane64(w_l, L), (uint8_t*)(uintptr_t)readlane64(c_l, L),
+                    __builtin_amdgcn_readlane(g0_l, L), MT_HALF_GENS, true, scratch);
   }
 }
 
@@ -437,24 +453,24 @@ __global__ void k_kst_init(unsigned long long* ks, int64_t slots) {
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
-// random.seed(seed0 + i): init_by_array into the ring's last generation slot (tg_core.h
-// init_mt); k_gen_twist then makes generations 1 .. 2 x MT_HALF_GENS, and k_reset (mask NULL)
+// random.seed(seed0 + i): init_by_array into half 0's last stored slot (tg_core.h init_mt);
+// k_gen_twist then makes the ring's 2 x MT_HALF_GENS generations from it, and k_reset (mask NULL)
 // performs the constructor's game build (_TreasureGameImpl.__init__, IM/:31-53: 4 draws) —
 // tg_create.
 __global__ __launch_bounds__(BLOCK) void k_create(Soa S, int64_t n, uint64_t seed0,
                                                    const uint32_t* __restrict__ genrand) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
-  seed_mt(S.mt + i * MT_WORDS + (MT_WORDS - MT_N), genrand, seed0 + (uint64_t)i);
+  seed_mt(S.mt + i * MT_STORE + MT_SEED_OFF, genrand, seed0 + (uint64_t)i);
   Env e{};
   e.mti = 0u;
   S.st4[i] = pack(e);
   S.ang[i] = make_double2(0.0, 0.0);
   S.ep[i] = make_int2(0, 0);
 }
-// `gens` generations for every env, in sequence after the one at word offset src, into word
-// offsets dst, dst + MT_N, ... (words and codes; tg_create, tg_write_state)
-__global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t src, uint32_t dst,
+// `gens` generations for every env, in sequence after the stored words at offset src: ring
+// generations g0, g0 + 1, ... (codes; words of the even ones; tg_create, tg_write_state)
+__global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t src, int g0,
                                                      int gens) {
   __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -464,15 +480,15 @@ __global__ __launch_bounds__(BLOCK) void k_gen_twist(Soa S, int64_t n, uint32_t 
     const int L = __ffsll((long long)need) - 1;
     need &= need - 1;
     const int64_t e = i0 + L;
-    wave_twist_gens((const glb_u32*)(S.mt + e * MT_WORDS + src), (glb_u32*)(S.mt + e * MT_WORDS + dst),
-                    S.mc + e * MT_CODES + dst / 2, gens, (lds_u32*)scratch[threadIdx.x >> 6]);
+    wave_twist_gens((const glb_u32*)(S.mt + e * MT_STORE + src), (glb_u32*)(S.mt + e * MT_STORE),
+                    S.mc + e * MT_CODES, g0, gens, false, (lds_u32*)scratch[threadIdx.x >> 6]);
   }
 }
 
-// the draw codes of the ring's first generation (words [0, 624)) of every env (tg_write_state)
+// the draw codes of the ring's first generation (stored words [0, 624)) of every env (tg_write_state)
 __global__ __launch_bounds__(BLOCK) void k_gen_codes(Soa S, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  if (i < n) gen_codes(S.mt + i * MT_WORDS, S.mc + i * MT_CODES);
+  if (i < n) gen_codes(S.mt + i * MT_STORE, S.mc + i * MT_CODES);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
@@ -487,7 +503,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
   if (live) {
     unpack(S.st4[i], S.ang[i], e);
     if (reset) {
-      Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
+      Rng rng(S.mt + i * MT_STORE, e.mti, S.mc + i * MT_CODES);
       reset_env(L, e, rng);
       e.mti = rng.finish();
     }
@@ -498,7 +514,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
     }
   }
   const bool stale = reset && (e.mti & MT_STALE);
-  wave_refill(__ballot(stale), S.mt + (live ? i : 0) * MT_WORDS, S.mc + (live ? i : 0) * MT_CODES, e.mti,
+  wave_refill(__ballot(stale), S.mt + (live ? i : 0) * MT_STORE, S.mc + (live ? i : 0) * MT_CODES, e.mti,
               (lds_u32*)scratch[threadIdx.x >> 6]);
   if (reset) {
     e.mti &= ~(MT_STALE | MT_LISTED);
@@ -690,7 +706,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
     unpack(S.st4[i], S.ang[i], e);
     ep = S.ep[i];
     ep_in = ep;
-    RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
+    RngCodes rng(S.mt + i * MT_STORE, S.mc + i * MT_CODES, e.mti, wscr);
     int act;
     if constexpr (POL >= 0) {
       act = policy_action(L, m, e, POL, io.a0, g0 + i, io.t);
@@ -709,7 +725,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
   }
   // one pass, no classify pass after it: regenerate the halves left in this launch now
   const unsigned long long need = __ballot(live && (e.mti & MT_STALE));
-  wave_refill(need, S.mt + (live ? i : 0) * MT_WORDS,
+  wave_refill(need, S.mt + (live ? i : 0) * MT_STORE,
               S.mc + (live ? i : 0) * MT_CODES, e.mti,
               (lds_u32*)wscr);
   e.mti &= ~(MT_STALE | MT_LISTED);
@@ -883,7 +899,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     e.ang0 = a2.x;
     e.ang1 = a2.y;
     dn = is_done(e);
-    Rng rng(S.mt + i * MT_WORDS, e.mti, S.mc + i * MT_CODES);
+    Rng rng(S.mt + i * MT_STORE, e.mti, S.mc + i * MT_CODES);
     StepResult r{0, 0, (int)dn, 0};
     finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io, orow);
     // the stale half keeps its bits unless the auto-reset's draws crossed into it (the Rng then
@@ -1028,7 +1044,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   if (live) {
     unpack(s4w, a2w, e);
     ep = epw;
-    RngCodes rng(S.mt + i * MT_WORDS, S.mc + i * MT_CODES, e.mti, wscr);
+    RngCodes rng(S.mt + i * MT_STORE, S.mc + i * MT_CODES, e.mti, wscr);
     rng.prime();  // issue the code loads now; the first draw comes after the policy setup
     TG_STAMP(t1);
     if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
@@ -1132,7 +1148,7 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
   uint32_t* const st_w = reinterpret_cast<uint32_t*>(S.st4);  // word 4i + 3: env i's MT word
   auto src_of = [&](uint32_t env, uint32_t s) {
     const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
-    return (const glb_u32*)(S.mt + (int64_t)env * MT_WORDS + mt_prev_gen(dst));
+    return (const glb_u32*)(S.mt + (int64_t)env * MT_STORE + regen_src_off(dst));
   };
   int halves = 0;
   while (true) {
@@ -1159,8 +1175,8 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
       const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
       TwistIn t;
       twist_load(src_of(env, s), t);
-      twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_WORDS + dst),
-                        S.mc + (int64_t)env * MT_CODES + dst / 2, MT_HALF_GENS, scr);
+      twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_STORE), S.mc + (int64_t)env * MT_CODES,
+                  (int)(dst / (uint32_t)MT_N), MT_HALF_GENS, true, scr);
       if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
       ++halves;
     }
@@ -1260,7 +1276,8 @@ __global__ __launch_bounds__(BLOCK) void k_predicates(Level L, const uint32_t* _
 }
 
 // tg_read_state's MT part: the generation holding each env's position (CPython's mt[]),
-// envs [first, first + count) -> dst [count][624] (contiguous), 16 B per lane
+// envs [first, first + count) -> dst [count][624] (contiguous), 4 words per lane (an odd
+// generation's twisted from the stored one before it)
 __global__ __launch_bounds__(BLOCK) void k_gather_mt(Soa S, int64_t first, int64_t count,
                                                       uint32_t* __restrict__ dst) {
   constexpr int Q = MT_N / 4;  // 156 uint4 per generation
@@ -1269,9 +1286,17 @@ __global__ __launch_bounds__(BLOCK) void k_gather_mt(Soa S, int64_t first, int64
   const int64_t k = t / Q;
   const int q = (int)(t - k * Q);
   const int64_t i = first + k;
-  const uint32_t pos = S.st4[i].w & MT_POS_MASK;
-  const uint4* src = reinterpret_cast<const uint4*>(S.mt + i * MT_WORDS + (pos - pos % MT_N));
-  reinterpret_cast<uint4*>(dst)[t] = src[q];
+  const uint32_t g = (S.st4[i].w & MT_POS_MASK) / (uint32_t)MT_N;
+  const uint32_t* const mt = S.mt + i * MT_STORE;
+  uint4 v;
+  if (g & 1u) {
+    const uint32_t* const prev = mt + mt_store_off(g - 1u);
+    v = make_uint4(twist_at(prev, 4 * q), twist_at(prev, 4 * q + 1), twist_at(prev, 4 * q + 2),
+                   twist_at(prev, 4 * q + 3));
+  } else {
+    v = reinterpret_cast<const uint4*>(mt + mt_store_off(g))[q];
+  }
+  reinterpret_cast<uint4*>(dst)[t] = v;
 }
 
 // ---- the N=1 drop-in over a Python-level random stream (tg_step1_py / tg_reset1_py) ---------
@@ -1597,7 +1622,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   ALLOC(h->S.st4, sizeof(uint4) * n);
   ALLOC(h->S.ang, sizeof(double2) * n);
   ALLOC(h->S.ep, sizeof(int2) * n);
-  ALLOC(h->S.mt, sizeof(uint32_t) * MT_WORDS * (size_t)n);
+  ALLOC(h->S.mt, sizeof(uint32_t) * MT_STORE * (size_t)n);
   ALLOC(h->S.mc, sizeof(uint8_t) * MT_CODES * (size_t)n);
   ALLOC(h->eps, sizeof(tg_episode) * (size_t)h->eps_cap);
   ALLOC(h->eps_count, sizeof(int32_t));
@@ -1617,7 +1642,7 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   hipLaunchKernelGGL(k_create, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n,
                      seed_base + (uint64_t)global_offset, h->genrand);
   hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n,
-                     (uint32_t)(MT_WORDS - MT_N), 0u, 2 * MT_HALF_GENS);
+                     MT_SEED_OFF, 0, 2 * MT_HALF_GENS);
   hipLaunchKernelGGL(k_reset, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, h->L,
                      (const uint8_t*)nullptr, (double*)nullptr, 0u);
   hipError_t e = hipGetLastError();
@@ -1659,7 +1684,7 @@ namespace {
 // k_regen over the pending refill-list slots (timed with its own event pair when timing is on)
 // a stepper's envs as a Soa view (StepCtx: envs [off, off + n) of the handle)
 Soa soa_of(const tg_batch* h, const StepCtx& c) {
-  return Soa{h->S.st4 + c.off, h->S.ang + c.off, h->S.ep + c.off, h->S.mt + c.off * (int64_t)MT_WORDS,
+  return Soa{h->S.st4 + c.off, h->S.ang + c.off, h->S.ep + c.off, h->S.mt + c.off * (int64_t)MT_STORE,
              h->S.mc + c.off * (int64_t)MT_CODES};
 }
 int launch_regen(tg_batch* h, StepCtx& c, hipStream_t st) {
@@ -2139,6 +2164,13 @@ int tg_stats_reset(tg_batch* h) {
   return TG_OK;
 }
 
+int tg_mt_layout(int32_t* ring_words, int32_t* stored_words, int32_t* code_bytes) {
+  if (ring_words) *ring_words = MT_WORDS;
+  if (stored_words) *stored_words = MT_STORE;
+  if (code_bytes) *code_bytes = MT_CODES;
+  return TG_OK;
+}
+
 int tg_kernel_info(tg_batch* h, int kernel, int32_t* blocks_per_cu, int32_t* vgprs, int32_t* sgprs,
                    int32_t* lds_bytes) {
   BIND(h);
@@ -2267,10 +2299,10 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
                          : make_int2(0, (int32_t)h->tstep);
     HIP_TRY(hipMemcpy(h->S.ep, e2.data(), sizeof(int2) * n, hipMemcpyHostToDevice));
   }
-  HIP_TRY(hipMemcpy2D(h->S.mt, sizeof(uint32_t) * MT_WORDS, mt, sizeof(uint32_t) * MT_N,
+  HIP_TRY(hipMemcpy2D(h->S.mt, sizeof(uint32_t) * MT_STORE, mt, sizeof(uint32_t) * MT_N,
                       sizeof(uint32_t) * MT_N, (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_gen_codes, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n);
-  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, 0u, (uint32_t)MT_N,
+  hipLaunchKernelGGL(k_gen_twist, dim3(grid_for(n)), dim3(BLOCK), 0, 0, h->S, n, 0u, 1,
                      2 * MT_HALF_GENS - 1);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipDeviceSynchronize());

@@ -34,7 +34,7 @@ struct Soa {
   uint4* st4;
   double2* ang;
   int2* ep;
-  uint32_t* mt;   // [N][MT_WORDS]
+  uint32_t* mt;   // [N][MT_STORE]: the ring's even generations (tg_core.h)
   uint8_t* mc;    // [N][MT_CODES]: the draw codes of the ring's generations (tg_core.h draw_code)
 };
 

@@ -145,11 +145,22 @@ TG_HD int floordiv48(int a) { return div48(a + 16 * S) - 16; }              // -
 //   a two-generation ring whose every twist re-reads its source from HBM, and the refill
 //   list is an eighth as long (A/B, 1M envs: 2 + 2 / 4 + 4 / 8 + 8 per half: uniform 0.172 /
 //   0.168 / 0.164 ms, masked 0.399 / 0.391 / 0.368 ms per step; 1 + 1: 0.176 / 0.483).
-//   40 KB of words + 5 KB of codes per env.
+//   Stored words (round 4): only the EVEN generations of the ring (gens 0, 2, ..., 14 of the
+//   16; MT_STORE words per env, mt_store_off), the codes of all.  The option loops read codes;
+//   the words serve the rare draws that need their double (handle angles, an auto-reset's
+//   gauss) and the twists.  An odd generation's word is the twist of the stored generation
+//   before it (twist_at: <= 4 twist_word evaluations on that generation's words, mt_pair), and
+//   a half's regeneration starts from the other half's generation 7 = the twist of its stored
+//   generation 6.  A regenerated generation costs 312 B of codes + 1,248 B of words instead of
+//   312 + 2,496.  20 KB of words + 5 KB of codes per env.
 // ==========================================================================================
 constexpr int MT_HALF_GENS = 8;                // generations per half
-constexpr int MT_HALF = MT_HALF_GENS * MT_N;   // words per half
-constexpr int MT_WORDS = 2 * MT_HALF;          // per env
+constexpr int MT_HALF = MT_HALF_GENS * MT_N;   // ring positions per half (words of 8 generations)
+constexpr int MT_WORDS = 2 * MT_HALF;          // ring positions per env
+constexpr int MT_STORE = MT_WORDS / 2;         // words stored per env: the even generations
+static_assert(MT_HALF_GENS % 2 == 0, "a half starts on a stored generation");
+// word offset in the stored words of ring generation g (even; g = ring position / MT_N)
+TG_HD uint32_t mt_store_off(uint32_t g) { return (g >> 1) * (uint32_t)MT_N; }
 constexpr uint32_t MT_STALE = 1u << 31;   // state word: the half not holding pos is stale
 constexpr uint32_t MT_LISTED = 1u << 30;  // state word: that stale half is on a refill list (k_regen)
 constexpr uint32_t MT_POS_MASK = 0xFFFFu;
@@ -179,10 +190,53 @@ TG_HD void twist_gen(const uint32_t* src, uint32_t* dst) {
     dst[p] = mt_twist(src[p], src[p + 1], dst[p - (MT_N - MT_M)]);
   dst[MT_N - 1] = mt_twist(src[MT_N - 1], dst[0], dst[MT_M - 1]);
 }
+// the same in place: twist_gen reads src only at or after the word it writes and dst only
+// before it, so src == dst is CPython's own in-place loop
+TG_HD void twist_gen_inplace(uint32_t* w) { twist_gen(w, w); }
+// Word i (< 623) of the generation after g, from g's words alone: new word i reads new word
+// i - 227 for i >= 227 (twist_gen), so it is a chain of at most 3 twist words back to an i < 227.
+TG_HD uint32_t twist_at_lo(const uint32_t* g, int i) {
+  constexpr int K = MT_N - MT_M;  // 227
+  int j = i;
+  int hops = 0;
+  while (j >= K) {
+    j -= K;
+    ++hops;
+  }
+  uint32_t w = mt_twist(g[j], g[j + 1], g[j + MT_M]);
+  while (hops-- > 0) {
+    j += K;
+    w = mt_twist(g[j], g[j + 1], w);
+  }
+  return w;
+}
+// word i of the generation after g (word 623 reads new words 0 and 396)
+TG_HD uint32_t twist_at(const uint32_t* g, int i) {
+  return i < MT_N - 1 ? twist_at_lo(g, i)
+                      : mt_twist(g[MT_N - 1], twist_at_lo(g, 0), twist_at_lo(g, MT_M - 1));
+}
+// the two words at ring position p (even) from the stored generations: an even generation's
+// are stored, an odd one's are twisted from the generation before it (rare: the draws that
+// need their double)
+TG_HD void mt_pair_odd(const uint32_t* mt, uint32_t g, uint32_t i, uint32_t* w) {
+  const uint32_t* const prev = mt + mt_store_off(g - 1u);
+  w[0] = twist_at(prev, (int)i);
+  w[1] = twist_at(prev, (int)i + 1);
+}
+TG_HD void mt_pair(const uint32_t* mt, uint32_t p, uint32_t& w0, uint32_t& w1) {
+  const uint32_t g = p / (uint32_t)MT_N, i = p - g * (uint32_t)MT_N;
+  if (g & 1u) {
+    uint32_t w[2];
+    mt_pair_odd(mt, g, i, w);
+    w0 = w[0];
+    w1 = w[1];
+  } else {
+    w0 = mt[mt_store_off(g) + i];
+    w1 = mt[mt_store_off(g) + i + 1];
+  }
+}
 // word offset of the half holding word position pos
 TG_HD uint32_t mt_half(uint32_t pos) { return pos >= (uint32_t)MT_HALF ? (uint32_t)MT_HALF : 0u; }
-// word offset of the generation before the one at word offset g (ring order)
-TG_HD uint32_t mt_prev_gen(uint32_t g) { return (g == 0u ? (uint32_t)MT_WORDS : g) - (uint32_t)MT_N; }
 
 // ---- draw codes ------------------------------------------------------------------------------
 // Every random() value the option loops consume decides one of four things, each a comparison
@@ -252,13 +306,40 @@ TG_HD int code_step(uint32_t c, bool neg) {
 TG_HD void gen_codes(const uint32_t* words, uint8_t* c) {
   for (int k = 0; k < MT_N / 2; ++k) c[k] = (uint8_t)draw_code(mt_double(words[2 * k], words[2 * k + 1]));
 }
-// regenerate half h (word offset 0 / MT_HALF): its generations in sequence from the one before
-// it (the other half's last), words and, with mc, codes (per-lane form of wave_twist_gens)
-TG_HD void twist_half(uint32_t* mt, uint32_t h, uint8_t* mc = nullptr) {
-  for (int g = 0; g < MT_HALF_GENS; ++g) {
-    const uint32_t dst = h + (uint32_t)(g * MT_N);
-    twist_gen(mt + mt_prev_gen(dst), mt + dst);
-    if (mc) gen_codes(mt + dst, mc + dst / 2);
+// Regenerate half h (ring position 0 / MT_HALF): its generations in sequence from the one
+// before it — the other half's generation 7, the twist of its stored generation 6, or, with
+// seeded, the 624 words already in the half's last stored slot (init_mt) — its even
+// generations' words and, with mc, all its codes (per-lane form of tg_twist.h twist_chain).
+// The half's 4 stored slots are the work space: slot 3 holds the source until generation 5,
+// each odd generation goes to the next slot and becomes the even one after it in place;
+// generation 7 (codes only) is twisted in place over generation 6, which is then made again
+// from generation 4 (two extra twists on this rare per-lane path, no other scratch).
+// (Ops: the whole-generation loops, inline here; tg_amd.hip's regen_half calls them out of line
+// so that k_run's register allocation does not grow around its rare call)
+struct GenOps {
+  TG_HD void twist(const uint32_t* src, uint32_t* dst) const { twist_gen(src, dst); }
+  TG_HD void codes(const uint32_t* w, uint8_t* c) const { gen_codes(w, c); }
+};
+template <class Ops = GenOps>
+TG_HD void twist_half(uint32_t* mt, uint32_t h, uint8_t* mc = nullptr, bool seeded = false,
+                      const Ops& op = Ops()) {
+  const uint32_t g0 = h / (uint32_t)MT_N;  // ring generation of the half's first (0 / 8)
+  uint32_t* const s = mt + mt_store_off(g0);
+  uint32_t* const s3 = s + 3 * MT_N;
+  if (!seeded) op.twist(mt + mt_store_off((g0 + (uint32_t)MT_HALF_GENS + 6u) % (2u * MT_HALF_GENS)), s3);
+  uint8_t* const c = mc ? mc + h / 2 : nullptr;
+  // generation g: 0 from slot 3 into slot 0; odd 2k + 1 from slot k into slot k + 1; even
+  // 2k + 2 in place in slot k + 1; 7 (codes only) in place in slot 3
+  const int last = c ? MT_HALF_GENS : MT_HALF_GENS - 1;
+  for (int g = 0; g < last; ++g) {
+    const int to = (g + 1) >> 1 < 3 ? (g + 1) >> 1 : 3;
+    const uint32_t* const from = g == 0 ? s3 : (g & 1) ? s + (g >> 1) * MT_N : s + to * MT_N;
+    op.twist(from, s + to * MT_N);
+    if (c) op.codes(s + to * MT_N, c + g * (MT_N / 2));
+  }
+  if (c) {  // generation 6 again, from 4 through 5
+    op.twist(s + 2 * MT_N, s3);
+    op.twist(s3, s3);
   }
 }
 
@@ -279,7 +360,7 @@ TG_HD int walk_ticks(R& rng, int& x, int lim, int cap) {
 
 // Direct-load consumer (few draws per launch: create/reset/classify, and the host checks).
 struct Rng {
-  uint32_t* mt;    // this env's MT_WORDS words
+  uint32_t* mt;    // this env's MT_STORE stored words (the ring's even generations)
   uint32_t pos;    // [0, MT_WORDS), even
   uint32_t draws;  // random() calls (instrumentation for the roofline)
   bool crossed;    // the half not holding pos is stale (MT_STALE on entry, or entered one)
@@ -291,7 +372,8 @@ struct Rng {
         entered(false), mc(c) {}
 
   TG_HD double random() {
-    const uint32_t w0 = mt[pos], w1 = mt[pos + 1];
+    uint32_t w0, w1;
+    mt_pair(mt, pos, w0, w1);
     pos += 2;
     if (pos == (uint32_t)MT_WORDS) pos = 0u;
     if (pos == 0u || pos == (uint32_t)MT_HALF) {
@@ -359,11 +441,13 @@ TG_HD void seed_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed)
   mt[0] = 0x80000000u;
 }
 // random.seed(seed) into an env's ring (per-lane form of tg_create: k_create + k_gen_twist):
-// the seeded words in the last generation's slot, then the ring's generations, pos 0
+// the seeded words (the state before the first twist) in half 0's last stored slot, then the
+// ring's generations from them, pos 0
+constexpr uint32_t MT_SEED_OFF = 3 * MT_N;  // mt_store_off(6)
 TG_HD void init_mt(uint32_t* mt, const uint32_t* genrand19650218, uint64_t seed,
                    uint8_t* mc = nullptr) {
-  seed_mt(mt + MT_WORDS - MT_N, genrand19650218, seed);
-  twist_half(mt, 0u, mc);
+  seed_mt(mt + MT_SEED_OFF, genrand19650218, seed);
+  twist_half(mt, 0u, mc, true);
   twist_half(mt, (uint32_t)MT_HALF, mc);
 }
 

@@ -1,6 +1,7 @@
 // tg_twist.h — whole-wavefront MT19937 regeneration (device only): a half of the ring
 // (MT_HALF_GENS generations, tg_core.h) twisted by the 64 lanes of one wave, the generations
-// chained in the wave's LDS scratch, every generation's 624 words and 312 draw codes stored.
+// chained in the wave's LDS scratch, every generation's 312 draw codes and the even
+// generations' 624 words stored (tg_core.h MT_STORE).
 // Used by k_regen (the deferred regeneration, every 16 compact steps), k_gen_twist (tg_create,
 // tg_write_state), k_reset and k_step (tg_amd.hip), and timed in isolation by
 // scripts/calib/regen_bench.hip, which includes this header.
@@ -78,7 +79,8 @@ __device__ __forceinline__ void twist_load(const glb_u32* src, TwistIn& t) {
 // p - 227 written by rounds r - 4 and r - 3 only, so a group needs nothing from itself, and its
 // reads issue together (4 LDS round trips per generation instead of 10).
 constexpr int TWIST_GROUP = 3;
-// the generation after the one in t (registers), into scratch (LDS) and dst (HBM), then its codes
+// the generation after the one in t (registers), into scratch (LDS) and, unless null, dst
+// (HBM), then, unless dst_c is null, its codes (dst / dst_c wave-uniform)
 __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint8_t* dst_c,
                                             lds_u32* scratch) {
   const int lane = threadIdx.x & 63;
@@ -92,7 +94,7 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
         const uint32_t cc = p < MT_N - MT_M ? t.c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
         const uint32_t w = twist_word(t.a[r], bb, cc);
         scratch[p] = w;
-        dst[p] = w;
+        if (dst) dst[p] = w;
       }
     }
     // the group visible to later groups, whose lanes read what other lanes wrote: a
@@ -101,14 +103,14 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
     // s_waitcnt lgkmcnt(0) after every round: 0.1322 vs 0.1340 ms)
     wave_fence();
   }
-  codes_from_lds(scratch, dst_c);
+  if (dst_c) codes_from_lds(scratch, dst_c);
 }
 // The next generation in place in LDS (s: a generation -> its successor), stored to dst with
 // its codes.  Round r reads words p + 1 (old: round r + 1 writes it, for lane 63), p + 397
 // (old for p < 227: rounds >= 6 write them) or p - 227 (new: rounds r - 4 / r - 3), then
 // writes p.  A group's reads are all issued before its writes (the compiler barrier: one
 // wave's LDS operations execute in order), so round r + 1's write cannot overtake round r's
-// read of word 64 (r + 1).  Must be reached by all 64 lanes.
+// read of word 64 (r + 1).  dst / dst_c as twist_store.  Must be reached by all 64 lanes.
 __device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst_c) {
   const int lane = threadIdx.x & 63;
   wave_fence();  // the previous codes pass's reads of s before this twist's writes
@@ -131,27 +133,37 @@ __device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst
       const int p = r * 64 + lane;
       if (p < MT_N) {
         s[p] = w[r - r0];
-        dst[p] = w[r - r0];
+        if (dst) dst[p] = w[r - r0];
       }
     }
     wave_fence();
   }
-  codes_from_lds(s, dst_c);
+  if (dst_c) codes_from_lds(s, dst_c);
 }
-// `gens` generations in sequence after the one in t into dst, dst + MT_N, ... (words) and dst_c,
-// dst_c + MT_N / 2, ... (codes): the first twisted from registers, the rest chained in the wave's
-// LDS scratch, so a half's regeneration reads one generation from HBM.  dst / dst_c are
-// wave-uniform; must be reached by all 64 lanes.
-__device__ __forceinline__ void twist_chain(const TwistIn& t, glb_u32* dst, uint8_t* dst_c, int gens,
-                                            lds_u32* scratch) {
-  twist_store(t, dst, dst_c, scratch);
-  for (int g = 1; g < gens; ++g) twist_lds(scratch, dst + g * MT_N, dst_c + g * (MT_N / 2));
+// `gens` generations in sequence after the one in t, ring generations g0, g0 + 1, ... of an env
+// whose stored words start at w and codes at c: each one's codes, and the words of the even
+// ones (tg_core.h mt_store_off).  With lead, one twist leads in first (t holds a stored
+// generation 6; its successor, the other half's generation 7, is the chain's source: neither
+// stored nor coded).  The first twist from registers, the rest chained in the wave's LDS
+// scratch, so a half's regeneration reads one generation from HBM.  w / c wave-uniform; must
+// be reached by all 64 lanes.
+__device__ __forceinline__ void twist_chain(const TwistIn& t, glb_u32* w, uint8_t* c, int g0, int gens,
+                                            bool lead, lds_u32* scratch) {
+  auto wd = [&](int g) { return (g & 1) ? (glb_u32*)nullptr : w + mt_store_off((uint32_t)g); };
+  if (lead) twist_store(t, nullptr, nullptr, scratch);
+  else twist_store(t, wd(g0), c + g0 * (MT_N / 2), scratch);
+  for (int j = lead ? 0 : 1; j < gens; ++j) twist_lds(scratch, wd(g0 + j), c + (g0 + j) * (MT_N / 2));
 }
-__device__ __forceinline__ void wave_twist_gens(const glb_u32* src, glb_u32* dst, uint8_t* dst_c,
-                                                int gens, lds_u32* scratch) {
+__device__ __forceinline__ void wave_twist_gens(const glb_u32* src, glb_u32* w, uint8_t* c, int g0,
+                                                int gens, bool lead, lds_u32* scratch) {
   TwistIn t;
   twist_load(src, t);
-  twist_chain(t, dst, dst_c, gens, scratch);
+  twist_chain(t, w, c, g0, gens, lead, scratch);
+}
+// stored word offset of the source of half dst's regeneration (dst: ring position 0 / MT_HALF):
+// the other half's stored generation 6, whose twist (the lead-in) is that half's generation 7
+__device__ __forceinline__ uint32_t regen_src_off(uint32_t dst) {
+  return mt_store_off(((uint32_t)MT_HALF - dst) / (uint32_t)MT_N + (uint32_t)MT_HALF_GENS - 2u);
 }
 
 }  // namespace tg

@@ -240,6 +240,11 @@ int tg_stats_reset(tg_batch *h);
 #define TG_KERNEL_REGEN 2    /* k_regen */
 int tg_kernel_info(tg_batch *h, int kernel, int32_t *blocks_per_cu, int32_t *vgprs, int32_t *sgprs,
                    int32_t *lds_bytes);
+/* Per-env MT19937 storage of this build (no reference counterpart; for sizing and for the
+ * measurement's byte counts): ring_words = the word positions of the ring of pre-twisted
+ * generations, stored_words = the words kept in HBM (the even generations), code_bytes = one
+ * draw code per random() of the ring.  Any pointer may be NULL. */
+int tg_mt_layout(int32_t *ring_words, int32_t *stored_words, int32_t *code_bytes);
 
 /* Raw SoA state copy-out for checkpoints and tests (host buffers, synchronises; the MT
  * generations are gathered on the device and copied out in chunks of 64 Ki envs):
