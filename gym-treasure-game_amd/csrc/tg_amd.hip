@@ -103,13 +103,12 @@ __device__ __forceinline__ void stage_level(LdsLevel& lv, const uint32_t* __rest
   stage_level(lv, grid, L);              \
   const uint32_t* const trig = lv.trig;  \
   const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H}
-// k_run's LDS beyond its few static words: the waves' code windows (WIN_WAVE_BYTES each, at
-// offset 0: 16-B aligned for the LDS-DMA), then the level's grid words and bitmasks (Map::mk),
-// sized for the handle's level at launch instead of for the largest level (MAX_CELLS + 25 *
-// MK_DIM words: 5.5 KB against ~2 KB for the default level), so that a 64-thread workgroup
-// still fits 5 waves per SIMD
+// k_run's LDS: the waves' code windows (WIN_WAVE_BYTES each, at offset 0: 16-B aligned for the
+// LDS-DMA), then the level's grid words and bitmasks (Map::mk).  (Sized at launch for the
+// handle's level instead of the largest, with the rows' loads issued before the staging
+// barrier, it measured ~4 % slower for the masked policy: DESIGN.md §3.1.)
 #define RUN_LEVEL_IN_LDS()                                                                \
-  extern __shared__ uint4 run_lds[];                                                      \
+  __shared__ uint4 run_lds[((RUN_BLOCK / 64) * WIN_WAVE_BYTES + MAX_CELLS + 4 * MK_MAX_WORDS) / 16]; \
   __shared__ uint32_t ltrig[12];                                                          \
   uint8_t* const win = reinterpret_cast<uint8_t*>(run_lds);                                \
   uint32_t* const lgrid = reinterpret_cast<uint32_t*>(win + (RUN_BLOCK / 64) * WIN_WAVE_BYTES); \
@@ -161,11 +160,6 @@ constexpr int WIN_WAVE_BYTES = WIN_SLOTS * WIN_SLOT_BYTES;  // 4 KB per wave
 constexpr int WAVE_SCRATCH = MT_N * 4;                       // wave_twist's scratch (aliases it)
 static_assert(WIN_WAVE_BYTES >= WAVE_SCRATCH, "wave_refill reuses the window as scratch");
 static_assert(WIN_DRAWS - WIN_UNIT + 1 >= (int)MAX_TICK_DRAWS, "a refilled window holds a tick's draws");
-// k_run's dynamic LDS for a level (RUN_LEVEL_IN_LDS)
-TG_HD size_t run_lds_bytes(int W, int H, bool masks) {
-  return (size_t)(RUN_BLOCK / 64) * WIN_WAVE_BYTES +
-         4 * (size_t)(grid_words(W, H) + (masks ? mk_words(W, H) : 0));
-}
 
 // LDS-DMA of one WIN_UNIT-byte unit per active lane into LDS [m0 + lane * WIN_UNIT]; M0 is
 // saved/restored
@@ -991,7 +985,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     ostart[O_COUNT] = acc;
     oraw[O_COUNT] = pre[NSEG];
   }
-  __syncthreads();  // ostart / oraw
+  RUN_LEVEL_IN_LDS();  // includes the barrier (ostart / oraw)
   const int total = ostart[O_COUNT];
   const int base = (blockIdx.x * RUN_BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
   int oj = 0;  // ostart[oj] <= base < ostart[oj + 1] (wave-uniform)
@@ -1010,19 +1004,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     }
   }
   const int idx = qraw - pre[seg];
-  // the chunk's rows, loaded before the level staging so that their latency overlaps it
   int64_t i = 0;
-  uint4 s4w = make_uint4(0u, 0u, 0u, 0u);
-  double2 a2w = make_double2(0.0, 0.0);
-  int2 epw = make_int2(0, 0);
-  if (live) {
-    const int64_t at = (int64_t)seg * w.shard_cap + idx;
-    i = w.lists[at];
-    s4w = w.wst4[at];
-    a2w = w.wang[at];
-    epw = w.wep[at];
-  }
-  RUN_LEVEL_IN_LDS();  // includes the barrier
   StepResult r{0, 0, 0, 0};
   Env e;
   e.mti = 0u;
@@ -1042,8 +1024,10 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   uint32_t prounds = 0;
 #endif
   if (live) {
-    unpack(s4w, a2w, e);
-    ep = epw;
+    const int64_t at = (int64_t)seg * w.shard_cap + idx;
+    i = w.lists[at];
+    unpack(w.wst4[at], w.wang[at], e);
+    ep = w.wep[at];
     RngCodes rng(S.mt + i * MT_STORE, S.mc + i * MT_CODES, e.mti, wscr);
     rng.prime();  // issue the code loads now; the first draw comes after the policy setup
     TG_STAMP(t1);
@@ -1785,9 +1769,8 @@ int launch_step(tg_batch* h, StepCtx& c, const StepIO& io_in, bool ar, hipStream
                        ks0);
     HIP_TRY(hipGetLastError());
     if (mid) HIP_TRY(hipEventRecord(mid, st));  // (tg_rollout's stagger between groups)
-    hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n) * (BLOCK / RUN_BLOCK)), dim3(RUN_BLOCK),
-                       run_lds_bytes(h->L.W, h->L.H, h->L.masks != nullptr), st, S, c.n, h->L,
-                       h->grid, io, q, w,
+    hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n) * (BLOCK / RUN_BLOCK)), dim3(RUN_BLOCK), 0, st, S,
+                       c.n, h->L, h->grid, io, q, w,
                        g0, c.stats, h->err, ks1);
   }
   HIP_TRY(hipGetLastError());
@@ -2182,13 +2165,12 @@ int tg_kernel_info(tg_batch* h, int kernel, int32_t* blocks_per_cu, int32_t* vgp
   hipFuncAttributes fa;
   HIP_TRY(hipFuncGetAttributes(&fa, k));
   int nb = 0;
-  const bool run = kernel == TG_KERNEL_RUN;
-  const size_t dyn = run ? run_lds_bytes(h->L.W, h->L.H, h->L.masks != nullptr) : 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, run ? RUN_BLOCK : BLOCK, dyn));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kernel == TG_KERNEL_RUN ? RUN_BLOCK : BLOCK,
+                                                       0));
   if (blocks_per_cu) *blocks_per_cu = nb;
   if (vgprs) *vgprs = fa.numRegs;
   if (sgprs) *sgprs = -1;  // not reported by hipFuncGetAttributes
-  if (lds_bytes) *lds_bytes = (int32_t)(fa.sharedSizeBytes + dyn);
+  if (lds_bytes) *lds_bytes = (int32_t)fa.sharedSizeBytes;
   return TG_OK;
 }
 
