@@ -28,6 +28,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MT_HALF_GENS = 8  # tg_core.h: generations per half of an env's MT ring
+REGEN_STEPS = 16  # tg_amd.hip: steps per k_regen launch
 
 
 def short(name):
@@ -53,6 +54,14 @@ def bench_line(path):
     return json.loads(lines[-1]) if lines else None
 
 
+def last_of(k, last):
+    """dispatches of kernel k in the timed region: the last `last` of a step kernel, the last
+    last / REGEN_STEPS of k_regen (one launch per 16 steps; the profile runs 160 steps)"""
+    if not last:
+        return None
+    return max(last // REGEN_STEPS, 1) if k.startswith("k_regen") else last
+
+
 def counters(path, last=None):
     per = defaultdict(lambda: defaultdict(list))
     meta = {}
@@ -63,9 +72,29 @@ def counters(path, last=None):
             meta[k] = {"grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),
                        "sgpr": int(r["SGPR_Count"]), "lds": int(r["LDS_Block_Size"])}
     # the timed steps are the last dispatches of each step kernel
-    avg = {k: {c: sum(v[-last:] if last else v) / len(v[-last:] if last else v)
-               for c, v in d.items()} for k, d in per.items()}
+    avg = {}
+    for k, d in per.items():
+        n = last_of(k, last)
+        avg[k] = {c: sum(v[-n:] if n else v) / len(v[-n:] if n else v) for c, v in d.items()}
     return avg, meta
+
+
+def timed_durations(path, last):
+    """average duration (ns) of each kernel's timed dispatches in a kernel-trace CSV"""
+    per = defaultdict(list)
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            per[short(r["Kernel_Name"])].append(
+                (int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    out = {}
+    for k, v in per.items():
+        v.sort()
+        n = last_of(k, last)
+        sel = [d for _, d in (v[-n:] if n else v)]
+        out[k] = {"timed_dispatches": len(sel), "avg_ns": sum(sel) / len(sel)}
+    return out
 
 
 def main():
@@ -88,10 +117,16 @@ def main():
     res["kernel_trace"] = ks
     pm = {}
     meta = {}
-    prof_line = bench_line(os.path.join(a.out, "pmc_fetch_%s.log" % a.policy))
-    if prof_line is None:
-        prof_line = bench_line(os.path.join(a.out, "pmc_fetch.log"))
+    prof_line = None
+    for name in ("pmc_fetch_%s.log" % a.tag, "pmc_fetch_%s.log" % a.policy, "pmc_fetch.log"):
+        prof_line = prof_line or bench_line(os.path.join(a.out, name))
     last = prof_line["steps"] if prof_line else None
+    # the kernels' durations in the timed region of the trace run (same workload)
+    td = timed_durations(os.path.join(a.out, "trace_" + a.tag, "run_kernel_trace.csv"), last)
+    for k, v in td.items():
+        if k in ks:
+            ks[k]["timed_avg_ns"] = v["avg_ns"]
+            ks[k]["timed_dispatches"] = v["timed_dispatches"]
     for p in ("fetch", "write", "sq1", "sq2", "regen_fetch", "regen_write", "regen_sq1", "regen_sq2"):
         path = os.path.join(a.out, "pmc_%s_%s" % (p, a.tag), "run_counter_collection.csv")
         if os.path.exists(path):
@@ -127,12 +162,22 @@ def main():
                 coal = 44.0 * a.envs + 2496.0 / MT_HALF_GENS * regens
             scat = max(fr - coal / 2.0, 0.0)
             rd = coal + scat
-            kn = ks.get(k, {}).get("avg_ns")
+            kn = ks.get(k, {}).get("timed_avg_ns") or ks.get(k, {}).get("avg_ns")
             cyc = pm[k].get("SQ_WAVE_CYCLES")
             ent = {"fetch_bytes_raw": fr, "coalesced_read_bytes": coal,
                    "scattered_read_bytes": scat, "read_bytes": rd, "write_bytes": wr,
                    "hbm_bytes": rd + wr, "fetch_bytes_kerrors_factor": fr * (cal or 1.0),
                    "avg_ns": kn}
+            if base == "k_regen" and regens:
+                # per MT generation regenerated (a full launch: REGEN_STEPS steps' lists)
+                gens = regens * spl
+                alg = (((prof_line or {}).get("roofline", {}).get("step", {}).get("kernels", {})
+                        .get("regen", {})).get("alg_bytes_per_generation"))
+                ent.update({"generations_per_launch": gens, "write_bytes_per_generation": wr / gens,
+                            "read_bytes_per_generation": rd / gens,
+                            "hbm_bytes_per_generation": (rd + wr) / gens,
+                            "alg_bytes_per_generation": alg,
+                            "ns_per_generation": kn / gens if kn else None})
             if kn:
                 ent["hbm_gbs"] = (rd + wr) / kn
                 v = pm[k].get("SQ_INSTS_VALU")
