@@ -377,12 +377,22 @@ class Runner:
         return ctypes.c_void_p(t.data_ptr())
 
     def drain(self, log=True):
+        """one drain of the device queue, gathered to rank 0's log: written in place into the
+        log's next slot (one launch at one rank, the drain and the all-gather beyond)"""
         chk, L, p = self.tg._lib.check, self.L, self.p
+        if log and self.world == 1:
+            rows, cnt = self.log.target()
+            chk(L.tg_episodes(self.h, p(rows), p(cnt), self.ep_cap, self.stream), "episodes")
+            self.log.commit()
+            return cnt
         chk(L.tg_episodes(self.h, p(self.ep_rows), p(self.ep_cnt), self.ep_cap, self.stream),
             "episodes")
-        rows, cnt = self.D.gather_padded(self.ep_rows, self.ep_cnt, self.all_rows, self.all_cnt)
         if log:
-            self.log.add(rows, cnt)
+            rows, cnt = self.log.target()
+            self.D.gather_padded(self.ep_rows, self.ep_cnt, rows, cnt)
+            self.log.commit()
+            return cnt
+        _, cnt = self.D.gather_padded(self.ep_rows, self.ep_cnt, self.all_rows, self.all_cnt)
         return cnt
 
     def drain_all(self, log):

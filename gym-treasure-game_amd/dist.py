@@ -122,16 +122,31 @@ class EpisodeLog:
         self.records = torch.zeros(1, dtype=torch.int64, device=device)
         self.used = 0
 
-    def add(self, all_rows, all_count):
-        self.records.add_(all_count.sum())
+    def target(self):
+        """``(rows [world*cap, 2], counts [world])``: the next drain's slot, for the drain
+        (``tg_episodes``) or the all-gather to write in place, then ``commit()``: one launch
+        per drain instead of a drain, its gather and two copies (the bench)."""
         if not self.keep:
-            return
+            return self.rows[0], self.counts[0]
         if self.used >= self.rows.size(0):  # more drains than sized for: grow (allocates)
             self.rows = torch.cat([self.rows, torch.zeros_like(self.rows)])
             self.counts = torch.cat([self.counts, torch.zeros_like(self.counts)])
-        self.rows[self.used].copy_(all_rows, non_blocking=True)
-        self.counts[self.used].copy_(all_count, non_blocking=True)
-        self.used += 1
+        return self.rows[self.used], self.counts[self.used]
+
+    def commit(self):
+        """the slot from ``target()`` now holds a drain"""
+        if self.keep:
+            self.used += 1
+        else:  # one reused slot: its count is added up at once
+            self.records.add_(self.counts[0].sum())
+
+    def add(self, all_rows, all_count):
+        """a drain gathered elsewhere, copied into the next slot"""
+        rows, counts = self.target()
+        if self.keep or rows.data_ptr() != all_rows.data_ptr():
+            rows.copy_(all_rows, non_blocking=True)
+            counts.copy_(all_count, non_blocking=True)
+        self.commit()
 
     def reset(self):
         self.records.zero_()
