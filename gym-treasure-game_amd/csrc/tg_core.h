@@ -194,20 +194,20 @@ TG_HD void twist_gen(const uint32_t* src, uint32_t* dst) {
 // before it, so src == dst is CPython's own in-place loop
 TG_HD void twist_gen_inplace(uint32_t* w) { twist_gen(w, w); }
 // Word i (< 623) of the generation after g, from g's words alone: new word i reads new word
-// i - 227 for i >= 227 (twist_gen), so it is a chain of at most 3 twist words back to an i < 227.
+// i - 227 for i >= 227 (twist_gen), so it is a chain of d = i / 227 (0-2) twist words on top of
+// new word j0 = i - 227 d (< 227, which reads old words only).  The chain's old words are at
+// fixed offsets from j0, so all of them load at once (one memory round trip on the rare draws
+// that need an odd generation's double), then the chain computes.
 TG_HD uint32_t twist_at_lo(const uint32_t* g, int i) {
   constexpr int K = MT_N - MT_M;  // 227
-  int j = i;
-  int hops = 0;
-  while (j >= K) {
-    j -= K;
-    ++hops;
-  }
-  uint32_t w = mt_twist(g[j], g[j + 1], g[j + MT_M]);
-  while (hops-- > 0) {
-    j += K;
-    w = mt_twist(g[j], g[j + 1], w);
-  }
+  const int d = i >= 2 * K ? 2 : i >= K ? 1 : 0;
+  const int j0 = i - K * d;
+  const uint32_t a0 = g[j0], b0 = g[j0 + 1], c0 = g[j0 + MT_M];
+  const uint32_t a1 = d >= 1 ? g[j0 + K] : 0u, b1 = d >= 1 ? g[j0 + K + 1] : 0u;
+  const uint32_t a2 = d >= 2 ? g[j0 + 2 * K] : 0u, b2 = d >= 2 ? g[j0 + 2 * K + 1] : 0u;
+  uint32_t w = mt_twist(a0, b0, c0);
+  if (d >= 1) w = mt_twist(a1, b1, w);
+  if (d >= 2) w = mt_twist(a2, b2, w);
   return w;
 }
 // word i of the generation after g (word 623 reads new words 0 and 396)
