@@ -185,12 +185,6 @@ struct GenCalls {
   __device__ void twist(const uint32_t* src, uint32_t* dst) const { twist_gen_call(src, dst); }
   __device__ void codes(const uint32_t* w, uint8_t* c) const { gen_codes_call(w, c); }
 };
-// a double's two words (RngCodes::random), out of line for the same reason
-__device__ __noinline__ uint2 mt_pair_call(const uint32_t* mt, uint32_t p) {
-  uint2 w;
-  mt_pair(mt, p, w.x, w.y);
-  return w;
-}
 __device__ __noinline__ void regen_half(uint32_t* mt, uint8_t* mc, uint32_t h) {
   twist_half(mt, h, mc, false, GenCalls());
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
@@ -362,8 +356,8 @@ struct RngCodes {
     uint32_t p = (pos >> 1) + n;
     p = 2u * (p >= (uint32_t)MT_CODES ? p - (uint32_t)MT_CODES : p);
     (void)code();
-    const uint2 w = mt_pair_call(mt, p);
-    return mt_double(w.x, w.y);
+    const WordPair w = mt_pair_ool(mt, p);
+    return mt_double(w.w0, w.w1);
   }
   __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
   // drain the DMAs (the window is reused as scratch); returns the state word to store: the

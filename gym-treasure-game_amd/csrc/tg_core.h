@@ -196,44 +196,68 @@ TG_HD void twist_gen_inplace(uint32_t* w) { twist_gen(w, w); }
 // Word i (< 623) of the generation after g, from g's words alone: new word i reads new word
 // i - 227 for i >= 227 (twist_gen), so it is a chain of d = i / 227 (0-2) twist words on top of
 // new word j0 = i - 227 d (< 227, which reads old words only).  The chain's old words are at
-// fixed offsets from j0, so all of them load at once (one memory round trip on the rare draws
-// that need an odd generation's double), then the chain computes.
+// fixed offsets from j0 and all load unconditionally (indices clamped into the generation):
+// one memory round trip, and no divergence between lanes of different chain lengths.
 TG_HD uint32_t twist_at_lo(const uint32_t* g, int i) {
   constexpr int K = MT_N - MT_M;  // 227
   const int d = i >= 2 * K ? 2 : i >= K ? 1 : 0;
   const int j0 = i - K * d;
+  const int c2 = j0 + 2 * K < MT_N - 1 ? j0 + 2 * K : MT_N - 2;
   const uint32_t a0 = g[j0], b0 = g[j0 + 1], c0 = g[j0 + MT_M];
-  const uint32_t a1 = d >= 1 ? g[j0 + K] : 0u, b1 = d >= 1 ? g[j0 + K + 1] : 0u;
-  const uint32_t a2 = d >= 2 ? g[j0 + 2 * K] : 0u, b2 = d >= 2 ? g[j0 + 2 * K + 1] : 0u;
+  const uint32_t a1 = g[j0 + K], b1 = g[j0 + K + 1];
+  const uint32_t a2 = g[c2], b2 = g[c2 + 1];
   uint32_t w = mt_twist(a0, b0, c0);
-  if (d >= 1) w = mt_twist(a1, b1, w);
-  if (d >= 2) w = mt_twist(a2, b2, w);
-  return w;
+  const uint32_t w1 = mt_twist(a1, b1, w);
+  w = d >= 1 ? w1 : w;
+  const uint32_t w2 = mt_twist(a2, b2, w);
+  return d >= 2 ? w2 : w;
 }
 // word i of the generation after g (word 623 reads new words 0 and 396)
 TG_HD uint32_t twist_at(const uint32_t* g, int i) {
   return i < MT_N - 1 ? twist_at_lo(g, i)
                       : mt_twist(g[MT_N - 1], twist_at_lo(g, 0), twist_at_lo(g, MT_M - 1));
 }
-// the two words at ring position p (even) from the stored generations: an even generation's
-// are stored, an odd one's are twisted from the generation before it (rare: the draws that
-// need their double)
-TG_HD void mt_pair_odd(const uint32_t* mt, uint32_t g, uint32_t i, uint32_t* w) {
-  const uint32_t* const prev = mt + mt_store_off(g - 1u);
-  w[0] = twist_at(prev, (int)i);
-  w[1] = twist_at(prev, (int)i + 1);
-}
+// The two words at ring position p (even) from the stored generations: an even generation's
+// are stored, an odd one's are twisted from the generation before it (the rare draws that need
+// their double).  Branch-free: every lane issues the loads of both cases (~20 words) at once,
+// so a wave whose lanes sit in even and odd generations pays one memory round trip, not two.
 TG_HD void mt_pair(const uint32_t* mt, uint32_t p, uint32_t& w0, uint32_t& w1) {
+  const uint32_t g = p / (uint32_t)MT_N, i = p - g * (uint32_t)MT_N;  // i even, <= 622
+  const uint32_t* const cur = mt + mt_store_off(g & ~1u);  // g's own words if g is even
+  const uint32_t* const prev = mt + mt_store_off(g == 0u ? 0u : (g - 1u) & ~1u);
+  const uint32_t e0 = cur[i], e1 = cur[i + 1];
+  const uint32_t o0 = twist_at_lo(prev, (int)i);
+  // word i + 1: a chain of its own, or, for i + 1 = 623, the twist of old word 623 with new
+  // words 0 and 396
+  const bool last = i + 1u == (uint32_t)MT_N - 1u;
+  const uint32_t x = twist_at_lo(prev, last ? MT_M - 1 : (int)i + 1);
+  const uint32_t y0 = twist_at_lo(prev, 0);
+  const uint32_t o1 = last ? mt_twist(prev[MT_N - 1], y0, x) : x;
+  w0 = (g & 1u) ? o0 : e0;
+  w1 = (g & 1u) ? o1 : e1;
+}
+// the same with a branch (few registers, inline: tg::Rng, whose draws of doubles in the step
+// kernels are resets of envs whose option did not run, rarer still)
+TG_HD void mt_pair_branchy(const uint32_t* mt, uint32_t p, uint32_t& w0, uint32_t& w1) {
   const uint32_t g = p / (uint32_t)MT_N, i = p - g * (uint32_t)MT_N;
   if (g & 1u) {
-    uint32_t w[2];
-    mt_pair_odd(mt, g, i, w);
-    w0 = w[0];
-    w1 = w[1];
+    const uint32_t* const prev = mt + mt_store_off(g - 1u);
+    w0 = twist_at(prev, (int)i);
+    w1 = twist_at(prev, (int)i + 1);
   } else {
     w0 = mt[mt_store_off(g) + i];
     w1 = mt[mt_store_off(g) + i + 1];
   }
+}
+// mt_pair out of line (RngCodes, the option loops' draws: its loads and chains would
+// otherwise add ~30 VGPRs to k_run's allocation)
+struct WordPair {
+  uint32_t w0, w1;
+};
+__host__ __device__ inline __attribute__((noinline)) WordPair mt_pair_ool(const uint32_t* mt, uint32_t p) {
+  WordPair r;
+  mt_pair(mt, p, r.w0, r.w1);
+  return r;
 }
 // word offset of the half holding word position pos
 TG_HD uint32_t mt_half(uint32_t pos) { return pos >= (uint32_t)MT_HALF ? (uint32_t)MT_HALF : 0u; }
@@ -373,7 +397,7 @@ struct Rng {
 
   TG_HD double random() {
     uint32_t w0, w1;
-    mt_pair(mt, pos, w0, w1);
+    mt_pair_branchy(mt, pos, w0, w1);
     pos += 2;
     if (pos == (uint32_t)MT_WORDS) pos = 0u;
     if (pos == 0u || pos == (uint32_t)MT_HALF) {

@@ -184,6 +184,29 @@ int64_t hc_check_code_top27(int64_t* slow) {
   return bad;
 }
 
+// mt_pair (branch-free, RngCodes on the device), mt_pair_branchy (tg::Rng) and the plain
+// twist against each other and against full generations: a seeded ring, every even position
+// of all 16 generations.  Returns the mismatches.
+int64_t hc_check_mt_pair(uint64_t seed) {
+  uint32_t gen[MT_N];
+  gen[0] = 19650218u;
+  for (int i = 1; i < MT_N; ++i) gen[i] = 1812433253u * (gen[i - 1] ^ (gen[i - 1] >> 30)) + (uint32_t)i;
+  std::vector<uint32_t> mt(MT_STORE), full((size_t)(2 * MT_HALF_GENS + 1) * MT_N);
+  init_mt(mt.data(), gen, seed);
+  seed_mt(full.data(), gen, seed);  // generation -1, then 16 twists: the ring's generations
+  for (int g = 0; g < 2 * MT_HALF_GENS; ++g) twist_gen(&full[(size_t)g * MT_N], &full[(size_t)(g + 1) * MT_N]);
+  int64_t bad = 0;
+  for (uint32_t p = 0; p < (uint32_t)MT_WORDS; p += 2) {
+    uint32_t a0, a1, b0, b1;
+    mt_pair(mt.data(), p, a0, a1);
+    mt_pair_branchy(mt.data(), p, b0, b1);
+    const WordPair c = mt_pair_ool(mt.data(), p);
+    const uint32_t f0 = full[MT_N + p], f1 = full[MT_N + p + 1];
+    bad += (a0 != f0) + (a1 != f1) + (b0 != f0) + (b1 != f1) + (c.w0 != f0) + (c.w1 != f1);
+  }
+  return bad;
+}
+
 // top27_code / top27_slow (the wave twist's code pass, tg_twist.h) against code_of_top27 for
 // every a: equal wherever top27_slow is false, and top27_slow covers every CODE_SLOW interval;
 // returns the mismatches and the number of slow intervals

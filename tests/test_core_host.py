@@ -197,6 +197,18 @@ def test_draw_code_from_the_top_27_bits(hostcheck):
     assert slow.value == 9
 
 
+@pytest.mark.parametrize("seed", [0, 7, 2**40 + 3])
+def test_odd_generation_words_equal_the_twist(hostcheck, seed):
+    """The ring stores its even generations only (tg_core.h MT_STORE): an odd generation's
+    word pairs, twisted from the stored generation before it — branch-free (mt_pair, the option
+    loops' doubles), with a branch (mt_pair_branchy, tg::Rng) and out of line (mt_pair_ool) —
+    equal CPython's generations (init_by_array, then plain twists) at every even position of
+    all 16 generations, including word 623 (new words 0 and 396)"""
+    hostcheck.hc_check_mt_pair.restype = ctypes.c_int64
+    hostcheck.hc_check_mt_pair.argtypes = [ctypes.c_uint64]
+    assert hostcheck.hc_check_mt_pair(seed) == 0
+
+
 def test_lean_draw_code_equals_top27(hostcheck):
     """top27_code / top27_slow (the wave twist's code pass, tg_twist.h: the class from a's top
     two bits plus one compare) equal code_of_top27 on every a they decide, and the slow set
