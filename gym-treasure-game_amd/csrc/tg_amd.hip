@@ -1104,6 +1104,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
 // default level (<= ~110 per step); a lane that gets there first regenerates the half itself.
 constexpr int REGEN_STEPS = 16;
 constexpr int REGEN_GRAB = 16;  // list regions a wave takes from its XCD's counter at a time
+static_assert(REGEN_GRAB <= 64, "a grab's region counts load one per lane");
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  const uint8_t* __restrict__ nrefill, int64_t n,
                                                  int slots, int32_t* __restrict__ ctr,
@@ -1130,35 +1131,41 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
   };
   int halves = 0;
   while (true) {
-  int64_t j0 = 0;
-  if (lane == 0) j0 = atomicAdd(q, REGEN_GRAB);
-  j0 = __builtin_amdgcn_readfirstlane((int)j0);
-  if (j0 >= nmine) break;
-  const int64_t j1 = j0 + REGEN_GRAB < nmine ? j0 + REGEN_GRAB : nmine;
-  for (int64_t j = j0; j < j1; ++j) {
-    const int64_t r = xcd + 8 * j;
-    const int64_t slot = r / nreg, rg = r - slot * nreg;
-    const int cnt = __builtin_amdgcn_readfirstlane((int)nrefill[slot * nreg + rg]);
-    if (!cnt) continue;
-    const uint32_t env_l = lane < cnt ? refill[(slot * nreg + rg) * 64 + lane] & 0x7FFFFFFFu : 0u;
-    const uint32_t st_l = lane < cnt ? st_w[(int64_t)env_l * 4 + 3] : 0u;
-    unsigned long long need = __ballot(lane < cnt && (st_l & MT_STALE));
-    if (!need) continue;
-    // one half at a time: 52 VGPRs, 8 waves per SIMD (the next half's source loads pipelined
-    // into this one's twist took 76 VGPRs, 6 waves, and measured no faster: DESIGN.md §3.3)
-    while (need) {
-      const int L = __ffsll((long long)need) - 1;
-      need &= need - 1;
-      const uint32_t env = __builtin_amdgcn_readlane(env_l, L), s = __builtin_amdgcn_readlane(st_l, L);
-      const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
-      TwistIn t;
-      twist_load(src_of(env, s), t);
-      twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_STORE), S.mc + (int64_t)env * MT_CODES,
-                  (int)(dst / (uint32_t)MT_N), MT_HALF_GENS, true, scr);
-      if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
-      ++halves;
+    int64_t j0 = 0;
+    if (lane == 0) j0 = atomicAdd(q, REGEN_GRAB);
+    j0 = __builtin_amdgcn_readfirstlane((int)j0);
+    if (j0 >= nmine) break;
+    const int64_t j1 = j0 + REGEN_GRAB < nmine ? j0 + REGEN_GRAB : nmine;
+    // the grab's region counts in one load round, one lane each (region r = xcd + 8 j; its
+    // count at nrefill[r], its entries at refill[64 r ..]): most regions are empty (~0.2 halves
+    // per region at the uniform policy's rate), and reading the counts one by one made every
+    // grab a chain of dependent byte loads, ~120 us of each launch whatever its work
+    int cnt_l = 0;
+    if (lane < j1 - j0) cnt_l = nrefill[xcd + 8 * (j0 + lane)];
+    unsigned long long ne = __ballot(cnt_l != 0);
+    while (ne) {
+      const int jl = __ffsll((long long)ne) - 1;
+      ne &= ne - 1;
+      const int64_t r = xcd + 8 * (j0 + jl);
+      const int cnt = __builtin_amdgcn_readlane(cnt_l, jl);
+      const uint32_t env_l = lane < cnt ? refill[r * 64 + lane] & 0x7FFFFFFFu : 0u;
+      const uint32_t st_l = lane < cnt ? st_w[(int64_t)env_l * 4 + 3] : 0u;
+      unsigned long long need = __ballot(lane < cnt && (st_l & MT_STALE));
+      // one half at a time: 52 VGPRs, 8 waves per SIMD (the next half's source loads pipelined
+      // into this one's twist took 76 VGPRs, 6 waves, and measured no faster: DESIGN.md §3.3)
+      while (need) {
+        const int L = __ffsll((long long)need) - 1;
+        need &= need - 1;
+        const uint32_t env = __builtin_amdgcn_readlane(env_l, L), s = __builtin_amdgcn_readlane(st_l, L);
+        const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
+        TwistIn t;
+        twist_load(src_of(env, s), t);
+        twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_STORE), S.mc + (int64_t)env * MT_CODES,
+                    (int)(dst / (uint32_t)MT_N), MT_HALF_GENS, true, scr);
+        if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
+        ++halves;
+      }
     }
-  }
   }
   // the grid can exceed the stats slots (>= 8 workgroups, one per XCD counter, at small n)
   if (lane == 0 && halves)
