@@ -1130,10 +1130,21 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
     return (const glb_u32*)(S.mt + (int64_t)env * MT_STORE + regen_src_off(dst));
   };
   int halves = 0;
+  // the first grab is static (this wave's index among its XCD's waves), the rest come from the
+  // counter, which starts past the static ones: one atomic per wave fewer, and at a small
+  // launch (the end of a timed region drains a few steps' lists) no round of 1,024 atomics per
+  // counter before any work starts
+  const int wx = (int)(blockIdx.x >> 3) * (BLOCK / 64) + (int)(threadIdx.x >> 6);
+  const int64_t nwx = (int64_t)((gridDim.x - (unsigned)xcd + 7u) >> 3) * (BLOCK / 64);
+  bool first = true;
   while (true) {
-    int64_t j0 = 0;
-    if (lane == 0) j0 = atomicAdd(q, REGEN_GRAB);
-    j0 = __builtin_amdgcn_readfirstlane((int)j0);
+    int64_t j0 = (int64_t)wx * REGEN_GRAB;
+    if (!first) {
+      int g = 0;
+      if (lane == 0) g = atomicAdd(q, REGEN_GRAB);
+      j0 = nwx * REGEN_GRAB + __builtin_amdgcn_readfirstlane(g);
+    }
+    first = false;
     if (j0 >= nmine) break;
     const int64_t j1 = j0 + REGEN_GRAB < nmine ? j0 + REGEN_GRAB : nmine;
     // the grab's region counts in one load round, one lane each (region r = xcd + 8 j; its

@@ -22,6 +22,7 @@ namespace tg {
 typedef __attribute__((address_space(1))) uint32_t glb_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
 
 __device__ __forceinline__ void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -30,24 +31,21 @@ __device__ __forceinline__ void wave_fence() {
 }
 
 // ---- draw codes: one tempered word per draw (tg_core.h top27_code) --------------------------
-// draw_code of the draw whose words are w0, w1 (w1 is read only on the slow path)
-__device__ __forceinline__ uint32_t draw_code_lean(uint32_t w0, const lds_u32* w1p) {
-  const uint32_t a = mt_temper(w0) >> 5;
-  if (__builtin_expect(top27_slow(a), 0)) return draw_code(mt_double(w0, *w1p));
-  return top27_code(a);
-}
-
 // A generation's 312 draw codes from its words in LDS: draw d = r * 64 + lane per round, its
-// first word one LDS read (immediate offsets from one lane address), its code one byte of a
-// coalesced 64-B store.
+// two words one 8-B LDS read (consecutive lanes, consecutive 8 B: no bank conflict, where a
+// 4-B read of every other word conflicted 2-way), its code one byte of a coalesced 64-B store.
 __device__ __forceinline__ void codes_from_lds(const lds_u32* w, uint8_t* dst_c) {
   const int lane = threadIdx.x & 63;
-  const lds_u32* const wl = w + 2 * lane;
+  const lds_u64* const wl = reinterpret_cast<const lds_u64*>(w) + lane;
   uint8_t* const cl = dst_c + lane;
 #pragma unroll
   for (int r = 0; r < (MT_N / 2 + 63) / 64; ++r) {
-    if (r < MT_N / 2 / 64 || lane < MT_N / 2 - 64 * (MT_N / 2 / 64))
-      cl[64 * r] = (uint8_t)draw_code_lean(wl[128 * r], wl + 128 * r + 1);
+    if (r < MT_N / 2 / 64 || lane < MT_N / 2 - 64 * (MT_N / 2 / 64)) {
+      const uint64_t p = wl[64 * r];  // words 128 r + 2 lane (low) and + 1
+      const uint32_t w0 = (uint32_t)p, a = mt_temper(w0) >> 5;
+      cl[64 * r] = (uint8_t)(__builtin_expect(top27_slow(a), 0) ? draw_code(mt_double(w0, (uint32_t)(p >> 32)))
+                                                                  : top27_code(a));
+    }
   }
 }
 
