@@ -621,6 +621,15 @@ __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ part
 
 // finish one env-step: obs/reward/valid/done rows, episode counters, optional auto-reset.
 // keep != nullptr: the obs row is returned there instead of stored (the caller stores it).
+// The option waves' epilogue computes its obs rows by f64 division: the quotient table
+// (tg_core.h obs_div) is a global load on their tail, and by stamps the epilogue was ~4,000
+// cycles shorter without it (profiles/r04/stamps_divq_uniform_r04k.log); k_classify, whose
+// waves are not a tail, keeps the table
+__device__ __forceinline__ Level level_div(const Level& L) {
+  Level d = L;
+  d.obs_q = nullptr;
+  return d;
+}
 template <bool AUTORESET, bool FINAL, class R>
 __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int64_t i,
                                             const StepResult& r, int2& ep, const StepIO& io,
@@ -705,7 +714,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
       act = io.actions[i];
     }
     r = env_step(L, trig, m, e, act, rng);
-    finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
+    finish_step<AUTORESET, FINAL>(level_div(L), e, rng, i, r, ep, io);
     e.mti = rng.finish();
     draws = rng.draws;
     lregen = (int)rng.regens;
@@ -848,7 +857,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     if (stale)
       w.refill[wv * 64 + __popcll(b & ((1ull << lane) - 1ull))] =
           (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
-    if (lane == 0) w.nrefill[wv] = (uint8_t)__popcll(b);
+    if (lane == 0 && live) w.nrefill[wv] = (uint8_t)__popcll(b);  // (a wave past n has no region)
     if (stale) e.mti |= MT_LISTED;
   }
   // workgroup-local slots: one LDS atomic per wave and option present in the wave (the
@@ -1032,7 +1041,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     ph1 = rng.ph[1], ph2 = rng.ph[2], ph3 = rng.ph[3], prounds = rng.rounds;
 #endif
     r.done = is_done(e);
-    finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io);
+    finish_step<AUTORESET, FINAL>(level_div(L), e, rng, i, r, ep, io);
     e.mti = rng.finish();  // a half left here: MT_STALE, listed by the next k_classify
     draws = rng.draws;
     lregen = (int)rng.regens;
