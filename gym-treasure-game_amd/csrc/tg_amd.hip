@@ -750,19 +750,25 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
 // predicted length class), which raised lane efficiency from 0.53 to 0.84 but ran 2-5 % slower:
 // DESIGN.md §3.1.)
 constexpr int SHARDS = 8;
-constexpr int kOrderH[O_COUNT] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
-                                  O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
-                                  O_INTERACT};
+// Worklists: one per option, and one (L_RESET) of the envs whose option cannot run but which
+// enter the step done with auto-reset on (stepped with auto-reset off until done, then on):
+// k_run resets them (reward None, no option), so k_classify carries no reset path (the gauss
+// pair's f64 library code held it at 79 VGPRs, 6 waves per SIMD; without it 58, 8 waves)
+constexpr int L_RESET = O_COUNT;
+constexpr int NLIST = O_COUNT + 1;
+constexpr int kOrderH[NLIST] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
+                                O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
+                                O_INTERACT,  L_RESET};
 struct RunPos {
-  int of[O_COUNT];  // run position of option k (kOrder's inverse)
+  int of[NLIST];  // run position of list k (kOrder's inverse)
 };
 constexpr RunPos make_runpos() {
   RunPos r{};
-  for (int j = 0; j < O_COUNT; ++j) r.of[kOrderH[j]] = j;
+  for (int j = 0; j < NLIST; ++j) r.of[kOrderH[j]] = j;
   return r;
 }
 constexpr RunPos kRunPos = make_runpos();
-constexpr int NSEG = O_COUNT * SHARDS;  // segment = run position * SHARDS + shard
+constexpr int NSEG = NLIST * SHARDS;  // segment = run position * SHARDS + shard
 static_assert(NSEG <= 2 * RUN_BLOCK, "k_run's prefix: two segments per thread");
 constexpr int NCTR = NSEG;      // the worklist counters
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
@@ -785,14 +791,14 @@ struct Work {
 // ticks are the slowest in wall time (~2,100 cycles each) and which end the kernel, then the
 // long go walks (mean 56 ticks), drops, ladders, interact.  A/B against go
 // first: 0.1366 vs 0.1400 ms.
-__constant__ int kOrder[O_COUNT] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
-                                    O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
-                                    O_INTERACT};
-__constant__ int kSegBase[O_COUNT] = {kRunPos.of[0] * SHARDS, kRunPos.of[1] * SHARDS,
+__constant__ int kOrder[NLIST] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
+                                  O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
+                                  O_INTERACT,  L_RESET};
+__constant__ int kSegBase[NLIST] = {kRunPos.of[0] * SHARDS, kRunPos.of[1] * SHARDS,
                                       kRunPos.of[2] * SHARDS, kRunPos.of[3] * SHARDS,
                                       kRunPos.of[4] * SHARDS, kRunPos.of[5] * SHARDS,
                                       kRunPos.of[6] * SHARDS, kRunPos.of[7] * SHARDS,
-                                      kRunPos.of[8] * SHARDS};
+                                      kRunPos.of[8] * SHARDS, kRunPos.of[9] * SHARDS};
 
 template <bool AUTORESET, bool FINAL, int POL = -1>
 __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
@@ -802,7 +808,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
                                                      uint32_t* __restrict__ err_or,
                                                      unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
-  __shared__ int bcnt[O_COUNT], bbase[O_COUNT];
+  __shared__ int bcnt[NLIST], bbase[NLIST];
   // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
   // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
   // keeps 8 waves per SIMD
@@ -828,7 +834,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     a2 = S.ang[i];
     ep = S.ep[i];
   }
-  if (threadIdx.x < O_COUNT) bcnt[threadIdx.x] = 0;
+  if (threadIdx.x < NLIST) bcnt[threadIdx.x] = 0;
   if (blockIdx.x == 0)
     for (int c = threadIdx.x; c < NCTR; c += BLOCK) w.ctr_next[c * CTR_STRIDE] = 0;
   stage_level(lv, grid, L);  // includes the barrier
@@ -845,8 +851,11 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     }
     k = option_index(act);
     runs = k >= 0 && can_run(L, m, e, k);
+    if (k < 0) e.f |= E_ACTION;
   }
-  const int bk = runs ? k : -1;  // the env's worklist
+  // entering done with auto-reset on and no option to run: reset in k_run (L_RESET)
+  const bool rst = AUTORESET && live && !runs && is_done(e);
+  const int bk = runs ? k : rst ? L_RESET : -1;  // the env's worklist
   // halves left stale and not listed yet go on this step's refill list (MT_LISTED); k_regen
   // regenerates the lists of several steps at once (a lane that needs a half first does it
   // itself: the ring leaves >= ~2,400 draws of slack, launch_step)
@@ -864,7 +873,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   // wave's lanes are matched option by option)
   int slot = 0;
   {
-    unsigned long long pend = __ballot(runs);
+    unsigned long long pend = __ballot(bk >= 0);
     while (pend) {
       const int first = __ffsll((long long)pend) - 1;
       const int b0 = __builtin_amdgcn_readlane(bk, first);
@@ -881,35 +890,26 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   // reward-None envs are finished (their latency overlaps that work)
   const int shard = blockIdx.x % SHARDS;
   int my_base = 0;
-  if (threadIdx.x < O_COUNT) {
+  if (threadIdx.x < NLIST) {
     const int c = bcnt[threadIdx.x];
     my_base = c ? atomicAdd(&w.ctr[(kSegBase[threadIdx.x] + shard) * CTR_STRIDE], c) : 0;
   }
-  uint4 s4w = s4;  // the state the worklist copy carries
-  s4w.w = e.mti;
+  const uint4 s4w = pack(e);  // the state the worklist copy carries (listed half, E_ACTION)
 
-  // envs whose option cannot run: reward None, state unchanged (TG/:91-96, OP/:22-23)
-  bool dn = false;
-  uint32_t draws = 0;
-  if (live && !runs) {
-    if (k < 0) e.f |= E_ACTION;
+  // envs whose option cannot run: reward None, state unchanged (TG/:91-96, OP/:22-23); not
+  // done, or auto-reset off (the others are k_run's, L_RESET)
+  const bool fin = live && !runs && !rst;
+  if (fin) {
     e.ang0 = a2.x;
     e.ang1 = a2.y;
-    dn = is_done(e);
-    Rng rng(S.mt + i * MT_STORE, e.mti, S.mc + i * MT_CODES);
-    StepResult r{0, 0, (int)dn, 0};
-    finish_step<AUTORESET, FINAL>(L, e, rng, i, r, ep, io, orow);
-    // the stale half keeps its bits unless the auto-reset's draws crossed into it (the Rng then
-    // regenerated it; the half left is stale, not listed)
-    e.mti = rng.entered ? (rng.pos | MT_STALE) : (rng.pos | (e.mti & (MT_STALE | MT_LISTED)));
-    draws = rng.draws;
+    Rng rng(S.mt + i * MT_STORE, e.mti, S.mc + i * MT_CODES);  // no draws without a reset
+    StepResult r{0, 0, (int)is_done(e), 0};
+    finish_step<false, FINAL>(L, e, rng, i, r, ep, io, orow);
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   const int2 ep_in = ep;
-  if (AUTORESET) record_episodes(live && !runs && dn, g0 + i, ep, io.tstep, q, stats);
-  store_obs_wave(io.obs, i - lane, __ballot(live && !runs), orow,
-                 ostage + (threadIdx.x & ~63) * 9);
-  if (live && !runs) {
+  store_obs_wave(io.obs, i - lane, __ballot(fin), orow, ostage + (threadIdx.x & ~63) * 9);
+  if (fin) {
     const uint4 s4n = pack(e);
     if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w) {  // reset / flag
       S.st4[i] = s4n;
@@ -918,17 +918,16 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
     // reward None: the return and the episode's start step are unchanged unless it ended
     if (ep.x != ep_in.x || ep.y != ep_in.y) S.ep[i] = ep;
   }
-  if (threadIdx.x < O_COUNT) bbase[threadIdx.x] = my_base;
+  if (threadIdx.x < NLIST) bbase[threadIdx.x] = my_base;
   __syncthreads();
-  if (runs) {
-    const int64_t at = (int64_t)(kSegBase[k] + shard) * w.shard_cap + bbase[k] + slot;
+  if (bk >= 0) {
+    const int64_t at = (int64_t)(kSegBase[bk] + shard) * w.shard_cap + bbase[bk] + slot;
     w.lists[at] = (int32_t)i;
     w.wst4[at] = s4w;
     w.wang[at] = a2;
     w.wep[at] = ep;
   }
-  wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, (int)draws,
-              AUTORESET ? (live && !runs && dn) : 0);
+  wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, 0);
   kst_end(ks, kt0);
 }
 
@@ -957,7 +956,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   // prefix and its start in the chunk space, where each option is padded to whole chunks
   __shared__ int pre[NSEG + 1];
   __shared__ int wtot[RUN_BLOCK / 64];
-  __shared__ int ostart[O_COUNT + 1], oraw[O_COUNT + 1];
+  __shared__ int ostart[NLIST + 1], oraw[NLIST + 1];
   {
     const int s0 = 2 * (int)threadIdx.x, ln = threadIdx.x & 63;
     const int c0 = s0 < NSEG ? w.ctr[s0 * CTR_STRIDE] : 0;
@@ -979,20 +978,20 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
-    for (int j = 0; j < O_COUNT; ++j) {
+    for (int j = 0; j < NLIST; ++j) {
       const int sb = j * SHARDS, se = sb + SHARDS;
       ostart[j] = acc;
       oraw[j] = pre[sb];
       acc += (pre[se] - pre[sb] + 63) & ~63;
     }
-    ostart[O_COUNT] = acc;
-    oraw[O_COUNT] = pre[NSEG];
+    ostart[NLIST] = acc;
+    oraw[NLIST] = pre[NSEG];
   }
   RUN_LEVEL_IN_LDS();  // includes the barrier (ostart / oraw)
-  const int total = ostart[O_COUNT];
+  const int total = ostart[NLIST];
   const int base = (blockIdx.x * RUN_BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
   int oj = 0;  // ostart[oj] <= base < ostart[oj + 1] (wave-uniform)
-  while (oj + 1 < O_COUNT && ostart[oj + 1] <= base) ++oj;
+  while (oj + 1 < NLIST && ostart[oj + 1] <= base) ++oj;
   oj = __builtin_amdgcn_readfirstlane(oj);
   const int k = kOrder[oj];
   // this lane's place in option k's lists (the raw prefix's coordinates), and its segment
@@ -1451,10 +1450,10 @@ __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4,
 namespace {
 int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 // k_run needs one wave per 64-lane chunk of the worklists, each option padded to whole chunks:
-// at most n/64 + O_COUNT chunks (idle blocks interleaved among the option blocks, so that MT
+// at most n/64 + NLIST chunks (idle blocks interleaved among the option blocks, so that MT
 // regenerations start at once, measured no faster for the masked policy and slower for the
 // uniform one: DESIGN.md §3.3)
-int run_grid_for(int64_t n) { return grid_for(n) + (O_COUNT * 64 + BLOCK - 1) / BLOCK; }
+int run_grid_for(int64_t n) { return grid_for(n) + (NLIST * 64 + BLOCK - 1) / BLOCK; }
 // one launch-counter slot per workgroup of the widest step launch (k_run)
 int stat_slots(int64_t n) { return run_grid_for(n); }
 

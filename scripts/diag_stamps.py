@@ -91,8 +91,8 @@ def main():
     for t in np.linspace(0, span, 11):
         print("  t=%6.1f us active waves %5d" % (t, ((st_us <= t) & (en_us > t)).sum()))
     names = ["go_left", "go_right", "up_ladder", "down_ladder", "interact", "down_left",
-             "down_right", "jump_left", "jump_right"]
-    for k in range(9):
+             "down_right", "jump_left", "jump_right", "reset_only"]
+    for k in range(10):
         sel = kk == k
         if sel.any():
             print("  %-11s waves %5d end max %6.1f us p90 %6.1f  iters max %4d mean %5.1f  cyc/iter %6.0f"

@@ -189,6 +189,42 @@ def test_available_mask_matches_oracle(tg, oracle):
         vec.step(torch.as_tensor(a, device=vec.device))
 
 
+def test_done_envs_reset_when_autoreset_turns_on(tg, oracle):
+    """Envs left done with auto-reset off, then stepped with it on: an env whose option cannot
+    run is reset within the step (reward None: k_run's reset-only list since round 4), one
+    whose option runs finishes it and resets.  Rows, final rows and the state after equal
+    OracleEnv under the same rule (a step that ends done is followed by reset())."""
+    n, a0, t1 = 256, 0x5A, 700
+    vec = tg.TreasureGameVec(n, seed=11, autoreset=False)
+    vec.reset()
+    envs = [oracle.OracleEnv(11 + g) for g in range(n)]
+    for t in range(t1):
+        a = vec.policy_actions(t, a0, "masked")
+        vec.step(a)
+        for g, e in enumerate(envs):
+            e.step(int(a[g]))
+    _, _, _, d, _ = vec.step(vec.policy_actions(t1, a0, "masked"))  # (oracle below)
+    a = vec.policy_actions(t1, a0, "masked").cpu().numpy()
+    for g, e in enumerate(envs):
+        e.step(int(a[g]))
+    assert int(d.sum()) >= 3  # envs that enter the auto-reset steps done (5 with these seeds)
+    vec.autoreset = True
+    for t in range(t1 + 1, t1 + 25):
+        a = vec.policy_actions(t, a0, "masked")
+        o, r, v, d, info = vec.step(a)
+        o, r, v, d, fo = (x.cpu().numpy() for x in (o, r, v, d, info["final_obs"]))
+        a = a.cpu().numpy()
+        for g, e in enumerate(envs):
+            eo, er, ed, _ = e.step(int(a[g]))
+            np.testing.assert_array_equal(fo[g].view(np.uint64), eo.view(np.uint64))
+            assert (bool(v[g]), bool(d[g])) == (er is not None, ed)
+            assert er is None or int(r[g]) == er
+            if ed:
+                eo = e.reset()
+            np.testing.assert_array_equal(o[g].view(np.uint64), eo.view(np.uint64))
+    assert vec.errors() == 0
+
+
 def test_dropin_single_env(tg, oracle):
     """TreasureGame(seed=s) == random.seed(s); TreasureGame() of the reference, with the
     reference's Python types (TG/:91-96): list of floats, int or None, bool, {}."""
