@@ -1111,14 +1111,17 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
 // in, >= MT_HALF / 2 - (one step's draws) ~ 2,400 draws, more than REGEN_STEPS steps draw on the
 // default level (<= ~110 per step); a lane that gets there first regenerates the half itself.
 constexpr int REGEN_STEPS = 16;
-constexpr int REGEN_GRAB = 16;  // list regions a wave takes from its XCD's counter at a time
+// list regions a wave takes at a time: REGEN_GRAB at most (a full launch: ~32 per wave), fewer
+// when the launch has fewer regions than its waves x REGEN_GRAB (a drain of a few steps' lists,
+// the end of a timed region), so that every wave gets some (launch_regen)
+constexpr int REGEN_GRAB = 16;
 static_assert(REGEN_GRAB <= 64, "a grab's region counts load one per lane");
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  const uint8_t* __restrict__ nrefill, int64_t n,
                                                  int slots, int32_t* __restrict__ ctr,
                                                  int32_t* __restrict__ ctr_next,
                                                  unsigned long long* __restrict__ stats,
-                                                 int nstat, unsigned long long* __restrict__ ks) {
+                                                 int nstat, int grab, unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
   __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   lds_u32* const scr = (lds_u32*)scratch[threadIdx.x >> 6];
@@ -1146,15 +1149,15 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
   const int64_t nwx = (int64_t)((gridDim.x - (unsigned)xcd + 7u) >> 3) * (BLOCK / 64);
   bool first = true;
   while (true) {
-    int64_t j0 = (int64_t)wx * REGEN_GRAB;
+    int64_t j0 = (int64_t)wx * grab;
     if (!first) {
       int g = 0;
-      if (lane == 0) g = atomicAdd(q, REGEN_GRAB);
-      j0 = nwx * REGEN_GRAB + __builtin_amdgcn_readfirstlane(g);
+      if (lane == 0) g = atomicAdd(q, grab);
+      j0 = nwx * grab + __builtin_amdgcn_readfirstlane(g);
     }
     first = false;
     if (j0 >= nmine) break;
-    const int64_t j1 = j0 + REGEN_GRAB < nmine ? j0 + REGEN_GRAB : nmine;
+    const int64_t j1 = j0 + grab < nmine ? j0 + grab : nmine;
     // the grab's region counts in one load round, one lane each (region r = xcd + 8 j; its
     // count at nrefill[r], its entries at refill[64 r ..]): most regions are empty (~0.2 halves
     // per region at the uniform policy's rate), and reading the counts one by one made every
@@ -1720,8 +1723,12 @@ int launch_regen(tg_batch* h, StepCtx& c, hipStream_t st) {
   int32_t* const cur = c.regen_ctr + c.regen_parity * 8 * CTR_STRIDE;
   int32_t* const nxt = c.regen_ctr + (c.regen_parity ^ 1) * 8 * CTR_STRIDE;
   c.regen_parity ^= 1;
+  const int64_t waves = grid * (BLOCK / 64);
+  int64_t grab = (regions + waves - 1) / waves;  // regions per wave at an even share
+  if (grab > REGEN_GRAB) grab = REGEN_GRAB;
+  if (grab < 1) grab = 1;
   hipLaunchKernelGGL(k_regen, dim3((unsigned)grid), dim3(BLOCK), 0, st, soa_of(h, c), c.refill,
-                     c.nrefill, c.n, c.rpend, cur, nxt, c.stats, stat_slots(c.n), ks);
+                     c.nrefill, c.n, c.rpend, cur, nxt, c.stats, stat_slots(c.n), (int)grab, ks);
   HIP_TRY(hipGetLastError());
   c.rpend = 0;
   ++h->regen_launches;
