@@ -195,7 +195,8 @@ def test_done_envs_reset_when_autoreset_turns_on(tg, oracle):
     whose option runs finishes it and resets.  Rows, final rows and the state after equal
     OracleEnv under the same rule (a step that ends done is followed by reset())."""
     n, a0, t1 = 256, 0x5A, 700
-    vec = tg.TreasureGameVec(n, seed=11, autoreset=False)
+    vec = tg.TreasureGameVec(n, seed=11, autoreset=True)  # (allocates the final-obs rows)
+    vec.autoreset = False
     vec.reset()
     envs = [oracle.OracleEnv(11 + g) for g in range(n)]
     for t in range(t1):
