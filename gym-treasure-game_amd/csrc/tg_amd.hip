@@ -606,8 +606,10 @@ __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ part
                                            int valid, int ticks, int draws, int episodes,
                                            int regens = 0, bool wave_ticks = false,
                                            int64_t sl = -1) {  // slot: blockIdx.x by default
-  const int v[5] = {wave_sum(steps), wave_sum(valid), wave_sum(ticks), wave_sum(draws),
-                    wave_sum(episodes)};
+  // a counter that is 0 on every lane (k_run's steps / valid, most waves' episodes) skips its
+  // six cross-lane steps: the reductions sit in the option waves' epilogue, on the tail
+  auto sum = [](int x) { return __ballot(x != 0) ? wave_sum(x) : 0; };
+  const int v[5] = {sum(steps), sum(valid), sum(ticks), sum(draws), sum(episodes)};
   const int wt = wave_ticks ? wave_max(ticks) : 0;
   if ((threadIdx.x & 63) == 0) {
     unsigned long long* const slot = part + (size_t)(sl < 0 ? (int64_t)blockIdx.x : sl) * ST_COUNT;
@@ -1054,7 +1056,8 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   }
   __builtin_amdgcn_s_setprio(0);
   wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
-             regens + wave_sum(lregen), true, (int64_t)blockIdx.x / (BLOCK / RUN_BLOCK));
+             regens + (__ballot(lregen != 0) ? wave_sum(lregen) : 0), true,
+             (int64_t)blockIdx.x / (BLOCK / RUN_BLOCK));
   kst_end(ks, kt0);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
