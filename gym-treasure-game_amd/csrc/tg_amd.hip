@@ -1036,7 +1036,8 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     rng.prime();  // issue the code loads now; the first draw comes after the policy setup
     TG_STAMP(t1);
     if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
-    run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform: one specialised loop
+    // k is wave-uniform: one specialised loop; L_RESET's envs run none (reward None)
+    if (k != L_RESET) run_option(L, trig, m, e, k, rng, r);
     TG_STAMP(t2);
 #ifdef TG_DIAG_STAMPS
     ph1 = rng.ph[1], ph2 = rng.ph[2], ph3 = rng.ph[3], prounds = rng.rounds;
