@@ -199,15 +199,14 @@ def test_done_envs_reset_when_autoreset_turns_on(tg, oracle):
     vec.autoreset = False
     vec.reset()
     envs = [oracle.OracleEnv(11 + g) for g in range(n)]
-    for t in range(t1):
+    for t in range(t1 + 1):
         a = vec.policy_actions(t, a0, "masked")
-        vec.step(a)
+        o, _, _, d, _ = vec.step(a)
+        o, d, a = o.cpu().numpy(), d.cpu().numpy(), a.cpu().numpy()
         for g, e in enumerate(envs):
-            e.step(int(a[g]))
-    _, _, _, d, _ = vec.step(vec.policy_actions(t1, a0, "masked"))  # (oracle below)
-    a = vec.policy_actions(t1, a0, "masked").cpu().numpy()
-    for g, e in enumerate(envs):
-        e.step(int(a[g]))
+            eo, _, ed, _ = e.step(int(a[g]))
+            assert bool(d[g]) == ed and np.array_equal(o[g].view(np.uint64), eo.view(np.uint64)), \
+                ("auto-reset off", t, g)
     assert int(d.sum()) >= 3  # envs that enter the auto-reset steps done (5 with these seeds)
     vec.autoreset = True
     for t in range(t1 + 1, t1 + 25):
@@ -217,12 +216,13 @@ def test_done_envs_reset_when_autoreset_turns_on(tg, oracle):
         a = a.cpu().numpy()
         for g, e in enumerate(envs):
             eo, er, ed, _ = e.step(int(a[g]))
-            np.testing.assert_array_equal(fo[g].view(np.uint64), eo.view(np.uint64))
-            assert (bool(v[g]), bool(d[g])) == (er is not None, ed)
-            assert er is None or int(r[g]) == er
+            where = ("auto-reset on", t, g, int(a[g]), er, ed)
+            assert np.array_equal(fo[g].view(np.uint64), eo.view(np.uint64)), where
+            assert (bool(v[g]), bool(d[g])) == (er is not None, ed), where
+            assert er is None or int(r[g]) == er, where
             if ed:
                 eo = e.reset()
-            np.testing.assert_array_equal(o[g].view(np.uint64), eo.view(np.uint64))
+            assert np.array_equal(o[g].view(np.uint64), eo.view(np.uint64)), where
     assert vec.errors() == 0
 
 
