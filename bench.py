@@ -161,6 +161,9 @@ def parse(argv=None):
     ap.add_argument("--timing-every", type=int, default=1,
                     help="kernel spans of every k-th timed step (in-kernel s_memrealtime stamps: "
                          "nothing goes on the stream) for the roofline")
+    ap.add_argument("--no-spin", dest="spin", action="store_false",
+                    help="wait for the timed region's end in torch.cuda.synchronize alone (the "
+                         "default polls the end event first, then synchronizes)")
     ap.add_argument("--secondary-steps", type=int, default=30,
                     help="N = 1, c3: steps of the masked-policy line (0 disables it)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -497,11 +500,18 @@ class Runner:
                 t += 1
         self.tg._lib.check(self.L.tg_regenerate(self.h, self.stream), "tg_regenerate")
         ev1.record()
+        t_launched = time.perf_counter()
+        if self.args.spin:  # a blocking wait's wake-up costs tens of us after the last kernel
+            while not ev1.query():
+                pass
         torch.cuda.synchronize(self.dev)
+        t_synced = time.perf_counter()
         if self.world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
         self.events_ms = ev0.elapsed_time(ev1)
+        self.host_ms = {"launch": (t_launched - t0) * 1e3, "wait": (t_synced - t_launched) * 1e3,
+                        "spin": bool(self.args.spin)}
         self.timing = False
         vec.set_timing(0)
         st = vec.stats()
@@ -643,6 +653,7 @@ def step_line(args, runner, dt, st, node, world, total):
                         if args.mode == "compact" else ["k_step"])),
                     "alg_bytes_per_launch": all_b, "kernel_ms": all_s * 1e3,
                     "events_ms_per_step": runner.events_ms / args.steps,
+                    "host_ms": runner.host_ms,
                     "gaps_ms": ms_step - all_s * 1e3,
                     "achieved": all_b / all_s / 1e9,
                     "frac": all_b / all_s / 1e9 / HBM_PEAK_GBS,

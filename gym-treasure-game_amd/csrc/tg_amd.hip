@@ -784,8 +784,11 @@ struct Work {
   int2* __restrict__ wep;
   int32_t* __restrict__ ctr;     // [NCTR * CTR_STRIDE], this step's counters
   int32_t* __restrict__ ctr_next;  // the other parity's, zeroed here for the next step
-  uint32_t* __restrict__ refill;  // [n]: per classify wave w, slots 64w..: env | source half
-  uint8_t* __restrict__ nrefill;  // [n / 64]: entries of classify wave w (no atomics)
+  // stale MT halves, one list per shard (= blockIdx.x % SHARDS, the XCD), appended across the
+  // pending steps: list x at refill[x * rcap ..], its length at rcnt[x * CTR_STRIDE]
+  uint32_t* __restrict__ refill;  // env | source half
+  int32_t* __restrict__ rcnt;
+  int64_t rcap;
   int64_t shard_cap;
 };
 // worklist order = the order the chunks' loads reach HBM at the kernel's start (all option
@@ -861,14 +864,20 @@ __global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
   // halves left stale and not listed yet go on this step's refill list (MT_LISTED); k_regen
   // regenerates the lists of several steps at once (a lane that needs a half first does it
   // itself: the ring leaves >= ~2,400 draws of slack, launch_step)
+  // (dense lists: a drain of a few steps' lists spreads one half per wave, where the per-wave
+  // regions of round 4 left a wave with the few regions holding 3-4 halves for ~0.1 ms)
   {
     const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
     const unsigned long long b = __ballot(stale);
-    const int64_t wv = i >> 6;
-    if (stale)
-      w.refill[wv * 64 + __popcll(b & ((1ull << lane) - 1ull))] =
-          (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
-    if (lane == 0 && live) w.nrefill[wv] = (uint8_t)__popcll(b);  // (a wave past n has no region)
+    if (b) {
+      const int shard = (int)(blockIdx.x % SHARDS);
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&w.rcnt[shard * CTR_STRIDE], __popcll(b));
+      base = __builtin_amdgcn_readlane(base, 0);
+      if (stale)
+        w.refill[shard * w.rcap + base + __popcll(b & ((1ull << lane) - 1ull))] =
+            (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
+    }
     if (stale) e.mti |= MT_LISTED;
   }
   // workgroup-local slots: one LDS atomic per wave and option present in the wave (the
@@ -1103,94 +1112,76 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
 }
 
 // ---- deferred regeneration of the listed stale MT halves (k_regen) ----------------------------
-// k_classify lists the halves the previous step left stale (MT_STALE) on the refill list of the
-// step's slot and marks them MT_LISTED; every REGEN_STEPS compact steps (and on tg_regenerate)
-// k_regen regenerates the lists of all pending slots at once with a full-occupancy grid and no
-// option loops beside it: each wave takes a contiguous range of list regions (a region = one
-// classify wave's <= 64 entries).  An entry is regenerated iff its env's state word still
-// says MT_STALE (its lane may have regenerated the half itself, or crossed again since): the
-// half not holding the position, from the last generation of the one holding it; then the word
-// loses MT_STALE | MT_LISTED.  It runs alone on the stream, so nothing else touches the state.
+// k_classify appends the halves the previous step left stale (MT_STALE) to its shard's refill
+// list and marks them MT_LISTED; every REGEN_STEPS compact steps (and on tg_regenerate) k_regen
+// regenerates every pending entry with a full-occupancy grid and no option loops beside it: the
+// waves of XCD x (blockIdx.x % 8) take list x's entries, an even share each (the halves cost
+// the same: MT_HALF_GENS twists), the rest from the list's counter.  An entry is regenerated iff
+// its env's state word still says MT_STALE (its lane may have regenerated the half itself, or
+// crossed again since): the half not holding the position, from the last generation of the one
+// holding it; then the word loses MT_STALE | MT_LISTED.  It runs alone on the stream, so
+// nothing else touches the state.
 // Slack: a listed half is needed again only after the env consumes the rest of the half it is
 // in, >= MT_HALF / 2 - (one step's draws) ~ 2,400 draws, more than REGEN_STEPS steps draw on the
 // default level (<= ~110 per step); a lane that gets there first regenerates the half itself.
 constexpr int REGEN_STEPS = 16;
-// list regions a wave takes at a time: REGEN_GRAB at most (a full launch: ~32 per wave), fewer
-// when the launch has fewer regions than its waves x REGEN_GRAB (a drain of a few steps' lists,
-// the end of a timed region), so that every wave gets some (launch_regen)
-constexpr int REGEN_GRAB = 16;
-static_assert(REGEN_GRAB <= 64, "a grab's region counts load one per lane");
+// regen_ctr, per set: the 8 grab counters, then the 8 list lengths (k_classify's rcnt)
+constexpr int RCTR_LIST = 8;
+constexpr int RCTR_N = 16;
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
-                                                 const uint8_t* __restrict__ nrefill, int64_t n,
-                                                 int slots, int32_t* __restrict__ ctr,
+                                                 int64_t rcap, int32_t* __restrict__ ctr,
                                                  int32_t* __restrict__ ctr_next,
                                                  unsigned long long* __restrict__ stats,
-                                                 int nstat, int grab, unsigned long long* __restrict__ ks) {
+                                                 int nstat, unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
   __shared__ __attribute__((aligned(16))) uint32_t scratch[BLOCK / 64][MT_N];
   lds_u32* const scr = (lds_u32*)scratch[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x < 8) ctr_next[threadIdx.x * CTR_STRIDE] = 0;  // next launch's
-  const int64_t nreg = (n + 63) >> 6;  // regions per slot
-  const int64_t total = nreg * slots;
-  // regions go out REGEN_GRAB at a time from one counter per XCD (blockIdx.x % 8: regions
-  // xcd, xcd + 8, ...): the halves per region vary, and a fixed share per wave left the
-  // launch to its most loaded waves
   const int xcd = (int)(blockIdx.x & 7u);
-  const int64_t nmine = (total - xcd + 7) >> 3;
+  const int64_t cnt = ctr[(RCTR_LIST + xcd) * CTR_STRIDE];
+  if (blockIdx.x == 0 && threadIdx.x < RCTR_N) ctr_next[threadIdx.x * CTR_STRIDE] = 0;
   int32_t* const q = ctr + xcd * CTR_STRIDE;
+  const uint32_t* const list = refill + xcd * rcap;
   uint32_t* const st_w = reinterpret_cast<uint32_t*>(S.st4);  // word 4i + 3: env i's MT word
   auto src_of = [&](uint32_t env, uint32_t s) {
     const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
     return (const glb_u32*)(S.mt + (int64_t)env * MT_STORE + regen_src_off(dst));
   };
-  int halves = 0;
-  // the first grab is static (this wave's index among its XCD's waves), the rest come from the
-  // counter, which starts past the static ones: one atomic per wave fewer, and at a small
-  // launch (the end of a timed region drains a few steps' lists) no round of 1,024 atomics per
-  // counter before any work starts
+  // this wave's index among its XCD's waves; the first grab is static (an even share, at most
+  // 64: one entry per lane), the rest come from the counter, which starts past the static ones
   const int wx = (int)(blockIdx.x >> 3) * (BLOCK / 64) + (int)(threadIdx.x >> 6);
   const int64_t nwx = (int64_t)((gridDim.x - (unsigned)xcd + 7u) >> 3) * (BLOCK / 64);
+  int64_t grab = (cnt + nwx - 1) / nwx;
+  if (grab > 64) grab = 64;
+  if (grab < 1) grab = 1;
+  int halves = 0;
   bool first = true;
   while (true) {
     int64_t j0 = (int64_t)wx * grab;
     if (!first) {
       int g = 0;
-      if (lane == 0) g = atomicAdd(q, grab);
+      if (lane == 0) g = atomicAdd(q, (int)grab);
       j0 = nwx * grab + __builtin_amdgcn_readfirstlane(g);
     }
     first = false;
-    if (j0 >= nmine) break;
-    const int64_t j1 = j0 + grab < nmine ? j0 + grab : nmine;
-    // the grab's region counts in one load round, one lane each (region r = xcd + 8 j; its
-    // count at nrefill[r], its entries at refill[64 r ..]): most regions are empty (~0.2 halves
-    // per region at the uniform policy's rate), and reading the counts one by one made every
-    // grab a chain of dependent byte loads, ~120 us of each launch whatever its work
-    int cnt_l = 0;
-    if (lane < j1 - j0) cnt_l = nrefill[xcd + 8 * (j0 + lane)];
-    unsigned long long ne = __ballot(cnt_l != 0);
-    while (ne) {
-      const int jl = __ffsll((long long)ne) - 1;
-      ne &= ne - 1;
-      const int64_t r = xcd + 8 * (j0 + jl);
-      const int cnt = __builtin_amdgcn_readlane(cnt_l, jl);
-      const uint32_t env_l = lane < cnt ? refill[r * 64 + lane] & 0x7FFFFFFFu : 0u;
-      const uint32_t st_l = lane < cnt ? st_w[(int64_t)env_l * 4 + 3] : 0u;
-      unsigned long long need = __ballot(lane < cnt && (st_l & MT_STALE));
-      // one half at a time: 52 VGPRs, 8 waves per SIMD (the next half's source loads pipelined
-      // into this one's twist took 76 VGPRs, 6 waves, and measured no faster: DESIGN.md §3.3)
-      while (need) {
-        const int L = __ffsll((long long)need) - 1;
-        need &= need - 1;
-        const uint32_t env = __builtin_amdgcn_readlane(env_l, L), s = __builtin_amdgcn_readlane(st_l, L);
-        const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
-        TwistIn t;
-        twist_load(src_of(env, s), t);
-        twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_STORE), S.mc + (int64_t)env * MT_CODES,
-                    (int)(dst / (uint32_t)MT_N), MT_HALF_GENS, true, scr);
-        if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
-        ++halves;
-      }
+    if (j0 >= cnt) break;
+    const int64_t m = cnt - j0 < grab ? cnt - j0 : grab;
+    const uint32_t env_l = lane < m ? list[j0 + lane] & 0x7FFFFFFFu : 0u;
+    const uint32_t st_l = lane < m ? st_w[(int64_t)env_l * 4 + 3] : 0u;
+    unsigned long long need = __ballot(lane < m && (st_l & MT_STALE));
+    // one half at a time: 52 VGPRs, 8 waves per SIMD (the next half's source loads pipelined
+    // into this one's twist took 76 VGPRs, 6 waves, and measured no faster: DESIGN.md §3.3)
+    while (need) {
+      const int L = __ffsll((long long)need) - 1;
+      need &= need - 1;
+      const uint32_t env = __builtin_amdgcn_readlane(env_l, L), s = __builtin_amdgcn_readlane(st_l, L);
+      const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
+      TwistIn t;
+      twist_load(src_of(env, s), t);
+      twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_STORE), S.mc + (int64_t)env * MT_CODES,
+                  (int)(dst / (uint32_t)MT_N), MT_HALF_GENS, true, scr);
+      if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
+      ++halves;
     }
   }
   // the grid can exceed the stats slots (>= 8 workgroups, one per XCD counter, at small n)
@@ -1544,17 +1535,18 @@ int alloc_ctx(StepCtx& c, int64_t off, int64_t n) {
   ALLOC_C(c.wang, sizeof(double2) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wep, sizeof(int2) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
-  ALLOC_C(c.refill, sizeof(uint32_t) * (size_t)((n + 63) & ~(int64_t)63) * REGEN_STEPS);
-  ALLOC_C(c.nrefill, (size_t)((n + 63) >> 6) * REGEN_STEPS);
-  ALLOC_C(c.regen_ctr, sizeof(int32_t) * 2 * 8 * CTR_STRIDE);
+  // a shard's list holds at most its workgroups' envs per pending step
+  c.rcap = c.shard_cap * REGEN_STEPS;
+  ALLOC_C(c.refill, sizeof(uint32_t) * SHARDS * (size_t)c.rcap);
+  ALLOC_C(c.regen_ctr, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE);
 #undef ALLOC_C
   HIP_TRY(hipMemset(c.stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)));
   HIP_TRY(hipMemset(c.wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE));
-  HIP_TRY(hipMemset(c.regen_ctr, 0, sizeof(int32_t) * 2 * 8 * CTR_STRIDE));
+  HIP_TRY(hipMemset(c.regen_ctr, 0, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE));
   return TG_OK;
 }
 void free_ctx(StepCtx& c) {
-  void* bufs[] = {c.stats, c.wl, c.wst4, c.wang, c.wep, c.wctr, c.refill, c.nrefill, c.regen_ctr};
+  void* bufs[] = {c.stats, c.wl, c.wst4, c.wang, c.wep, c.wctr, c.refill, c.regen_ctr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c.ev) (void)hipEventDestroy(c.ev);
@@ -1720,19 +1712,17 @@ int launch_regen(tg_batch* h, StepCtx& c, hipStream_t st) {
                                                          BLOCK, 0));
     h->regen_per_cu = nb > 0 ? nb : 1;
   }
-  const int64_t regions = ((c.n + 63) >> 6) * c.rpend;
+  // (the lists' lengths are on the device: the grid is sized for ~0.25 entries per env and step,
+  // 64 per wave)
+  const int64_t bound = ((c.n + 63) >> 6) * c.rpend;
   int64_t grid = (int64_t)h->cus * h->regen_per_cu;
-  if (grid > (regions + 3) / 4) grid = (regions + 3) / 4;  // 4 waves per workgroup
+  if (grid > (bound + 3) / 4) grid = (bound + 3) / 4;  // 4 waves per workgroup
   if (grid < 8) grid = 8;
-  int32_t* const cur = c.regen_ctr + c.regen_parity * 8 * CTR_STRIDE;
-  int32_t* const nxt = c.regen_ctr + (c.regen_parity ^ 1) * 8 * CTR_STRIDE;
+  int32_t* const cur = c.regen_ctr + c.regen_parity * RCTR_N * CTR_STRIDE;
+  int32_t* const nxt = c.regen_ctr + (c.regen_parity ^ 1) * RCTR_N * CTR_STRIDE;
   c.regen_parity ^= 1;
-  const int64_t waves = grid * (BLOCK / 64);
-  int64_t grab = (regions + waves - 1) / waves;  // regions per wave at an even share
-  if (grab > REGEN_GRAB) grab = REGEN_GRAB;
-  if (grab < 1) grab = 1;
   hipLaunchKernelGGL(k_regen, dim3((unsigned)grid), dim3(BLOCK), 0, st, soa_of(h, c), c.refill,
-                     c.nrefill, c.n, c.rpend, cur, nxt, c.stats, stat_slots(c.n), (int)grab, ks);
+                     c.rcap, cur, nxt, c.stats, stat_slots(c.n), ks);
   HIP_TRY(hipGetLastError());
   c.rpend = 0;
   ++h->regen_launches;
@@ -1780,10 +1770,11 @@ int launch_step(tg_batch* h, StepCtx& c, const StepIO& io_in, bool ar, hipStream
     int32_t* const cur = c.wctr + (c.parity ? NCTR * CTR_STRIDE : 0);
     int32_t* const nxt = c.wctr + (c.parity ? 0 : NCTR * CTR_STRIDE);
     c.parity ^= 1;
-    // this step's refill-list slot (k_regen drains the pending slots every REGEN_STEPS steps)
-    const int64_t nreg = (c.n + 63) >> 6;
-    const Work w{c.wl,  c.wst4, c.wang, c.wep, cur, nxt, c.refill + c.rpend * nreg * 64,
-                 c.nrefill + c.rpend * nreg, c.shard_cap};
+    // the refill lists append until k_regen drains them (every REGEN_STEPS steps), counted in
+    // the set the next k_regen reads
+    const Work w{c.wl,     c.wst4, c.wang, c.wep, cur, nxt, c.refill,
+                 c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
+                 c.shard_cap};
     decltype(&k_classify<true, true>) kc;
     if (io.policy == TG_POLICY_UNIFORM)
       kc = ar ? (fo ? k_classify<true, true, 0> : k_classify<true, false, 0>)
@@ -2303,6 +2294,8 @@ int tg_write_state(tg_batch* h, const int32_t* pos, const uint32_t* flags, const
   // validated: the pending refill lists name the old states' halves, and every ring is rebuilt
   h->main.rpend = 0;
   for (auto& c : h->grp) c.rpend = 0;
+  HIP_TRY(hipMemset(h->main.regen_ctr, 0, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE));
+  for (auto& c : h->grp) HIP_TRY(hipMemset(c.regen_ctr, 0, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE));
   HIP_TRY(hipMemcpy(h->S.st4, st.data(), sizeof(uint4) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->S.ang, ang, sizeof(double2) * n, hipMemcpyHostToDevice));
   {  // (return, length) -> (return, start step)

@@ -59,13 +59,13 @@ struct StepCtx {
   double2* wang = nullptr;
   int2* wep = nullptr;
   int32_t* wctr = nullptr; // sharded counters, two sets (step parity)
-  uint32_t* refill = nullptr;  // stale MT halves listed by k_classify: REGEN_STEPS slots (k_regen)
-  uint8_t* nrefill = nullptr;
+  uint32_t* refill = nullptr;  // stale MT halves listed by k_classify: SHARDS lists (k_regen)
+  int64_t rcap = 0;            // entries per list: a shard's envs x REGEN_STEPS
   int64_t shard_cap = 0;
   int parity = 0;  // which half of wctr this compact step counts in
   int rpend = 0;   // compact steps whose refill lists k_regen has not drained
-  int32_t* regen_ctr = nullptr;  // k_regen's per-XCD region counters, two sets (k_regen zeroes
-                                 // the other set for the next launch)
+  int32_t* regen_ctr = nullptr;  // per XCD: k_regen's grab counters and the lists' lengths, two
+                                 // sets (k_regen zeroes the other set for the next launch)
   int regen_parity = 0;          // which set the next k_regen counts in
   hipStream_t st = nullptr;      // a group's stream (groups only)
   hipEvent_t ev = nullptr;       //   and its join event
