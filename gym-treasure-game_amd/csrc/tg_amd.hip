@@ -805,18 +805,18 @@ __constant__ int kSegBase[NLIST] = {kRunPos.of[0] * SHARDS, kRunPos.of[1] * SHAR
                                       kRunPos.of[6] * SHARDS, kRunPos.of[7] * SHARDS,
                                       kRunPos.of[8] * SHARDS, kRunPos.of[9] * SHARDS};
 
+// 8 waves per SIMD: its 98-106 SGPRs (the level, the step's pointers) held it to 7; forced, 32-55
+// of them spill to VGPR lanes (no VGPR spills, 60 VGPRs).  A/B r04r: uniform 0.1246 vs 0.1258 ms
+// per step in each of 4 rounds; masked within its spread
 template <bool AUTORESET, bool FINAL, int POL = -1>
-__global__ __launch_bounds__(BLOCK) void k_classify(Soa S, int64_t n, Level L,
-                                                     const uint32_t* __restrict__ grid,
-                                                     StepIO io, EpQueue q, Work w, int64_t g0,
-                                                     unsigned long long* __restrict__ stats,
-                                                     uint32_t* __restrict__ err_or,
-                                                     unsigned long long* __restrict__ ks) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_classify(
+    Soa S, int64_t n, Level L, const uint32_t* __restrict__ grid, StepIO io, EpQueue q, Work w,
+    int64_t g0, unsigned long long* __restrict__ stats, uint32_t* __restrict__ err_or,
+    unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
   __shared__ int bcnt[NLIST], bbase[NLIST];
   // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
   // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
-  // keeps 8 waves per SIMD
   __shared__ union {
     LdsLevel lv;
     double ostage[BLOCK * 9];
