@@ -815,6 +815,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
   __shared__ int bcnt[NLIST], bbase[NLIST];
+  __shared__ int rwc[BLOCK / 64], rbase;  // stale halves per wave; the workgroup's list range
   // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
   // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
   __shared__ union {
@@ -865,19 +866,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   // regenerates the lists of several steps at once (a lane that needs a half first does it
   // itself: the ring leaves >= ~2,400 draws of slack, launch_step)
   // (dense lists: a drain of a few steps' lists spreads one half per wave, where the per-wave
-  // regions of round 4 left a wave with the few regions holding 3-4 halves for ~0.1 ms)
+  // regions of round 4 left a wave with the few regions holding 3-4 halves for ~0.1 ms; one
+  // atomic per workgroup, beside the worklists' below: per wave, ~2,000 returning atomics per
+  // counter and step at the masked policy's rate serialised k_classify, 30.8 -> 39.2 us)
+  const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
+  int srank = 0;
   {
-    const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
     const unsigned long long b = __ballot(stale);
-    if (b) {
-      const int shard = (int)(blockIdx.x % SHARDS);
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&w.rcnt[shard * CTR_STRIDE], __popcll(b));
-      base = __builtin_amdgcn_readlane(base, 0);
-      if (stale)
-        w.refill[shard * w.rcap + base + __popcll(b & ((1ull << lane) - 1ull))] =
-            (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
-    }
+    srank = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) rwc[threadIdx.x >> 6] = __popcll(b);
     if (stale) e.mti |= MT_LISTED;
   }
   // workgroup-local slots: one LDS atomic per wave and option present in the wave (the
@@ -904,6 +901,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   if (threadIdx.x < NLIST) {
     const int c = bcnt[threadIdx.x];
     my_base = c ? atomicAdd(&w.ctr[(kSegBase[threadIdx.x] + shard) * CTR_STRIDE], c) : 0;
+  } else if (threadIdx.x == 64) {  // (another wave than the worklists' atomics)
+    int c = 0;
+#pragma unroll
+    for (int v = 0; v < BLOCK / 64; ++v) c += rwc[v];
+    my_base = c ? atomicAdd(&w.rcnt[shard * CTR_STRIDE], c) : 0;
   }
   const uint4 s4w = pack(e);  // the state the worklist copy carries (listed half, E_ACTION)
 
@@ -930,7 +932,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (ep.x != ep_in.x || ep.y != ep_in.y) S.ep[i] = ep;
   }
   if (threadIdx.x < NLIST) bbase[threadIdx.x] = my_base;
+  if (threadIdx.x == 64) rbase = my_base;
   __syncthreads();
+  if (stale) {
+    int at = rbase + srank;
+    for (int v = 0; v < (int)(threadIdx.x >> 6); ++v) at += rwc[v];
+    w.refill[shard * w.rcap + at] = (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
+  }
   if (bk >= 0) {
     const int64_t at = (int64_t)(kSegBase[bk] + shard) * w.shard_cap + bbase[bk] + slot;
     w.lists[at] = (int32_t)i;
