@@ -317,7 +317,8 @@ def test_modes_identical_full_outputs(tg):
 CORRIDOR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", "corridor")
 
 
-@pytest.mark.parametrize("level,n,steps", [(None, 1 << 16, 80), (None, 192, 80), ("corridor", 192, 40)])
+@pytest.mark.parametrize("level,n,steps", [(None, 1 << 16, 80), (None, 192, 80), (None, 1000, 64),
+                                             ("corridor", 192, 40)])
 def test_deferred_regeneration_is_invisible(tg, level, n, steps):
     """k_regen drains the listed stale MT halves every 16 compact steps; when it runs must not
     matter.  The same batch stepped with the automatic drains only, and with tg_regenerate
