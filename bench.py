@@ -57,6 +57,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ACTION_SEED = 0x5EED0001
 PREGEN_BYTES = 8 << 30  # pre-generated action rows for the timed steps, at most this much HBM
 EP_CAP = 4096          # episode records gathered per rank per step of a drain interval (padded)
+KST_MAX = 512          # step launches whose kernel spans the library records (tg_amd.hip)
 # algorithmic bytes of one tg_step for THIS data layout, per kernel:
 #   k_classify, every env: action 4 + state word 16 + angles 16 + episode 8 read (44)
 #     reward-None env: obs 72 + reward/valid/done 6 written (78; its episode word holds the
@@ -371,6 +372,7 @@ class Runner:
                 tg._lib.check(L.tg_set_groups(h, args.groups, 1 if args.stagger else 0),
                               "tg_set_groups")
         self.frames, self.rev, self.timing, self.render_on = None, [], False, True
+        self.timing_every = args.timing_every
         if args.workload == "c5":  # ObservationWrapper.step: render every env after its step
             vec.render_init(tg.synthetic_sprites(seed=1))
             self.frames = torch.empty((count,) + vec.frame_shape, dtype=torch.uint8, device=dev)
@@ -482,7 +484,12 @@ class Runner:
         self.log.reset()
         vec = self.vec
         vec.stats_reset()
-        vec.set_timing(self.args.timing_every)
+        # the library keeps KST_MAX = 512 step records and would flush (a device sync and a
+        # copy) inside the timed region past them: sample every k-th step so that the timed
+        # steps' records fit
+        self.timing_every = (max(self.args.timing_every, -(-steps // KST_MAX))
+                             if self.args.timing_every else 0)
+        vec.set_timing(self.timing_every)
         self.timing = True
         if self.world > 1:
             dist.barrier()
@@ -617,7 +624,7 @@ def step_line(args, runner, dt, st, node, world, total):
             "timed_launches": st["timed_launches"],
             "timing": "every %d-th timed step: the kernel's span from its first wave's start to "
                       "its last wave's end (in-kernel s_memrealtime stamps); HIP events on the "
-                      "step's stream around the timed region (events_ms)" % args.timing_every,
+                      "step's stream around the timed region (events_ms)" % runner.timing_every,
             "rocprof_ms": run_k.get("rocprof_ms"),
             "limiter": run_k.get("limiter"), "valu_util": run_k.get("valu_util"),
             "wait_frac": run_k.get("wait_frac"), "lane_efficiency": lane_eff,
@@ -655,12 +662,12 @@ def step_line(args, runner, dt, st, node, world, total):
                     "events_ms_per_step": runner.events_ms / args.steps,
                     "host_ms": runner.host_ms,
                     "gaps_ms": ms_step - all_s * 1e3,
-                    "achieved": all_b / all_s / 1e9,
-                    "frac": all_b / all_s / 1e9 / HBM_PEAK_GBS,
+                    "achieved": all_b / all_s / 1e9 if all_s else None,
+                    "frac": all_b / all_s / 1e9 / HBM_PEAK_GBS if all_s else None,
                     "frac_wall": all_b / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS,
                     "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                     "alg_bytes_per_launch_survey": surv,
-                    "frac_survey": surv / all_s / 1e9 / HBM_PEAK_GBS,
+                    "frac_survey": surv / all_s / 1e9 / HBM_PEAK_GBS if all_s else None,
                     "frac_survey_wall": surv / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS,
                     "kernels": kernels}
     return {

@@ -162,18 +162,31 @@ static_assert(WIN_WAVE_BYTES >= WAVE_SCRATCH, "wave_refill reuses the window as 
 static_assert(WIN_DRAWS - WIN_UNIT + 1 >= (int)MAX_TICK_DRAWS, "a refilled window holds a tick's draws");
 
 // LDS-DMA of one WIN_UNIT-byte unit per active lane into LDS [m0 + lane * WIN_UNIT]; M0 is
-// saved/restored
+// saved/restored.  SC1: the load bypasses this CU's L1 (k_flow, whose codes another CU of the
+// XCD may have rewritten in the same launch: tg_flow.h)
+template <bool SC1 = false>
 __device__ __forceinline__ void glds_unit(uint32_t m0, const void* gptr) {
   uint32_t save;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(save)
-      : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
-      : "memory");
+  if constexpr (SC1)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, off sc1\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(save)
+        : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(save)
+        : "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(gptr)
+        : "memory");
 }
 
 // the rare second crossing (RngCodes::fill), out of line so that the draw sites stay small, its
@@ -189,8 +202,31 @@ __device__ __noinline__ void regen_half(uint32_t* mt, uint8_t* mc, uint32_t h) {
   twist_half(mt, h, mc, false, GenCalls());
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
 }
+// k_flow's form: the half's source words may have been written by another CU of the XCD in the
+// same launch (the env's previous item ran there), so this CU's L1 is invalidated first (an
+// agent-scope acquire, ~2 us on this rare path); the stores reach the XCD's L2, where the env's
+// next item, on whichever CU, reads them (tg_flow.h)
+__device__ __noinline__ void regen_half_flow(uint32_t* mt, uint8_t* mc, uint32_t h) {
+  asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+  twist_half(mt, h, mc, false, GenCalls());
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+}
 
-struct RngCodes {
+// a stored MT word read past this CU's L1 (an agent-scope relaxed load: global_load sc1), for
+// k_flow, where another CU of the XCD may have rewritten it in the same launch (tg_flow.h)
+struct Sc1Ld {
+  __device__ uint32_t operator()(const uint32_t* p) const {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+__device__ __noinline__ WordPair mt_pair_ool_sc1(const uint32_t* mt, uint32_t p) {
+  WordPair r;
+  mt_pair(mt, p, r.w0, r.w1, Sc1Ld());
+  return r;
+}
+
+template <bool FLOW = false>  // FLOW: k_flow's L1-bypassing loads (tg_flow.h)
+struct RngCodesT {
   static constexpr uint32_t NONE = 0xFFFFFFFFu;
   uint32_t* mt;      // this env's MT_STORE stored words (HBM)
   uint8_t* mc;       // this env's MT_CODES code bytes (HBM)
@@ -207,7 +243,7 @@ struct RngCodes {
   uint32_t regens;   // halves this lane regenerated itself (regen_half)
   bool primed, loaded, entered;  // entered: a half was entered in this launch (as tg::Rng)
 
-  __device__ __forceinline__ RngCodes(uint32_t* m, uint8_t* c, uint32_t state, lds_u8* wave_win)
+  __device__ __forceinline__ RngCodesT(uint32_t* m, uint8_t* c, uint32_t state, lds_u8* wave_win)
       : mt(m), mc(c), cell(wave_win + (threadIdx.x & 63) * WIN_UNIT),
         m0(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)wave_win)),
         pos(state & MT_POS_MASK), n(0u), rd(0u), left(0u), nxc(0u),
@@ -224,7 +260,8 @@ struct RngCodes {
     if (e / (MT_HALF / 2) != d / (MT_HALF / 2)) {
       const uint32_t left_half = mt_half(pos), entered_half = (uint32_t)MT_HALF - left_half;
       if (stale == entered_half) {
-        regen_half(mt, mc, entered_half);
+        if (FLOW) regen_half_flow(mt, mc, entered_half);
+        else regen_half(mt, mc, entered_half);
         ++regens;
       }
       stale = left_half;
@@ -243,7 +280,8 @@ struct RngCodes {
       const uint32_t w0 = pos, w1 = pos + 2u * ((uint32_t)WIN_DRAWS - d % (uint32_t)WIN_UNIT);
       if ((w0 < stale + (uint32_t)MT_HALF && stale < w1) ||
           (w1 > (uint32_t)MT_WORDS && stale < w1 - (uint32_t)MT_WORDS)) {
-        regen_half(mt, mc, stale);
+        if (FLOW) regen_half_flow(mt, mc, stale);
+        else regen_half(mt, mc, stale);
         ++regens;
         stale = NONE;
       }
@@ -251,7 +289,7 @@ struct RngCodes {
 #pragma unroll
     for (int j = 0; j < WIN_SLOTS; ++j) {
       const uint32_t c = c0 + j < CODE_UNITS ? c0 + j : c0 + j - CODE_UNITS;
-      glds_unit(m0 + j * WIN_SLOT_BYTES, mc + c * (uint32_t)WIN_UNIT);
+      glds_unit<FLOW>(m0 + j * WIN_SLOT_BYTES, mc + c * (uint32_t)WIN_UNIT);
     }
     rd = d % (uint32_t)WIN_UNIT;
     left = (uint32_t)WIN_DRAWS - rd;
@@ -356,7 +394,7 @@ struct RngCodes {
     uint32_t p = (pos >> 1) + n;
     p = 2u * (p >= (uint32_t)MT_CODES ? p - (uint32_t)MT_CODES : p);
     (void)code();
-    const WordPair w = mt_pair_ool(mt, p);
+    const WordPair w = FLOW ? mt_pair_ool_sc1(mt, p) : mt_pair_ool(mt, p);
     return mt_double(w.w0, w.w1);
   }
   __device__ __forceinline__ double uniform(double a, double b) { return a + (b - a) * random(); }
@@ -370,6 +408,8 @@ struct RngCodes {
     return pos | (stale == NONE ? 0u : entered ? MT_STALE : tag);
   }
 };
+
+using RngCodes = RngCodesT<false>;
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
@@ -566,7 +606,8 @@ struct EpQueue {
 // unsigned.  The records that do not fit are counted per wave in the wave's own block slot.
 // Must be reached by every lane of the wave.
 __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, uint32_t tstep,
-                                                const EpQueue& q, unsigned long long* stats) {
+                                                const EpQueue& q, unsigned long long* stats,
+                                                int64_t sl) {  // sl: the wave's stats slot
   const unsigned long long b = __ballot(mine);
   if (!b) return;
   const int lane = threadIdx.x & 63;
@@ -579,7 +620,7 @@ __device__ __forceinline__ void record_episodes(bool mine, int64_t g, int2& ep, 
       atomicMin(q.count, q.cap);
       const uint32_t lost = (uint32_t)base >= (uint32_t)q.cap
                                 ? (uint32_t)cnt : (uint32_t)base + (uint32_t)cnt - (uint32_t)q.cap;
-      atomicAdd(&stats[(size_t)blockIdx.x * ST_COUNT + ST_EP_OVERFLOW], (unsigned long long)lost);
+      atomicAdd(&stats[(size_t)sl * ST_COUNT + ST_EP_OVERFLOW], (unsigned long long)lost);
     }
   }
   base = __shfl(base, first, 64);
@@ -728,7 +769,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
               S.mc + (live ? i : 0) * MT_CODES, e.mti,
               (lds_u32*)wscr);
   e.mti &= ~(MT_STALE | MT_LISTED);
-  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats);
+  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats, blockIdx.x);
   if (live) {
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
@@ -1072,7 +1113,9 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     lregen = (int)rng.regens;
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
-  if (AUTORESET) record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats);
+  // (k_run's grid has BLOCK / RUN_BLOCK workgroups per stats slot, as wave_stats below)
+  if (AUTORESET)
+    record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats, (int64_t)blockIdx.x / (BLOCK / RUN_BLOCK));
   if (live) {
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
@@ -1133,8 +1176,9 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
 // the same: MT_HALF_GENS twists), the rest from the list's counter.  An entry is regenerated iff
 // its env's state word still says MT_STALE (its lane may have regenerated the half itself, or
 // crossed again since): the half not holding the position, from the last generation of the one
-// holding it; then the word loses MT_STALE | MT_LISTED.  It runs alone on the stream, so
-// nothing else touches the state.
+// holding it.  The word loses MT_STALE | MT_LISTED by an atomic AND before the twist (the
+// claim: of several entries for one env, one regenerates).  It runs alone on the stream, so
+// nothing else touches the state meanwhile.
 // Slack: a listed half is needed again only after the env consumes the rest of the half it is
 // in, >= MT_HALF / 2 - (one step's draws) ~ 2,400 draws, more than REGEN_STEPS steps draw on the
 // default level (<= ~110 per step); a lane that gets there first regenerates the half itself.
@@ -1181,7 +1225,13 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
     if (j0 >= cnt) break;
     const int64_t m = cnt - j0 < grab ? cnt - j0 : grab;
     const uint32_t env_l = lane < m ? list[j0 + lane] & 0x7FFFFFFFu : 0u;
-    const uint32_t st_l = lane < m ? st_w[(int64_t)env_l * 4 + 3] : 0u;
+    // claim: clear MT_STALE | MT_LISTED and regenerate only if this lane's clear found
+    // MT_STALE.  An env can be listed twice before a drain (its lane regenerated the listed
+    // half itself, crossed again, and the next k_classify listed the new stale half): both
+    // entries name the half not holding the position, and the second claim finds it clean
+    // (round 4 regenerated such a half once per entry: 20,320 vs 15,360 halves on the corridor
+    // level).  Entries of one grab for one env are serialised at the word's L2 channel.
+    const uint32_t st_l = lane < m ? atomicAnd(&st_w[(int64_t)env_l * 4 + 3], ~(MT_STALE | MT_LISTED)) : 0u;
     unsigned long long need = __ballot(lane < m && (st_l & MT_STALE));
     // one half at a time: 52 VGPRs, 8 waves per SIMD (the next half's source loads pipelined
     // into this one's twist took 76 VGPRs, 6 waves, and measured no faster: DESIGN.md §3.3)
@@ -1194,7 +1244,6 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
       twist_load(src_of(env, s), t);
       twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_STORE), S.mc + (int64_t)env * MT_CODES,
                   (int)(dst / (uint32_t)MT_N), MT_HALF_GENS, true, scr);
-      if (lane == 0) st_w[(int64_t)env * 4 + 3] = s & ~(MT_STALE | MT_LISTED);
       ++halves;
     }
   }

@@ -198,14 +198,19 @@ TG_HD void twist_gen_inplace(uint32_t* w) { twist_gen(w, w); }
 // new word j0 = i - 227 d (< 227, which reads old words only).  The chain's old words are at
 // fixed offsets from j0 and all load unconditionally (indices clamped into the generation):
 // one memory round trip, and no divergence between lanes of different chain lengths.
-TG_HD uint32_t twist_at_lo(const uint32_t* g, int i) {
+// (Ld: how a stored word is read — plain, or k_flow's L1-bypassing load, tg_amd.hip)
+struct PlainLd {
+  TG_HD uint32_t operator()(const uint32_t* p) const { return *p; }
+};
+template <class Ld = PlainLd>
+TG_HD uint32_t twist_at_lo(const uint32_t* g, int i, const Ld& ld = Ld()) {
   constexpr int K = MT_N - MT_M;  // 227
   const int d = i >= 2 * K ? 2 : i >= K ? 1 : 0;
   const int j0 = i - K * d;
   const int c2 = j0 + 2 * K < MT_N - 1 ? j0 + 2 * K : MT_N - 2;
-  const uint32_t a0 = g[j0], b0 = g[j0 + 1], c0 = g[j0 + MT_M];
-  const uint32_t a1 = g[j0 + K], b1 = g[j0 + K + 1];
-  const uint32_t a2 = g[c2], b2 = g[c2 + 1];
+  const uint32_t a0 = ld(g + j0), b0 = ld(g + j0 + 1), c0 = ld(g + j0 + MT_M);
+  const uint32_t a1 = ld(g + j0 + K), b1 = ld(g + j0 + K + 1);
+  const uint32_t a2 = ld(g + c2), b2 = ld(g + c2 + 1);
   uint32_t w = mt_twist(a0, b0, c0);
   const uint32_t w1 = mt_twist(a1, b1, w);
   w = d >= 1 ? w1 : w;
@@ -221,18 +226,19 @@ TG_HD uint32_t twist_at(const uint32_t* g, int i) {
 // are stored, an odd one's are twisted from the generation before it (the rare draws that need
 // their double).  Branch-free: every lane issues the loads of both cases (~20 words) at once,
 // so a wave whose lanes sit in even and odd generations pays one memory round trip, not two.
-TG_HD void mt_pair(const uint32_t* mt, uint32_t p, uint32_t& w0, uint32_t& w1) {
+template <class Ld = PlainLd>
+TG_HD void mt_pair(const uint32_t* mt, uint32_t p, uint32_t& w0, uint32_t& w1, const Ld& ld = Ld()) {
   const uint32_t g = p / (uint32_t)MT_N, i = p - g * (uint32_t)MT_N;  // i even, <= 622
   const uint32_t* const cur = mt + mt_store_off(g & ~1u);  // g's own words if g is even
   const uint32_t* const prev = mt + mt_store_off(g == 0u ? 0u : (g - 1u) & ~1u);
-  const uint32_t e0 = cur[i], e1 = cur[i + 1];
-  const uint32_t o0 = twist_at_lo(prev, (int)i);
+  const uint32_t e0 = ld(cur + i), e1 = ld(cur + i + 1);
+  const uint32_t o0 = twist_at_lo(prev, (int)i, ld);
   // word i + 1: a chain of its own, or, for i + 1 = 623, the twist of old word 623 with new
   // words 0 and 396
   const bool last = i + 1u == (uint32_t)MT_N - 1u;
-  const uint32_t x = twist_at_lo(prev, last ? MT_M - 1 : (int)i + 1);
-  const uint32_t y0 = twist_at_lo(prev, 0);
-  const uint32_t o1 = last ? mt_twist(prev[MT_N - 1], y0, x) : x;
+  const uint32_t x = twist_at_lo(prev, last ? MT_M - 1 : (int)i + 1, ld);
+  const uint32_t y0 = twist_at_lo(prev, 0, ld);
+  const uint32_t o1 = last ? mt_twist(ld(prev + MT_N - 1), y0, x) : x;
   w0 = (g & 1u) ? o0 : e0;
   w1 = (g & 1u) ? o1 : e1;
 }
@@ -1440,6 +1446,44 @@ TG_HD int ladder_tick(const Level& L, const Map& m, const LadMasks& lm, Env& e, 
   return -1;  // STEP_REWARD
 }
 
+// The ladder options' while-not-done loop (OP/:28-31): a plain phase (ladder_plain_limit's
+// span; one draw and py += noisy per tick, as the full tick there), then one full tick, which
+// may open the next span.  One loop for both probe forms (two copies of the
+// plain-tick / full-tick / TICK_CAP control flow): `pr` gives the span's predicates (cell probes
+// or the level bitmasks), `full()` the full tick (policy<K> + tick<>, or ladder_tick).  (A
+// batched walk here, RngCodes::walk, took k_run from 82 to 98 VGPRs: 4 instead of 5 waves per
+// SIMD.)
+template <int DIR, class R, class P, class Full>
+TG_HD void ladder_loop(const Level& L, const Map& m, Env& e, Opt& o, R& rng, StepResult& r,
+                       const P& pr, Full full) {
+  int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
+  do {
+    rng.phase(0);
+    bool capped = false;
+    while ((DIR > 0 ? e.py <= lim : e.py >= lim) && rng.has(TICK_DRAWS)) {
+      e.py += code_step(rng.code(), DIR < 0);
+      r.reward += -1;
+      if (DIR > 0 ? e.py > lim : e.py < lim) pickups(L, e);  // left the span: as the full tick
+      if (++r.ticks >= TICK_CAP) {
+        e.f |= E_TICKCAP;
+        capped = true;
+        lim = DIR > 0 ? -0x40000000 : 0x40000000;
+      }
+    }
+    if (capped) break;
+    rng.phase(1);
+    rng.reserve(TICK_DRAWS);
+    rng.phase(2);
+    r.reward += full();
+    if (!o.done) lim = ladder_plain_limit<DIR>(m, e, pr);
+    rng.phase(3);
+    if (++r.ticks >= TICK_CAP) {
+      e.f |= E_TICKCAP;
+      break;
+    }
+  } while (!o.done);
+}
+
 // the while-not-done loop of _Option.run (OP/:28-31) for option K, whose can_run held
 template <int K, class R>
 TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env& e, R& rng,
@@ -1486,67 +1530,16 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
   }
   if constexpr (K == O_UP_LADDER || K == O_DOWN_LADDER) {
     constexpr int DIR = K == O_UP_LADDER ? -1 : 1;
-    int lim = DIR > 0 ? -0x40000000 : 0x40000000;  // no plain tick before the first full one
     if (m.mk) {  // the level bitmasks: full ticks and span limits test bits, no cell probes
       const LadMasks lm(m, Map::dc_of(e.f), e.px);
-      const LadProbeMk pr{m, lm};
-      do {
-        rng.phase(0);
-        bool capped = false;
-        while ((DIR > 0 ? e.py <= lim : e.py >= lim) && rng.has(TICK_DRAWS)) {
-          e.py += code_step(rng.code(), DIR < 0);
-          r.reward += -1;
-          if (DIR > 0 ? e.py > lim : e.py < lim) pickups(L, e);
-          if (++r.ticks >= TICK_CAP) {
-            e.f |= E_TICKCAP;
-            capped = true;
-            lim = DIR > 0 ? -0x40000000 : 0x40000000;
-          }
-        }
-        if (capped) break;
-        rng.phase(1);
-        rng.reserve(TICK_DRAWS);
-        rng.phase(2);
-        r.reward += ladder_tick<DIR>(L, m, lm, e, o, rng);
-        if (!o.done) lim = ladder_plain_limit<DIR>(m, e, pr);
-        rng.phase(3);
-        if (++r.ticks >= TICK_CAP) {
-          e.f |= E_TICKCAP;
-          break;
-        }
-      } while (!o.done);
+      ladder_loop<DIR>(L, m, e, o, rng, r, LadProbeMk{m, lm},
+                       [&]() { return ladder_tick<DIR>(L, m, lm, e, o, rng); });
       return;
     }
-    const LadProbe pr{m, e};
-    do {
-      // plain phase (ladder_plain_limit), then one full tick: as the go loops
-      // per tick (a batched walk here, RngCodes::walk, took k_run from 82 to 98 VGPRs: 4
-      // instead of 5 waves per SIMD)
-      rng.phase(0);
-      bool capped = false;
-      while ((DIR > 0 ? e.py <= lim : e.py >= lim) && rng.has(TICK_DRAWS)) {
-        e.py += code_step(rng.code(), DIR < 0);
-        r.reward += -1;
-        if (DIR > 0 ? e.py > lim : e.py < lim) pickups(L, e);  // left the span: as the full tick
-        if (++r.ticks >= TICK_CAP) {
-          e.f |= E_TICKCAP;
-          capped = true;
-          lim = DIR > 0 ? -0x40000000 : 0x40000000;
-        }
-      }
-      if (capped) break;
-      rng.phase(1);
-      rng.reserve(TICK_DRAWS);
-      rng.phase(2);
+    ladder_loop<DIR>(L, m, e, o, rng, r, LadProbe{m, e}, [&]() {
       const int prim = policy<K>(L, m, e, o);
-      r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);
-      if (!o.done) lim = ladder_plain_limit<DIR>(m, e, pr);
-      rng.phase(3);
-      if (++r.ticks >= TICK_CAP) {
-        e.f |= E_TICKCAP;
-        break;
-      }
-    } while (!o.done);
+      return tick<prims_of(K), R>(L, trig, m, e, prim, rng);
+    });
     return;
   }
   if constexpr (K == O_JUMP_LEFT || K == O_JUMP_RIGHT || K == O_DOWN_LEFT || K == O_DOWN_RIGHT) {
