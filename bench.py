@@ -75,6 +75,7 @@ KST_MAX = 512          # step launches whose kernel spans the library records (t
 MT_HALF_GENS = 8
 CLS_ENV, CLS_INVALID, CLS_VALID, CLS_REGEN = 44, 78, 44, 4 / MT_HALF_GENS
 RUN_VALID, RUN_DRAW = 162, 1
+FLOW_VALID = 4  # k_flow (TG_MODE_FLOW): a valid env's list entry (its state is not copied)
 DIRECT_ENV, DIRECT_INVALID, DIRECT_VALID = 44, 78, 118
 # per generation regenerated, set by set_layout from the loaded library (round 3's layout, which
 # stored every generation's words, lacks tg_mt_layout)
@@ -111,7 +112,10 @@ def alg_bytes(st, mode="compact"):
         return 0, (DIRECT_ENV * st["steps"] + DIRECT_INVALID * inval +
                    DIRECT_VALID * st["valid_steps"] + BYTES_DRAW * st["draws"] +
                    DIRECT_REGEN * st["regens"]), 0
-    cls = (CLS_ENV * st["steps"] + CLS_INVALID * inval + CLS_VALID * st["valid_steps"] +
+    # flow: k_flow's lists carry the 4-B env index, its option waves gather the 40 B of state
+    # from the env arrays (the same 162 B per valid env as k_run's 44-B worklist row + 118)
+    cls = (CLS_ENV * st["steps"] + CLS_INVALID * inval +
+           (FLOW_VALID if mode == "flow" else CLS_VALID) * st["valid_steps"] +
            CLS_REGEN * st["regens"])
     run = RUN_VALID * st["valid_steps"] + RUN_DRAW * st["draws"]
     return cls, run, REGEN_GEN * st["regens"]
@@ -139,8 +143,10 @@ def parse(argv=None):
                     help="a level directory in the reference's three-file format (default: the "
                          "reference's own level)")
     ap.add_argument("--no-autoreset", action="store_true")
-    ap.add_argument("--mode", default="compact", choices=["compact", "direct"],
-                    help="step implementation (bit-identical): two-pass compacted or one-pass")
+    ap.add_argument("--mode", default="compact", choices=["compact", "direct", "flow"],
+                    help="step implementation (bit-identical): two-pass compacted, one-pass, or "
+                         "flow (with --rollout: k_flow, chunks advancing without a batch-wide "
+                         "barrier between steps, DESIGN.md 9.2)")
     ap.add_argument("--run-blocks", type=int, default=0, help="k_run workgroups (0 = default)")
     ap.add_argument("--rollout", type=int, default=0,
                     help="K > 0: tg_rollout, K steps per call with the policy evaluated inside "
@@ -581,6 +587,9 @@ def step_line(args, runner, dt, st, node, world, total):
     run_s = st["run_ms"] / 1e3 / timed          # k_run's span (k_step's in the direct mode)
     cls_s = st["classify_ms"] / 1e3 / timed     # k_classify's span
     cls_b, run_b, regen_b = (b / launches for b in alg_bytes(st, args.mode))
+    flow = args.mode == "flow" and args.rollout > 0
+    if flow:  # one kernel does both passes; its span per step is its launch's / K (run_ms)
+        cls_b, run_b = 0.0, cls_b + run_b
     if args.rollout and args.groups > 1:  # the spans are group 0's kernels: its share
         cls_b, run_b, regen_b = cls_b / args.groups, run_b / args.groups, regen_b / args.groups
     rl = st.get("regen_launches", 0)
@@ -594,7 +603,7 @@ def step_line(args, runner, dt, st, node, world, total):
     lane_eff = node["ticks"] / max(64 * node["wave_ticks"], 1)
     pmc = load_pmc(args.traffic_json, args.envs, args.policy_used, args.mode, regens,
                    args.burn_in_used)
-    run_name = "k_run" if args.mode == "compact" else "k_step"
+    run_name = "k_flow" if flow else "k_run" if args.mode != "direct" else "k_step"
     kp = pmc.get("kernels", {}) if pmc else {}
     run_pmc = next((v for k, v in kp.items() if k.split("<")[0] == run_name), None)
     cls_pmc = next((v for k, v in kp.items() if k.split("<")[0] == "k_classify"), None)
@@ -634,8 +643,9 @@ def step_line(args, runner, dt, st, node, world, total):
                     "(the MT regeneration is k_regen's: step.kernels.regen; the whole step: "
                     "step.frac) (DESIGN.md 3.6)"}
     kernels = {"run": run_k}
-    if args.mode == "compact":
-        kernels["classify"] = kern("k_classify", cls_b, cls_s, cls_pmc)
+    if args.mode != "direct":
+        if not flow:
+            kernels["classify"] = kern("k_classify", cls_b, cls_s, cls_pmc)
         if rl:
             regen_pmc = next((v for k, v in kp.items() if k.split("<")[0] == "k_regen"), None)
             gens_launch = st["regens"] / rl  # MT generations regenerated per k_regen launch
@@ -656,8 +666,9 @@ def step_line(args, runner, dt, st, node, world, total):
     all_b, all_s = cls_b + run_b + regen_b, cls_s + run_s + regen_s
     ms_step = dt / args.steps * 1e3
     roof["step"] = {"kernel": "tg_step = " + (" + ".join(
+                        ["k_flow / steps per launch", "k_regen / steps per launch"] if flow else
                         ["k_classify", "k_run", "k_regen / steps per launch"]
-                        if args.mode == "compact" else ["k_step"])),
+                        if args.mode != "direct" else ["k_step"])),
                     "alg_bytes_per_launch": all_b, "kernel_ms": all_s * 1e3,
                     "events_ms_per_step": runner.events_ms / args.steps,
                     "host_ms": runner.host_ms,

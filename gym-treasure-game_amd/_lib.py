@@ -17,12 +17,14 @@ TG_POLICY_UNIFORM = 0
 TG_POLICY_MASKED = 1
 TG_MODE_DIRECT = 0
 TG_MODE_COMPACT = 1
+TG_MODE_FLOW = 2
 TG_ERR_TICKCAP = 1 << 24
 TG_ERR_BAG = 1 << 25
 TG_ERR_ACTION = 1 << 26
 TG_ERR_NEARINT = 1 << 27
 TG_ERR_RENDER = 1 << 28
 TG_ERR_WINDOW = 1 << 29
+TG_ERR_FLOW = 1 << 30
 TG_SPR_COUNT = 24
 OBS_DIM = 9
 NUM_ACTIONS = 9
@@ -33,7 +35,7 @@ EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_
            "tg_available_mask",
            "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing", "tg_regenerate",
            "tg_set_episode_capacity", "tg_predicate_table",
-           "tg_get_stats", "tg_stats_reset", "tg_kernel_info", "tg_mt_layout", "tg_read_state", "tg_write_state", "tg_render_init", "tg_frame_shape",
+           "tg_get_stats", "tg_stats_reset", "tg_kernel_info", "tg_mt_layout", "tg_probe_dispatch", "tg_read_state", "tg_write_state", "tg_render_init", "tg_frame_shape",
            "tg_render", "tg_last_error", "tg_version")
 
 
@@ -105,6 +107,7 @@ def load():
         "tg_stats_reset": (i32, [P]),
         "tg_set_groups": (i32, [P, i32, i32]),
         "tg_mt_layout": (i32, [ctypes.POINTER(ctypes.c_int32)] * 3),
+        "tg_probe_dispatch": (i32, [i32, i32, P]),
         "tg_kernel_info": (i32, [P, i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                  ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
         "tg_read_state": (i32, [P, P, P, P, P, P, P, P]),

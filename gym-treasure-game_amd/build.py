@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f) for f in ("tg_amd.hip", "tg_render.hip")]
 DEPS = SRCS + [os.path.join(HERE, "csrc", f) for f in ("tg_core.h", "tg_level.h", "tg_batch.h",
-                                                        "tg_render.h")] + [
+                                                        "tg_render.h", "tg_twist.h", "tg_flow.h")] + [
     os.path.join(os.path.dirname(HERE), "include", "tg_amd.h")]
 OUT = os.path.join(HERE, "libtg_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
+#include <unistd.h>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -209,7 +211,9 @@ __device__ __noinline__ void regen_half(uint32_t* mt, uint8_t* mc, uint32_t h) {
 __device__ __noinline__ void regen_half_flow(uint32_t* mt, uint8_t* mc, uint32_t h) {
   asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   twist_half(mt, h, mc, false, GenCalls());
-  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+  // its words and codes out of this CU (the env's next items may run on another CU of the XCD)
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_wbl2 sc1\n\ts_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\t"
+               "s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // a stored MT word read past this CU's L1 (an agent-scope relaxed load: global_load sc1), for
@@ -673,7 +677,9 @@ __device__ __forceinline__ Level level_div(const Level& L) {
   d.obs_q = nullptr;
   return d;
 }
-template <bool AUTORESET, bool FINAL, class R>
+// VALID: the valid row is this call's (k_classify writes every env's valid row itself, coalesced:
+// k_run's scattered byte store cost a 32-B write granule per listed env)
+template <bool AUTORESET, bool FINAL, bool VALID = true, class R>
 __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int64_t i,
                                             const StepResult& r, int2& ep, const StepIO& io,
                                             double* keep = nullptr) {
@@ -681,7 +687,7 @@ __device__ __forceinline__ void finish_step(const Level& L, Env& e, R& rng, int6
   double o[9];
   observe(L, e, o);  // get_state (TG/:94)
   io.reward[i] = r.reward;
-  io.valid[i] = (uint8_t)r.ran;
+  if (VALID) io.valid[i] = (uint8_t)r.ran;
   io.done[i] = (uint8_t)r.done;
   ep.x += r.reward;  // (ep.y, the episode's start step, stays: no store for a reward-None step)
   if (FINAL) store_obs(io.final_obs, i, o);
@@ -900,6 +906,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     runs = k >= 0 && can_run(L, m, e, k);
     if (k < 0) e.f |= E_ACTION;
   }
+  // every env's valid row, coalesced (reward None unless its option runs; k_run writes the
+  // listed envs' other rows)
+  if (live) io.valid[i] = (uint8_t)runs;
   // entering done with auto-reset on and no option to run: reset in k_run (L_RESET)
   const bool rst = AUTORESET && live && !runs && is_done(e);
   const int bk = runs ? k : rst ? L_RESET : -1;  // the env's worklist
@@ -958,7 +967,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     e.ang1 = a2.y;
     Rng rng(S.mt + i * MT_STORE, e.mti, S.mc + i * MT_CODES);  // no draws without a reset
     StepResult r{0, 0, (int)is_done(e), 0};
-    finish_step<false, FINAL>(L, e, rng, i, r, ep, io, orow);
+    finish_step<false, FINAL, false>(L, e, rng, i, r, ep, io, orow);
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   const int2 ep_in = ep;
@@ -1107,7 +1116,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     ph1 = rng.ph[1], ph2 = rng.ph[2], ph3 = rng.ph[3], prounds = rng.rounds;
 #endif
     r.done = is_done(e);
-    finish_step<AUTORESET, FINAL>(level_div(L), e, rng, i, r, ep, io);
+    finish_step<AUTORESET, FINAL, false>(level_div(L), e, rng, i, r, ep, io);  // valid: k_classify's
     e.mti = rng.finish();  // a half left here: MT_STALE, listed by the next k_classify
     draws = rng.draws;
     lregen = (int)rng.regens;
@@ -1253,6 +1262,8 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
               (unsigned long long)halves);
   kst_end(ks, kt0);
 }
+
+#include "tg_flow.h"
 
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
                                                  const uint32_t* __restrict__ grid,
@@ -1499,6 +1510,9 @@ __global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __re
   wave_stats(stats, lane == 0 && !RESET ? 1 : 0, r.ran, r.ticks, (int)draws, 0);
 }
 
+// tg_probe_dispatch: nothing (a dependent kernel boundary's cost alone)
+__global__ __launch_bounds__(BLOCK) void k_null() {}
+
 __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4, int64_t n,
                                                    uint32_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -1540,6 +1554,7 @@ int kst_reset(tg_batch* h) {  // every record to (no start, no end)
   HIP_TRY(hipDeviceSynchronize());
   h->kst_steps = 0;
   h->kst_regens = 0;
+  h->kst_k.clear();
   return TG_OK;
 }
 // a kernel record's span in ms (first wave start to last wave end; 0 if it never ran)
@@ -1562,7 +1577,7 @@ int flush_timing(tg_batch* h) {
     h->classify_ms_done += c;
     h->run_ms_done += r;
     h->kernel_ms_done += c + r;
-    ++h->timed_launches;
+    h->timed_launches += k < (int)h->kst_k.size() ? h->kst_k[(size_t)k] : 1;  // k_flow: K steps
   }
   for (int k = 0; k < h->kst_regens; ++k) {
     h->regen_ms_done += kst_span_ms(rec.data() + ((size_t)KST_MAX * 2 + k) * kr);
@@ -1579,6 +1594,7 @@ bool timing_begin(tg_batch* h, int& rc, unsigned long long*& ks0, unsigned long 
   ks0 = kst_step(h, h->kst_steps, 0);
   ks1 = kst_step(h, h->kst_steps, 1);
   ++h->kst_steps;
+  h->kst_k.push_back(1);
   return true;
 }
 
@@ -1617,6 +1633,10 @@ void free_ctx(StepCtx& c) {
   c = StepCtx{};
 }
 }  // namespace
+
+namespace {
+void flow_free(tg_batch* h);  // TG_MODE_FLOW's buffers (below)
+}
 
 extern "C" {
 
@@ -1723,6 +1743,7 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   render_free(h->rs);
+  flow_free(h);
   void* bufs[] = {h->grid, h->genrand, h->gotab, h->masks, h->obs_q, h->S.st4, h->S.ang, h->S.ep,
                   h->S.mt, h->S.mc, h->eps, h->eps_count, h->err, h->obs_scratch, h->kst};
   for (void* b : bufs)
@@ -1870,6 +1891,168 @@ int regen_all(tg_batch* h, hipStream_t st) {
     if (!rc) rc = launch_regen(h, c, st);
   return rc;
 }
+
+// ---- TG_MODE_FLOW (tg_flow.h) ----------------------------------------------------------------
+void flow_free(tg_batch* h) {
+  auto& F = h->fl;
+  void* bufs[] = {F.ctl[0], F.ctl[1], F.q[0], F.q[1], F.fill[0], F.fill[1], F.list, F.outst};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  F = {};
+}
+// the XCD census (sub-problems) and the work structures, at the first flow rollout
+int flow_init(tg_batch* h) {
+  auto& F = h->fl;
+  if (F.ready) return TG_OK;
+  uint32_t* dmask = nullptr;
+  if (hipMalloc((void**)&dmask, sizeof(uint32_t)) != hipSuccess) return fail(TG_E_NOMEM, "flow census");
+  uint32_t mask = 0;
+  hipError_t e = hipMemset(dmask, 0, sizeof(uint32_t));
+  if (e == hipSuccess) {
+    // several workgroups per CU: every XCD of the device gets some (dispatch is round-robin)
+    hipLaunchKernelGGL(k_census, dim3((unsigned)(h->cus * 8)), dim3(64), 0, 0, dmask);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(&mask, dmask, sizeof mask, hipMemcpyDeviceToHost);
+  (void)hipFree(dmask);
+  if (e != hipSuccess) return fail(TG_E_HIP, "flow census: %s", hipGetErrorString(e));
+  mask &= 0xFFu;
+  F.P = 0;
+  F.xmap = 0xFFFFFFFFu;
+  for (int id = 0; id < 8; ++id)
+    if ((mask >> id) & 1u) F.xmap = (F.xmap & ~(0xFu << (4 * id))) | ((uint32_t)F.P++ << (4 * id));
+  if (F.P == 0) return fail(TG_E_HIP, "flow census: no XCC id in 0..7");
+  if (getenv("TG_FLOW_DEBUG")) fprintf(stderr, "[flow] census mask %08x P %d\n", mask, F.P);
+  const int64_t C = (h->n + 63) / 64, cxm = (C + F.P - 1) / F.P;
+  F.C = (int32_t)C;
+  F.lcap = cxm * 64;
+  F.jcap = cxm + 1;
+  F.qcap = (int64_t)FLOW_MAX_K * (cxm + NLIST);
+  const size_t nctl = (size_t)F.P * CTL_WORDS, nq = (size_t)F.P * F.qcap,
+               nfill = (size_t)F.P * FLOW_MAX_K * NLIST * F.jcap,
+               nlist = (size_t)F.P * FLOW_MAX_K * NLIST * F.lcap;
+  bool ok = true;
+  for (int k = 0; k < 2; ++k)
+    ok = ok && hipMalloc((void**)&F.ctl[k], sizeof(int32_t) * nctl) == hipSuccess &&
+         hipMalloc((void**)&F.q[k], sizeof(uint32_t) * nq) == hipSuccess &&
+         hipMalloc((void**)&F.fill[k], sizeof(int32_t) * nfill) == hipSuccess &&
+         hipMemset(F.ctl[k], 0, sizeof(int32_t) * nctl) == hipSuccess &&
+         hipMemset(F.q[k], 0xFF, sizeof(uint32_t) * nq) == hipSuccess &&
+         hipMemset(F.fill[k], 0, sizeof(int32_t) * nfill) == hipSuccess;
+  ok = ok && hipMalloc((void**)&F.list, sizeof(int32_t) * nlist) == hipSuccess &&
+       hipMalloc((void**)&F.outst, sizeof(int32_t) * (size_t)C) == hipSuccess;
+  if (!ok) {
+    flow_free(h);
+    return fail(TG_E_NOMEM, "flow work structures (%zu MB of lists)", nlist * 4 >> 20);
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  F.ready = true;
+  return TG_OK;
+}
+// k steps (<= FLOW_MAX_K) of the handle's own stepper in one k_flow launch; outputs at step s0
+// of the rollout's [K][N] arrays
+int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStream_t st) {
+  auto& F = h->fl;
+  StepCtx& c = h->main;
+  // the MT slack (k_regen every REGEN_STEPS steps): drain first if these steps would overrun it
+  if (c.rpend + k > REGEN_STEPS) {
+    const int rc = launch_regen(h, c, st);
+    if (rc) return rc;
+  }
+  decltype(&k_flow<true, 0>) kern = ar ? (pol ? k_flow<true, 1> : k_flow<true, 0>)
+                                       : (pol ? k_flow<false, 1> : k_flow<false, 0>);
+  int& bpc = F.bpc[ar ? 1 : 0][pol ? 1 : 0];
+  if (!bpc) {
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(kern), BLOCK, 0));
+    if (bpc < 1) bpc = 1;
+  }
+  unsigned long long* ks = nullptr;
+  if (h->timing_every && (h->timing_calls++ % (uint64_t)h->timing_every) == 0) {
+    if (h->kst_steps >= KST_MAX) {
+      const int rc = flush_timing(h);
+      if (rc) return rc;
+    }
+    ks = kst_step(h, h->kst_steps, 1);
+    ++h->kst_steps;
+    h->kst_k.push_back(k);
+  }
+  const int p = F.parity;
+  F.parity ^= 1;
+  Flow f{F.ctl[p], F.q[p], F.fill[p], F.list, F.outst, F.ctl[p ^ 1], F.q[p ^ 1], F.fill[p ^ 1],
+         c.refill, c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
+         F.qcap, F.jcap, F.lcap, F.C, F.P, k, F.xmap, nullptr, nullptr};
+#ifdef TG_FLOW_DBG
+  static uint32_t* dbg_host = nullptr;
+  static uint32_t* dbg_dev = nullptr;
+  if (!dbg_host) {
+    HIP_TRY(hipHostMalloc((void**)&dbg_host, 4096 * 4 * sizeof(uint32_t), hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&dbg_dev, dbg_host, 0));
+  }
+  memset(dbg_host, 0, 4096 * 4 * sizeof(uint32_t));
+  f.dbg = dbg_dev;
+  static uint32_t* dbgc = nullptr;
+  const size_t ndc = (size_t)F.C * 16 + 2 * (size_t)F.P * FLOW_MAX_K * NLIST * F.jcap;
+  if (!dbgc) HIP_TRY(hipMalloc((void**)&dbgc, sizeof(uint32_t) * ndc));
+  HIP_TRY(hipMemset(dbgc, 0, sizeof(uint32_t) * ndc));
+  f.dbgc = dbgc;
+#endif
+  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
+  if (getenv("TG_FLOW_DEBUG"))
+    fprintf(stderr, "[flow] launching k %d grid %d x %d lcap %lld qcap %lld jcap %lld C %d\n", k, h->cus, bpc,
+            (long long)F.lcap, (long long)F.qcap, (long long)F.jcap, F.C);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(h->cus * bpc)), dim3(BLOCK), 0, st, h->S, h->n, h->L,
+                     h->grid, io, q, f, h->g0, c.stats, stat_slots(h->n), h->err, ks);
+  HIP_TRY(hipGetLastError());
+  ++F.launches;
+#ifdef TG_FLOW_DBG
+  {  // watch the waves' progress for up to 8 s
+    for (int ms = 0; ms < 8000 && hipStreamQuery(st) == hipErrorNotReady; ms += 10) usleep(10000);
+    const bool hung = hipStreamQuery(st) == hipErrorNotReady;
+    int hist[64] = {0};
+    for (int w = 0; w < 4096; ++w) hist[dbg_host[w * 4] & 63]++;
+    fprintf(stderr, "[flowdbg] launch %lld %s; waves by code:", (long long)F.launches, hung ? "HUNG" : "done");
+    for (int c = 0; c < 64; ++c)
+      if (hist[c]) fprintf(stderr, " %d:%d", c, hist[c]);
+    fprintf(stderr, "\n");
+    int shown = 0;
+    for (int w = 0; w < 4090 && shown < 40; ++w) {
+      const uint32_t c = dbg_host[w * 4];
+      if (c && c != 9 && c != 1) {
+        fprintf(stderr, "[flowdbg]  wave %d code %u %u %u %u\n", w, c, dbg_host[w * 4 + 1], dbg_host[w * 4 + 2],
+                dbg_host[w * 4 + 3]);
+        ++shown;
+      }
+    }
+    for (int w = 4091; w < 4096; ++w)
+      if (dbg_host[w * 4])
+        fprintf(stderr, "[flowdbg]  DUP slot %d: code %u %u %08x %08x\n", w, dbg_host[w * 4], dbg_host[w * 4 + 1],
+                dbg_host[w * 4 + 2], dbg_host[w * 4 + 3]);
+    if (hung) {
+      fflush(stderr);
+      _exit(3);
+    }
+  }
+#endif
+  if (getenv("TG_FLOW_DEBUG")) {  // diagnostics: the census and every sub-problem's counters
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<int32_t> cw((size_t)F.P * CTL_WORDS);
+    HIP_TRY(hipMemcpy(cw.data(), F.ctl[p], sizeof(int32_t) * cw.size(), hipMemcpyDeviceToHost));
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpy(&err, h->err, sizeof err, hipMemcpyDeviceToHost));
+    fprintf(stderr, "[flow] launch %lld k %d P %d xmap %08x grid %d err %08x\n", (long long)F.launches,
+            k, F.P, F.xmap, h->cus * bpc, err);
+    for (int x = 0; x < F.P; ++x) {
+      const int32_t* c0 = cw.data() + (size_t)x * CTL_WORDS;
+      fprintf(stderr, "[flow]  x %d init %d qhead %d qtail %d fin %d done %d cls", x, c0[FC_INIT * FC_STRIDE],
+              c0[FC_QHEAD * FC_STRIDE], c0[FC_QTAIL * FC_STRIDE], c0[FC_FIN * FC_STRIDE], c0[FC_DONE * FC_STRIDE]);
+      for (int t = 0; t < k; ++t) fprintf(stderr, " %d", c0[(FC_CLS + t) * FC_STRIDE]);
+      fprintf(stderr, "\n");
+    }
+  }
+  c.rpend += k;
+  if (c.rpend >= REGEN_STEPS) return launch_regen(h, c, st);
+  return TG_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1998,7 +2181,19 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
                   reward + (size_t)s * n, valid + (size_t)s * n, done + (size_t)s * n,
                   nullptr, policy, action_seed, t0 + s};
   };
-  if (h->grp.empty() || h->mode == TG_MODE_DIRECT) {
+  if (h->grp.empty() && h->mode == TG_MODE_FLOW) {  // k_flow, up to FLOW_MAX_K steps per launch
+    int rc = flow_init(h);
+    for (int32_t s = 0; s < steps && !rc; s += FLOW_MAX_K) {
+      const int k = steps - s < FLOW_MAX_K ? steps - s : FLOW_MAX_K;
+      const FlowIO io{actions ? actions + (size_t)s * n : nullptr,
+                      obs ? obs + (size_t)s * n * 9 : h->obs_scratch, obs ? n * 9 : 0,
+                      reward + (size_t)s * n, valid + (size_t)s * n, done + (size_t)s * n,
+                      action_seed, t0 + s, tb + (uint32_t)s};
+      rc = launch_flow(h, k, io, ar, policy == TG_POLICY_MASKED ? 1 : 0, cs);
+    }
+    return rc;
+  }
+  if (h->grp.empty() || h->mode != TG_MODE_COMPACT) {
     for (int32_t s = 0; s < steps; ++s) {
       const int rc = launch_step(h, h->main, io_of(s), ar, cs, tb + (uint32_t)s);
       if (rc) return rc;
@@ -2126,7 +2321,7 @@ int tg_errors(tg_batch* h, uint32_t* out, void* stream) {
 
 int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
   BIND(h);
-  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT)
+  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT && mode != TG_MODE_FLOW)
     return fail(TG_E_INVAL, "tg_set_mode: unknown mode %d", mode);
   h->mode = mode;
   (void)run_blocks;  // reserved
@@ -2229,6 +2424,14 @@ int tg_stats_reset(tg_batch* h) {
   h->regen_ms_done = 0.0;
   h->regen_timed = 0;
   h->regen_launches = 0;
+  return TG_OK;
+}
+
+int tg_probe_dispatch(int32_t kernels, int32_t blocks, void* stream) {
+  if (kernels < 0 || blocks < 1) return fail(TG_E_INVAL, "tg_probe_dispatch: bad arguments");
+  for (int32_t k = 0; k < kernels; ++k)
+    hipLaunchKernelGGL(k_null, dim3((unsigned)blocks), dim3(BLOCK), 0, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
   return TG_OK;
 }
 

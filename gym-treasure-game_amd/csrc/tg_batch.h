@@ -120,6 +120,23 @@ struct tg_batch {
   tg_pystate py_last{};     // the state the last tg_*1_py call returned
   bool py_warm = false;     // pyc matches py_last
   tg::RenderState* rs = nullptr;   // tg_render_init
+  std::vector<int> kst_k;          // steps each in-use step record covers (a k_flow launch: K)
+  // TG_MODE_FLOW's work structures (tg_flow.h Flow; allocated at the first flow rollout)
+  struct {
+    bool ready = false;
+    int P = 0;                // sub-problems: the XCDs the census saw
+    uint32_t xmap = 0;        // XCC id -> sub-problem (nibbles)
+    int32_t C = 0;            // 64-env chunks
+    int64_t qcap = 0, jcap = 0, lcap = 0;
+    int32_t* ctl[2] = {nullptr, nullptr};  // two parities: a launch zeroes the other's
+    uint32_t* q[2] = {nullptr, nullptr};
+    int32_t* fill[2] = {nullptr, nullptr};
+    int32_t* list = nullptr;
+    int32_t* outst = nullptr;
+    int parity = 0;
+    int bpc[2][2] = {{0, 0}, {0, 0}};  // k_flow<AR, POL> workgroups per CU (occupancy API)
+    int64_t launches = 0;
+  } fl;
 };
 
 namespace tg {

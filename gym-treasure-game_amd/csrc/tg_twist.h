@@ -3,8 +3,8 @@
 // chained in the wave's LDS scratch, every generation's 312 draw codes and the even
 // generations' 624 words stored (tg_core.h MT_STORE).
 // Used by k_regen (the deferred regeneration, every 16 compact steps), k_gen_twist (tg_create,
-// tg_write_state), k_reset and k_step (tg_amd.hip), and timed in isolation by
-// scripts/calib/regen_bench.hip, which includes this header.
+// tg_write_state), k_reset and k_step (tg_amd.hip).  (The twist variants measured in isolation,
+// DESIGN.md §3.3, are restated in scripts/calib/twist_bench.hip.)
 //
 // What bounds it: not HBM.  One generation is ~2.8 KB of stores, and the
 // wave's VALU work per generation — 624 twists plus 312 draw codes — is what a k_regen launch

@@ -300,9 +300,11 @@ class TreasureGameVec:
         return int(v.value)
 
     def set_mode(self, mode="compact", run_blocks=0):
-        """Step implementation: "compact" (two-pass, default) or "direct" (one lane per env
-        runs in place); both are bit-identical."""
-        m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT}[mode]
+        """Step implementation: "compact" (two-pass, default), "direct" (one lane per env
+        runs in place) or "flow" (as compact per step; rollout() runs up to 16 steps per launch,
+        chunks advancing without a batch-wide barrier between steps); all bit-identical."""
+        m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT,
+             "flow": _lib.TG_MODE_FLOW}[mode]
         check(self._L.tg_set_mode(self.handle, m, int(run_blocks)), "tg_set_mode")
 
     def set_episode_capacity(self, cap):

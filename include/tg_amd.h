@@ -58,6 +58,8 @@ extern "C" {
 #define TG_ERR_RENDER (1u << 28)   /* render: a handle shaft end point within 1e-9 of an int()
                                       boundary (libm watch), or a shaft off the screen */
 #define TG_ERR_WINDOW (1u << 29)  /* a lane drew past its staged draw codes (a bound broken: bug) */
+#define TG_ERR_FLOW (1u << 30)    /* TG_MODE_FLOW: a k_flow wait ran past its 4-s bound (a bug; the
+                                      launch ended early, its results are not valid) */
 
 /* step flags */
 #define TG_STEP_AUTORESET 1u       /* reset() an env right after a step that returned done */
@@ -201,6 +203,11 @@ int tg_errors(tg_batch *h, uint32_t *or_of_flags, void *stream);
  *   TG_MODE_DIRECT: one k_step lane per env runs its option in place. */
 #define TG_MODE_DIRECT 0
 #define TG_MODE_COMPACT 1
+/*   TG_MODE_FLOW: as TG_MODE_COMPACT for tg_step; tg_rollout runs up to 16 steps per launch of
+ *     k_flow, in which each 64-env chunk is classified for step t + 1 as soon as its envs are
+ *     done with step t (no batch-wide barrier between steps).  Results are
+ *     identical to the other modes. */
+#define TG_MODE_FLOW 2
 /*   (Round 2's TG_MODE_ASYNC, all K steps of tg_rollout in one persistent launch, was exact
  *     but slower, 0.214 vs 0.142 ms per step, and was removed in round 3: DESIGN.md §9.1.) */
 int tg_set_mode(tg_batch *h, int mode, int run_blocks);
@@ -245,6 +252,11 @@ int tg_kernel_info(tg_batch *h, int kernel, int32_t *blocks_per_cu, int32_t *vgp
  * generations, stored_words = the words kept in HBM (the even generations), code_bytes = one
  * draw code per random() of the ring.  Any pointer may be NULL. */
 int tg_mt_layout(int32_t *ring_words, int32_t *stored_words, int32_t *code_bytes);
+
+/* Diagnostic (a timed region's fixed costs): `kernels` dependent launches of an
+ * empty kernel of `blocks` 256-thread workgroups on `stream` (the platform's dispatch gap between
+ * two dependent kernels, and an idle GPU's first dispatch).  No reference counterpart. */
+int tg_probe_dispatch(int32_t kernels, int32_t blocks, void *stream);
 
 /* Raw SoA state copy-out for checkpoints and tests (host buffers, synchronises; the MT
  * generations are gathered on the device and copied out in chunks of 64 Ki envs):

@@ -25,11 +25,15 @@ from gym_treasure_game_amd import _lib  # noqa: E402
 ACTION_SEED = 0x5EED0001
 
 
-def time_one(path, policy, n, burn, steps):
+def time_one(path, policy, n, burn, steps, mode="compact", K=0):
+    """K > 0: tg_rollout K steps per call (burn-in and timed steps) in step mode `mode`"""
     _lib._lib = None
     _lib.LIB_PATH = path
     vec = tg.TreasureGameVec(n, seed=0, autoreset=True)
     vec.reset()
+    vec.set_mode(mode)
+    if K:
+        return time_rollout(vec, policy, burn, steps, K)
     rec = torch.empty((1 << 16, 2), dtype=torch.int64, device=vec.device)
     cnt = torch.zeros(1, dtype=torch.int32, device=vec.device)
     for t in range(burn):
@@ -67,7 +71,42 @@ def time_one(path, policy, n, burn, steps):
             "lane_eff": st["ticks"] / max(64 * st["wave_ticks"], 1)}
 
 
+def time_rollout(vec, policy, burn, steps, K):
+    rec = torch.empty((1 << 16, 2), dtype=torch.int64, device=vec.device)
+    cnt = torch.zeros(1, dtype=torch.int32, device=vec.device)
+    t = 0
+    while t < burn:
+        k = min(K, burn - t)
+        vec.rollout(k, t0=t, action_seed=ACTION_SEED, policy=policy, obs=False, actions=False)
+        vec.drain_episodes(rec, cnt)
+        t += k
+    vec.regenerate()
+    torch.cuda.synchronize()
+    vec.stats_reset()
+    vec.set_timing(int(os.environ.get("TIMING", "0")))
+    t0 = time.perf_counter()
+    out = None
+    for j in range(0, steps, K):
+        out = vec.rollout(min(K, steps - j), t0=t + j, action_seed=ACTION_SEED, policy=policy,
+                          actions=False)
+        vec.drain_episodes(rec, cnt)
+    vec.regenerate()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = vec.stats()
+    obs = out["obs"][-1].contiguous().view(torch.int64)
+    digest = "%x/%d/%d" % (int((obs * torch.arange(1, obs.numel() + 1, device=obs.device,
+                                                       dtype=torch.int64).view_as(obs)).sum()) & (2**64 - 1),
+                          st["ticks"], st["draws"])
+    err = vec.errors()
+    vec.close()
+    return {"digest": digest, "ms_step": dt / steps * 1e3, "errors": err,
+            "kernel_ms": st["kernel_ms"] / max(st.get("timed_launches") or 1, 1),
+            "lane_eff": st["ticks"] / max(64 * st["wave_ticks"], 1)}
+
+
 def main():
+    # VARIANTS: name=lib[:mode[:K]], e.g. flow=gym-treasure-game_amd/libtg_amd.so:flow:16
     variants = [v.split("=", 1) for v in os.environ["VARIANTS"].split(",")]
     policies = os.environ.get("POLICIES", "uniform,masked").split(",")
     n = int(os.environ.get("N", 1 << 20))
@@ -77,8 +116,9 @@ def main():
     for pol in policies:
         burn = int(os.environ.get("BURN", 3000 if pol == "uniform" else 1500))
         for r in range(rounds):
-            for name, path in variants:
-                res = time_one(os.path.join(ROOT, path), pol, n, burn, steps)
+            for name, spec in variants:
+                path, mode, K = (spec.split(":") + ["compact", "0"])[:3]
+                res = time_one(os.path.join(ROOT, path), pol, n, burn, steps, mode, int(K))
                 key = "%s/%s" % (pol, name)
                 print(key, "round", r, json.dumps(res), flush=True)
                 best = out.get(key)

@@ -22,9 +22,10 @@ def episodes_sorted(vec):
 
 
 def run_pair(tg, n, k, policy, pre_steps=0, level=None, seed=5, a0=0xA5A5, chunks=(None,),
-             groups=1, stagger=False, post_steps=0):
+             groups=1, stagger=False, post_steps=0, mode="compact"):
     """the same batch through K x (tg_policy_actions + tg_step) and through tg_rollout (in
-    `chunks` calls); returns both sides' outputs, final states and sorted episodes"""
+    `chunks` calls, in step mode `mode`); returns both sides' outputs, final states and sorted
+    episodes"""
     ld = None if level is None else os.path.join(LEVELS, level)
     sides = []
     for side in ("steps", "rollout"):
@@ -41,6 +42,7 @@ def run_pair(tg, n, k, policy, pre_steps=0, level=None, seed=5, a0=0xA5A5, chunk
                              "done": d.clone(), "actions": act})
             out = {key: torch.stack([x[key] for x in outs]) for key in outs[0]}
         else:
+            v.set_mode(mode)
             if groups > 1:
                 v.set_groups(groups, stagger)
             t0, parts = pre_steps, []
