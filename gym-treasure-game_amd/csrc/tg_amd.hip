@@ -1980,7 +1980,7 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   F.parity ^= 1;
   Flow f{F.ctl[p], F.q[p], F.fill[p], F.list, F.outst, F.ctl[p ^ 1], F.q[p ^ 1], F.fill[p ^ 1],
          c.refill, c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
-         F.qcap, F.jcap, F.lcap, F.C, F.P, k, F.xmap, nullptr, nullptr};
+         F.qcap, F.jcap, F.lcap, F.C, F.P, k, F.xmap, nullptr, nullptr, nullptr};
 #ifdef TG_FLOW_DBG
   static uint32_t* dbg_host = nullptr;
   static uint32_t* dbg_dev = nullptr;
@@ -1995,6 +1995,13 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   if (!dbgc) HIP_TRY(hipMalloc((void**)&dbgc, sizeof(uint32_t) * ndc));
   HIP_TRY(hipMemset(dbgc, 0, sizeof(uint32_t) * ndc));
   f.dbgc = dbgc;
+  static uint32_t* dbgl = nullptr;
+  const char* logp = getenv("TG_FLOW_LOG");
+  if (logp) {
+    if (!dbgl) HIP_TRY(hipMalloc((void**)&dbgl, 64 + 32 * (size_t)FLOW_EVCAP));
+    HIP_TRY(hipMemset(dbgl, 0, 64));
+    f.dbgl = dbgl;
+  }
 #endif
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   if (getenv("TG_FLOW_DEBUG"))
@@ -2027,6 +2034,22 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
       if (dbg_host[w * 4])
         fprintf(stderr, "[flowdbg]  DUP slot %d: code %u %u %08x %08x\n", w, dbg_host[w * 4], dbg_host[w * 4 + 1],
                 dbg_host[w * 4 + 2], dbg_host[w * 4 + 3]);
+    if (logp && !hung) {  // the event log, for scripts/flow_log.py
+      uint32_t cnt = 0;
+      HIP_TRY(hipMemcpy(&cnt, dbgl, 4, hipMemcpyDeviceToHost));
+      if (cnt > FLOW_EVCAP) cnt = FLOW_EVCAP;
+      std::vector<uint32_t> ev((size_t)cnt * 8);
+      HIP_TRY(hipMemcpy(ev.data(), dbgl + 16, ev.size() * 4, hipMemcpyDeviceToHost));
+      char path[512];
+      snprintf(path, sizeof path, "%s.%lld.bin", logp, (long long)F.launches);
+      if (FILE* fp = fopen(path, "wb")) {
+        const uint32_t hdr[8] = {cnt, (uint32_t)F.C, (uint32_t)F.P, (uint32_t)k, F.xmap, (uint32_t)F.jcap, 0, 0};
+        fwrite(hdr, 4, 8, fp);
+        fwrite(ev.data(), 4, ev.size(), fp);
+        fclose(fp);
+      }
+      fprintf(stderr, "[flowdbg] %u events -> %s\n", cnt, path);
+    }
     if (hung) {
       fflush(stderr);
       _exit(3);

@@ -83,6 +83,7 @@ struct Flow {
   uint32_t xmap;     // nibble x: the sub-problem of XCC id x (0xF: none)
   uint32_t* dbg;     // TG_FLOW_DBG builds: per-wave progress in mapped host memory (else null)
   uint32_t* dbgc;    // TG_FLOW_DBG builds: [C][16] classifications, [P][16][NLIST][jcap] runs
+  uint32_t* dbgl;    // TG_FLOW_DBG builds: event log (count at [0], 32-B records from [16])
 };
 #ifdef TG_FLOW_DBG
 // DIAGNOSTIC BUILD ONLY: lane 0 of wave gw < 4096 publishes (code, a, b, c) to host memory
@@ -96,8 +97,24 @@ struct Flow {
       __hip_atomic_store(f.dbg + gw_ * 4 + 3, (uint32_t)(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);    \
     }                                                                                            \
   } while (0)
+// DIAGNOSTIC BUILD ONLY: one 32-B event record (type, a, b, c, d, wave, clock) per calling lane
+constexpr uint32_t FLOW_EVCAP = 1u << 22;
+#define FLOW_EV(ty, a, b, c, d)                                                                   \
+  do {                                                                                           \
+    if (f.dbgl) {                                                                                \
+      const uint32_t k_ = atomicAdd(f.dbgl, 1u);                                                 \
+      if (k_ < FLOW_EVCAP) {                                                                     \
+        const unsigned long long tm_ = realtime();                                               \
+        uint4* r_ = reinterpret_cast<uint4*>(f.dbgl + 16) + 2 * (int64_t)k_;                      \
+        r_[0] = make_uint4((uint32_t)(ty), (uint32_t)(a), (uint32_t)(b), (uint32_t)(c));          \
+        r_[1] = make_uint4((uint32_t)(d), (uint32_t)(((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6), \
+                           (uint32_t)tm_, (uint32_t)(tm_ >> 32));                                \
+      }                                                                                          \
+    }                                                                                            \
+  } while (0)
 #else
 #define FLOW_DBG(code, a, b, c) (void)0
+#define FLOW_EV(ty, a, b, c, d) (void)0
 #endif
 // the rollout's outputs, step-major [K][N] (obs_stride 0: one scratch row set for all steps)
 struct FlowIO {
@@ -232,9 +249,10 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
   int32_t* const list = f.list + (int64_t)x * FLOW_MAX_K * NLIST * f.lcap;
   const int64_t slot = (int64_t)blockIdx.x % nstat;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  if (lane == 0) FLOW_EV(10, x, 0, 0, 0);
 
   // a run item on the queue (by the lane that calls it)
-  auto push = [&](int t, int k, int j) {
+  auto push = [&](int t, int k, int j, int src) {
 #ifdef TG_FLOW_DBG
     if (f.dbgc) {  // pushes per list chunk: a second push of one goes to slot 4093
       const int64_t base2 = (int64_t)f.C * 16 + (int64_t)f.P * FLOW_MAX_K * NLIST * f.jcap;
@@ -248,6 +266,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     }
 #endif
     const int at = atomicAdd(fcw(ctl, FC_QTAIL), 1);
+    FLOW_EV(4, ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j, at, src, x);
     if ((int64_t)at < f.qcap) st_sc1(q + at, ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j);
     else atomicOr(err_or, E_FLOW);  // (capacity is the bound of the pushes: unreachable)
   };
@@ -346,8 +365,8 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       if (bk >= 0 && lane == lead) {
         int32_t* const fl = fill + (int64_t)lidx * f.jcap;
         const int j0 = base >> 6, in0 = min(nb, 64 - (base & 63));
-        if (atomicAdd(&fl[j0], in0) + in0 == 64) push(t, bk, j0);
-        if (nb > in0 && atomicAdd(&fl[j0 + 1], nb - in0) + (nb - in0) == 64) push(t, bk, j0 + 1);
+        if (atomicAdd(&fl[j0], in0) + in0 == 64) push(t, bk, j0, 0);
+        if (nb > in0 && atomicAdd(&fl[j0 + 1], nb - in0) + (nb - in0) == 64) push(t, bk, j0 + 1, 1);
       }
     } else {
       // the chain goes on with this chunk's next step in this wave: its stores land first
@@ -357,9 +376,10 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     // the last chunk classified for step t flushes step t's partial list chunks
     int last = 0;
     if (lane == 0) last = atomicAdd(fcw(ctl, FC_CLS + t), 1) + 1 == Cx;
+    if (lane == 0) FLOW_EV(2, c, t, cnt, x);
     if (__builtin_amdgcn_readlane(last, 0) && lane < NLIST) {
       const int tail = ld_sc1(fcw(ctl, FC_LTAIL + t * NLIST + lane));
-      if (tail & 63) push(t, lane, tail >> 6);
+      if (tail & 63) push(t, lane, tail >> 6, 2 | (tail << 8));
     }
     return cnt;
   };
@@ -430,7 +450,11 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       int old = 0;
       if (live) old = atomicSub(&f.outst[i >> 6], 1);
+#ifdef TG_FLOW_LANES
+      if (live) FLOW_EV(3, item, (uint32_t)i, (uint32_t)old, (uint32_t)lane | ((uint32_t)mcnt << 8) | ((uint32_t)x << 16));
+#endif
       unsigned long long ready = __ballot(live && old == 1);
+      if (lane == 0) FLOW_EV(7, item, (uint32_t)__popcll(ready), (uint32_t)mcnt, x);
       cl = (int)(i >> 6);
       return ready;
   };
@@ -479,6 +503,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       if (lane == 0) h = atomicAdd(fcw(ctl, FC_QHEAD), 1);
       h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(h, 0));
       FLOW_DBG(2, h, x, 0);
+      if (lane == 0) FLOW_EV(8, h, x, 0, 0);
       uint32_t item = Q_EMPTY;
       int stop = 0;
       while (!stop) {
@@ -504,6 +529,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       }
       if (item == Q_EMPTY) break;
       FLOW_DBG(3, h, item, x);
+      if (lane == 0) FLOW_EV(5, h, item, x, 0);
 #ifdef TG_FLOW_DBG
       dbg_item = item;
       if (lane == 0 && f.dbgc) {
@@ -517,8 +543,10 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       }
 #endif
       const unsigned long long rd = run(item, cl);
-      ready = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(rd >> 32)) << 32) |
-              __builtin_amdgcn_readfirstlane((uint32_t)rd);
+      // (readfirstlane returns int: the low half is cast back to 32 bits before it widens, or
+      // lane 31's bit sign-extends over lanes 32-63 and the wave classifies chunks never ready)
+      ready = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rd >> 32)) << 32) |
+              (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rd);
       tn = __builtin_amdgcn_readfirstlane((int)(item >> 28) + 1);
       FLOW_DBG(4, h, item, (uint32_t)__popcll(ready));
       continue;
@@ -530,6 +558,9 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       continue;
     }
     FLOW_DBG(10 + t, c, x, 0);
+#ifdef TG_FLOW_DBG
+    if (lane == 0) FLOW_EV(1, c, t, path, x);
+#endif
 #ifdef TG_FLOW_DBG
     if (lane == 0 && f.dbgc) {
       const uint32_t o = atomicAdd(&f.dbgc[(int64_t)c * 16 + t], 1u);
@@ -550,5 +581,6 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     }
   }
   FLOW_DBG(9, 0, 0, 0);
+  if (lane == 0) FLOW_EV(9, x, 0, 0, 0);
   kst_end(ks, kt0);
 }

@@ -190,18 +190,30 @@ __global__ __launch_bounds__(RBLOCK) void k_render_sweep(RenderArgs A, const Env
                                                          uint4* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (RBLOCK / 64);
-  const int64_t fc = (int64_t)A.Hpx * A.CH, total = count * fc;
-  const int64_t nseg = (total + 63) >> 6;
-  for (int64_t seg = (int64_t)blockIdx.x * (RBLOCK / 64) + (threadIdx.x >> 6); seg < nseg; seg += nw) {
+  const int fc = A.Hpx * A.CH;  // chunks per frame
+  const int64_t nseg = (count * fc + 63) >> 6;
+  // the wave's segment start as (frame e0, chunk f0 of it), advanced by nw segments = dq frames
+  // + dr chunks per iteration (one 64-bit division per wave, not per segment)
+  const int64_t seg0 = (int64_t)blockIdx.x * (RBLOCK / 64) + (threadIdx.x >> 6);
+  int64_t e0 = seg0 * 64 / fc;
+  int f0 = (int)(seg0 * 64 - e0 * fc);
+  const int64_t dq = nw * 64 / fc;
+  const int dr = (int)(nw * 64 - dq * fc);
+  for (int64_t seg = seg0; seg < nseg; seg += nw) {
     const int64_t c0 = seg * 64;
-    const int64_t e0 = c0 / fc;  // wave-uniform
-    int64_t e = e0, cif = c0 + lane - e0 * fc;
-    if (cif >= fc) {  // the segment runs into the next frame
-      cif -= fc;
+    int64_t e = e0;
+    int ci = f0 + lane;
+    if (ci >= fc) {  // the segment runs into the next frame
+      ci -= fc;
       ++e;
     }
+    e0 += dq;
+    f0 += dr;
+    if (f0 >= fc) {
+      f0 -= fc;
+      ++e0;
+    }
     if (e >= count) continue;
-    const int ci = (int)cif;
     const int r = ci / A.CH, q = ci - r * A.CH;
     const uint32_t rm = rows[e * A.Hpx + r];
     const uint4 v = A.bg[ci];

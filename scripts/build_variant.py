@@ -5,7 +5,8 @@
     python scripts/build_variant.py NAME 'old text' 'new text' ['old2' 'new2' ...]
 
 writes gym-treasure-game_amd/libtg_amd_NAME.so (timed by scripts/ab.py).  Every replacement
-must match exactly once in one of the csrc files."""
+must match exactly once in one of the csrc files.  EXTRA_FLAGS (environment) is appended to
+the compiler flags (e.g. '-mllvm -disable-machine-licm' or '-DTG_FLOW_W=4')."""
 import os
 import shutil
 import subprocess
@@ -32,7 +33,8 @@ def main():
         open(hits[0], "w").write(t)
     out = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_%s.so" % name)
     srcs = [os.path.join(src, "tg_amd.hip"), os.path.join(src, "tg_render.hip")]
-    subprocess.check_call([B.HIPCC] + B.FLAGS + ["-o", out] + srcs)
+    extra = os.environ.get("EXTRA_FLAGS", "").split()
+    subprocess.check_call([B.HIPCC] + B.FLAGS + extra + ["-o", out] + srcs)
     shutil.rmtree(tmp)
     print(out)
 

@@ -6,7 +6,10 @@ env run twice for one step, a chunk's outstanding count out of step.  Diagnostic
 Records (8 x u32): type, a, b, c, d, wave, clock lo, clock hi
   1 classify start (c, t, path, x)    2 classify end (c, t, cnt, x)
   3 run lane (item, env, old outst, lane | mcnt << 8 | x << 16)
-  4 push (item, slot, src, x)         5 ticket (h, item, x)"""
+  4 push (item, slot, src, x)         5 ticket served: run starts (h, item, x)
+  7 run end (item, chunks readied, entries, x)   8 ticket taken (h, x)
+  9 wave exits (x)                    10 wave starts its loop (x)
+(type 3 only in TG_FLOW_LANES builds).  --time: where the waves' time goes (clock: 100 MHz)."""
 import sys
 from collections import defaultdict
 
@@ -70,6 +73,61 @@ def main(path):
             print("  @%d run %s env %d old %d lane %d mcnt %d wave %d" % (tm, item_s(a), b, c, d & 255, (d >> 8) & 255, w))
 
 
+def timing(path):
+    raw = np.fromfile(path, dtype=np.uint32)
+    hdr, ev = raw[:8], raw[8:].reshape(-1, 8)
+    print("%s: %d events, C %d P %d K %d" % (path, hdr[0], hdr[1], hdr[2], hdr[3]))
+    clk = ev[:, 6].astype(np.int64) | (ev[:, 7].astype(np.int64) << 32)
+    order = np.lexsort((clk, ev[:, 5]))  # by wave, then clock
+    ev, clk = ev[order], clk[order]
+    t0 = clk.min()
+    tot = defaultdict(int)
+    durs = defaultdict(list)
+    open_ = {}
+    span_end = 0
+    step_last = defaultdict(int)
+    for r, tm in zip(ev, clk):
+        ty, a, b, w = int(r[0]), int(r[1]), int(r[2]), int(r[5])
+        tm -= t0
+        if ty == 10:
+            open_[w] = ("gap", tm)
+        elif ty in (1, 8, 5, 9):
+            kind, st = open_.get(w, ("gap", tm))
+            tot[kind] += tm - st
+            durs[kind].append(tm - st)
+            nxt = {1: "classify", 8: "gap", 5: "run", 9: None}[ty]
+            if ty == 5:  # the ticket wait ended
+                tot["ticket"] += 0
+            if ty == 8:
+                open_[w] = ("ticket", tm)
+            elif nxt:
+                open_[w] = (nxt, tm)
+            if ty == 9:
+                span_end = max(span_end, tm)
+            if ty == 1:
+                step_last[b] = max(step_last[b], tm)
+        elif ty in (2, 7):
+            kind, st = open_.get(w, ("gap", tm))
+            tot[kind] += tm - st
+            durs[kind].append(tm - st)
+            open_[w] = ("gap", tm)
+    waves = len(set(ev[:, 5].tolist()))
+    allt = sum(tot.values())
+    print("waves %d, span %.1f us, wave-time %.1f us per wave" % (waves, span_end / 100, allt / waves / 100))
+    for k in sorted(tot):
+        d = np.array(durs[k]) / 100
+        if not len(d):
+            continue
+        print("  %-9s %5.1f %%  n %7d  median %7.2f us  p90 %7.2f us  max %8.2f us" % (
+            k, 100 * tot[k] / allt, len(d), np.median(d), np.percentile(d, 90), d.max()))
+    print("  last classification of step t at (us):", " ".join("%d:%.0f" % (t, step_last[t] / 100) for t in sorted(step_last)))
+
+
 if __name__ == "__main__":
-    for p in sys.argv[1:]:
-        main(p)
+    args = sys.argv[1:]
+    if args and args[0] == "--time":
+        for p in args[1:]:
+            timing(p)
+    else:
+        for p in args:
+            main(p)
