@@ -457,6 +457,30 @@ class Runner:
                 ev[1].record()
                 self.rev.append(ev)
 
+    def probe_region(self, steps):
+        """The platform's share of a timed region: the same number of dependent
+        launches as the region held (2 step kernels per step + the k_regen launches + the final
+        drain), as EMPTY kernels of the step kernels' grid (tg_probe_dispatch), timed exactly as
+        the region is (synchronize, wall clock + event pair, end event polled, synchronize).
+        Untimed by the line itself; reported beside it."""
+        n = 2 * steps + -(-steps // 16) + 1
+        blocks = min(4096, max(1, self.count // 256))
+        out = []
+        for _ in range(3):
+            torch.cuda.synchronize(self.dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record()
+            self.tg._lib.check(self.L.tg_probe_dispatch(n, blocks, self.stream), "probe")
+            e1.record()
+            if self.args.spin:
+                while not e1.query():
+                    pass
+            torch.cuda.synchronize(self.dev)
+            out.append(((time.perf_counter() - t0) * 1e3, e0.elapsed_time(e1)))
+        w, e = sorted(out)[1]
+        return {"kernels": n, "blocks": blocks, "wall_ms": w, "events_ms": e, "wall_minus_events_ms": w - e}
+
     def measure(self, warmup, burn_in, steps):
         """warm-up + burn-in (untimed), then EXACTLY ``steps`` timed steps between barriers;
         returns the max-over-ranks wall time and this rank's stats."""
@@ -527,6 +551,7 @@ class Runner:
                         "spin": bool(self.args.spin)}
         self.timing = False
         vec.set_timing(0)
+        self.region_probe = self.probe_region(steps)
         st = vec.stats()
         self.drain_all(log=True)  # records of the timed steps still queued (untimed)
         if self.world > 1:
@@ -672,6 +697,10 @@ def step_line(args, runner, dt, st, node, world, total):
                     "alg_bytes_per_launch": all_b, "kernel_ms": all_s * 1e3,
                     "events_ms_per_step": runner.events_ms / args.steps,
                     "host_ms": runner.host_ms,
+                    # the region's wall clock minus its event pair, beside the same for a region
+                    # of as many empty dependent kernels
+                    "region_wall_minus_events_ms": dt * 1e3 - runner.events_ms,
+                    "region_probe": runner.region_probe,
                     "gaps_ms": ms_step - all_s * 1e3,
                     "achieved": all_b / all_s / 1e9 if all_s else None,
                     "frac": all_b / all_s / 1e9 / HBM_PEAK_GBS if all_s else None,

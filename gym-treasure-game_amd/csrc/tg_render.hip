@@ -182,6 +182,7 @@ __global__ __launch_bounds__(RBLOCK) void k_render_prep(RenderArgs A, const uint
   for (int y = threadIdx.x; y < A.Hpx; y += RBLOCK) rows[e * A.Hpx + y] = (uint16_t)row_items(lay, lv, y);
   if ((int)threadIdx.x < A.H) cell_sources(lay, lv, (int)threadIdx.x, A.W, sels + (e * A.H + threadIdx.x) * A.W);
 }
+constexpr int SU = 4;  // the sweep's segments in flight per wave
 // wave gw of nw: 1-KB segments gw, gw + nw, ... of the frames [0, count) (16-B chunks, 64 per
 // segment; a frame is Hpx * CH chunks, whole lines of 16 B, and may end inside a segment)
 __global__ __launch_bounds__(RBLOCK) void k_render_sweep(RenderArgs A, const EnvItems* __restrict__ items,
@@ -192,37 +193,55 @@ __global__ __launch_bounds__(RBLOCK) void k_render_sweep(RenderArgs A, const Env
   const int64_t nw = (int64_t)gridDim.x * (RBLOCK / 64);
   const int fc = A.Hpx * A.CH;  // chunks per frame
   const int64_t nseg = (count * fc + 63) >> 6;
-  // the wave's segment start as (frame e0, chunk f0 of it), advanced by nw segments = dq frames
-  // + dr chunks per iteration (one 64-bit division per wave, not per segment)
+  // SU segments per iteration (seg + u * nw), their loads issued together: one segment at a
+  // time left each wave a chain of dependent loads per KB stored.  Each segment start is kept
+  // as (frame, chunk of it) and advanced by SU * nw segments = dq frames + dr chunks (one 64-bit
+  // division per wave, not per segment).
   const int64_t seg0 = (int64_t)blockIdx.x * (RBLOCK / 64) + (threadIdx.x >> 6);
-  int64_t e0 = seg0 * 64 / fc;
-  int f0 = (int)(seg0 * 64 - e0 * fc);
-  const int64_t dq = nw * 64 / fc;
-  const int dr = (int)(nw * 64 - dq * fc);
-  for (int64_t seg = seg0; seg < nseg; seg += nw) {
-    const int64_t c0 = seg * 64;
-    int64_t e = e0;
-    int ci = f0 + lane;
-    if (ci >= fc) {  // the segment runs into the next frame
-      ci -= fc;
-      ++e;
+  int64_t fe[SU];
+  int ff[SU];
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int64_t c = (seg0 + u * nw) * 64;
+    fe[u] = c / fc;
+    ff[u] = (int)(c - fe[u] * fc);
+  }
+  const int64_t dq = SU * nw * 64 / fc;
+  const int dr = (int)(SU * nw * 64 - dq * fc);
+  for (int64_t seg = seg0; seg < nseg; seg += SU * nw) {
+    int64_t e[SU];
+    int ci[SU];
+    uint32_t rm[SU];
+    uint4 v[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      e[u] = fe[u];
+      ci[u] = ff[u] + lane;
+      if (ci[u] >= fc) {  // the segment runs into the next frame
+        ci[u] -= fc;
+        ++e[u];
+      }
+      fe[u] += dq;
+      ff[u] += dr;
+      if (ff[u] >= fc) {
+        ff[u] -= fc;
+        ++fe[u];
+      }
+      const bool ok = e[u] < count;
+      const int r = ci[u] / A.CH;
+      rm[u] = ok ? rows[e[u] * A.Hpx + r] : 0u;
+      v[u] = A.bg[ok ? ci[u] : 0];
     }
-    e0 += dq;
-    f0 += dr;
-    if (f0 >= fc) {
-      f0 -= fc;
-      ++e0;
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      if (e[u] >= count) continue;
+      uint4 o = v[u];
+      if (rm[u]) {
+        const int r = ci[u] / A.CH, q = ci[u] - r * A.CH, band = r / RS;
+        o = render_chunk(A, items[e[u]].lay, rm[u], sels + (e[u] * A.H + band) * A.W, band, r - band * RS, q, v[u]);
+      }
+      store16(out + (seg + u * nw) * 64 + lane, o);
     }
-    if (e >= count) continue;
-    const int r = ci / A.CH, q = ci - r * A.CH;
-    const uint32_t rm = rows[e * A.Hpx + r];
-    const uint4 v = A.bg[ci];
-    uint4 o = v;
-    if (rm) {
-      const int band = r / RS;
-      o = render_chunk(A, items[e].lay, rm, sels + (e * A.H + band) * A.W, band, r - band * RS, q, v);
-    }
-    store16(out + c0 + lane, o);
   }
 }
 
