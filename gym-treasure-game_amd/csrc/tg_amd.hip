@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <algorithm>
 #include <cstdlib>
 #include <unistd.h>
 #include <cstdio>
@@ -1995,11 +1996,21 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   if (!dbgc) HIP_TRY(hipMalloc((void**)&dbgc, sizeof(uint32_t) * ndc));
   HIP_TRY(hipMemset(dbgc, 0, sizeof(uint32_t) * ndc));
   f.dbgc = dbgc;
+#ifdef TG_FLOW_WAVELOG
+  f.dbg = nullptr;  // a timing log: no host-mapped progress words, no duplicate counters
+  f.dbgc = nullptr;
+#endif
   static uint32_t* dbgl = nullptr;
   const char* logp = getenv("TG_FLOW_LOG");
   if (logp) {
+#ifdef TG_FLOW_WAVELOG
+    const size_t evb = 64 + 32 * (size_t)FLOW_EVW * (size_t)h->cus * 8 * (BLOCK / 64);
+    if (!dbgl) HIP_TRY(hipMalloc((void**)&dbgl, evb));
+    HIP_TRY(hipMemset(dbgl, 0, evb));
+#else
     if (!dbgl) HIP_TRY(hipMalloc((void**)&dbgl, 64 + 32 * (size_t)FLOW_EVCAP));
     HIP_TRY(hipMemset(dbgl, 0, 64));
+#endif
     f.dbgl = dbgl;
   }
 #endif
@@ -2036,10 +2047,21 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
                 dbg_host[w * 4 + 2], dbg_host[w * 4 + 3]);
     if (logp && !hung) {  // the event log, for scripts/flow_log.py
       uint32_t cnt = 0;
+#ifdef TG_FLOW_WAVELOG
+      std::vector<uint32_t> ev((size_t)FLOW_EVW * h->cus * bpc * (BLOCK / 64) * 8);
+      HIP_TRY(hipMemcpy(ev.data(), dbgl + 16, ev.size() * 4, hipMemcpyDeviceToHost));
+      for (size_t r = 0; r < ev.size() / 8; ++r)  // the non-empty records, in place
+        if (ev[r * 8]) {
+          std::copy(ev.begin() + r * 8, ev.begin() + r * 8 + 8, ev.begin() + (size_t)cnt * 8);
+          ++cnt;
+        }
+      ev.resize((size_t)cnt * 8);
+#else
       HIP_TRY(hipMemcpy(&cnt, dbgl, 4, hipMemcpyDeviceToHost));
       if (cnt > FLOW_EVCAP) cnt = FLOW_EVCAP;
       std::vector<uint32_t> ev((size_t)cnt * 8);
       HIP_TRY(hipMemcpy(ev.data(), dbgl + 16, ev.size() * 4, hipMemcpyDeviceToHost));
+#endif
       char path[512];
       snprintf(path, sizeof path, "%s.%lld.bin", logp, (long long)F.launches);
       if (FILE* fp = fopen(path, "wb")) {

@@ -99,6 +99,21 @@ struct Flow {
   } while (0)
 // DIAGNOSTIC BUILD ONLY: one 32-B event record (type, a, b, c, d, wave, clock) per calling lane
 constexpr uint32_t FLOW_EVCAP = 1u << 22;
+#ifdef TG_FLOW_WAVELOG
+// (wave-local form: each wave's lane 0 appends to its own FLOW_EVW slots, no shared counter;
+// the lane-level events 3 and 4 are left out)
+constexpr uint32_t FLOW_EVW = 1024;
+#define FLOW_EV(ty, a, b, c, d)                                                                   \
+  do {                                                                                           \
+    if (f.dbgl && (ty) != 3 && (ty) != 4 && evn_ < FLOW_EVW) {                                   \
+      const int64_t gw_ = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;                      \
+      const unsigned long long tm_ = realtime();                                                 \
+      uint4* r_ = reinterpret_cast<uint4*>(f.dbgl + 16) + 2 * (gw_ * FLOW_EVW + evn_++);           \
+      r_[0] = make_uint4((uint32_t)(ty), (uint32_t)(a), (uint32_t)(b), (uint32_t)(c));            \
+      r_[1] = make_uint4((uint32_t)(d), (uint32_t)gw_, (uint32_t)tm_, (uint32_t)(tm_ >> 32));     \
+    }                                                                                            \
+  } while (0)
+#else
 #define FLOW_EV(ty, a, b, c, d)                                                                   \
   do {                                                                                           \
     if (f.dbgl) {                                                                                \
@@ -112,6 +127,7 @@ constexpr uint32_t FLOW_EVCAP = 1u << 22;
       }                                                                                          \
     }                                                                                            \
   } while (0)
+#endif
 #else
 #define FLOW_DBG(code, a, b, c) (void)0
 #define FLOW_EV(ty, a, b, c, d) (void)0
@@ -249,6 +265,10 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
   int32_t* const list = f.list + (int64_t)x * FLOW_MAX_K * NLIST * f.lcap;
   const int64_t slot = (int64_t)blockIdx.x % nstat;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
+#ifdef TG_FLOW_DBG
+  uint32_t evn_ = 0;  // (TG_FLOW_WAVELOG: this wave's events logged)
+  (void)evn_;
+#endif
   if (lane == 0) FLOW_EV(10, x, 0, 0, 0);
 
   // a run item on the queue (by the lane that calls it)
