@@ -1925,10 +1925,11 @@ int flow_init(tg_batch* h) {
   if (F.P == 0) return fail(TG_E_HIP, "flow census: no XCC id in 0..7");
   if (getenv("TG_FLOW_DEBUG")) fprintf(stderr, "[flow] census mask %08x P %d\n", mask, F.P);
   const int64_t C = (h->n + 63) / 64, cxm = (C + F.P - 1) / F.P;
+  if (C > 0xFFFFFF) return fail(TG_E_INVAL, "flow mode: at most 2^24 chunks of 64 envs");
   F.C = (int32_t)C;
   F.lcap = cxm * 64;
   F.jcap = cxm + 1;
-  F.qcap = (int64_t)FLOW_MAX_K * (cxm + NLIST);
+  F.qcap = (int64_t)FLOW_MAX_K * (2 * cxm + NLIST);  // run items + chunks to classify, per step
   const size_t nctl = (size_t)F.P * CTL_WORDS, nq = (size_t)F.P * F.qcap,
                nfill = (size_t)F.P * FLOW_MAX_K * NLIST * F.jcap,
                nlist = (size_t)F.P * FLOW_MAX_K * NLIST * F.lcap;

@@ -44,6 +44,7 @@
 constexpr int FLOW_MAX_K = REGEN_STEPS;  // steps per launch (the MT slack: k_regen every 16)
 constexpr int FLOW_MAX_PARTS = 8;        // sub-problems: one per XCD
 constexpr uint32_t Q_EMPTY = 0xFFFFFFFFu;
+constexpr int Q_CLASSIFY = 15;  // the list field of a queue item that is a chunk to classify
 constexpr unsigned long long FLOW_DEADLINE = 400000000ull;  // 4 s of s_memrealtime
 constexpr uint32_t E_FLOW = 1u << 30;    // TG_ERR_FLOW: a k_flow wait ran past FLOW_DEADLINE (a bug)
 // a sub-problem's control words, each on a 128-B line of its own
@@ -62,8 +63,8 @@ constexpr int CTL_WORDS = FC_N * FC_STRIDE;
 // per-wave LDS: the option loop's code window, or the classification's obs-row staging
 constexpr int FLOW_WAVE_BYTES = (WIN_WAVE_BYTES > 64 * 9 * 8 ? WIN_WAVE_BYTES : 64 * 9 * 8);
 static_assert(FLOW_WAVE_BYTES % 16 == 0, "16-B aligned windows for the LDS-DMA");
-// run item: step (4 bits), list (4 bits), list chunk (24 bits)
-static_assert(FLOW_MAX_K <= 16 && NLIST <= 16, "item fields");
+// queue item: step (4 bits), list (4 bits), list chunk (24 bits); or step, Q_CLASSIFY, chunk
+static_assert(FLOW_MAX_K <= 16 && NLIST < Q_CLASSIFY, "item fields");
 
 struct Flow {
   int32_t* ctl;      // [P][CTL_WORDS] this launch's control words (zero at launch)
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
   // a run item on the queue (by the lane that calls it)
   auto push = [&](int t, int k, int j, int src) {
 #ifdef TG_FLOW_DBG
-    if (f.dbgc) {  // pushes per list chunk: a second push of one goes to slot 4093
+    if (f.dbgc && k != Q_CLASSIFY) {  // pushes per list chunk: a second push of one goes to slot 4093
       const int64_t base2 = (int64_t)f.C * 16 + (int64_t)f.P * FLOW_MAX_K * NLIST * f.jcap;
       const uint32_t o = atomicAdd(&f.dbgc[base2 + ((int64_t)x * FLOW_MAX_K * NLIST + t * NLIST + k) * f.jcap + j], 1u);
       if (o && atomicCAS(f.dbg + 4093 * 4, 0u, 97u) == 0u) {
@@ -483,12 +484,15 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
   // (each read back with readfirstlane, so the loop's branches stay scalar: with the work in
   // nested loops whose exits the compiler did not prove uniform, it built a divergent loop
   // nest whose lanes could sit in different iterations, and a wave re-classified chunk 0
-  // forever).  In order: a chunk carried to its next step (none of its envs ran an option), the
-  // chunks the last run item completed, the step-0 chunks dealt out by a counter, run items.
+  // forever).  In order: a chunk carried to its next step (none of its envs ran an option, or
+  // the first chunk the wave's last run item completed), the step-0 chunks dealt out by a
+  // counter, then the queue: run items and the chunks other waves' run items completed (a run
+  // item's envs come from up to 64 chunks, and late in a step many of them complete together:
+  // classified by their one wave in turn they left the others waiting on the queue, 58 % of
+  // the waves' time in the r05g event log)
   bool phase0 = true;
-  unsigned long long ready = 0;  // lanes whose env's chunk the last run item completed
-  int cl = 0;                    // (per lane) that chunk
-  int tn = 0, cc = -1, ct = 0;   // their next step; the carried chunk and its step
+  int cl = 0;                    // (per lane) the chunk of the lane's env in the last run item
+  int cc = -1, ct = 0;           // the carried chunk and its step
 #ifdef TG_FLOW_DBG
   int path = 0;
   uint32_t dbg_item = 0;
@@ -496,17 +500,12 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
   while (true) {
     int c, t;
 #ifdef TG_FLOW_DBG
-    path = cc >= 0 ? 1 : ready ? 2 : 3;
+    path = cc >= 0 ? 1 : phase0 ? 3 : 2;
 #endif
     if (cc >= 0) {
       c = cc;
       t = ct;
       cc = -1;
-    } else if (ready) {
-      const int l0 = __ffsll((long long)ready) - 1;
-      ready &= ready - 1;
-      c = __builtin_amdgcn_readlane(cl, l0);
-      t = tn;
     } else if (phase0) {
       int j = 0;
       if (lane == 0) j = atomicAdd(fcw(ctl, FC_INIT), 1);
@@ -518,7 +517,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       c = x + P * j;
       t = 0;
     } else {
-      // a run item by ticket: wait for its slot (lane 0 polls, the wave reads its answer)
+      // an item by ticket: wait for its slot (lane 0 polls, the wave reads its answer)
       int h = 0;
       if (lane == 0) h = atomicAdd(fcw(ctl, FC_QHEAD), 1);
       h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(h, 0));
@@ -552,7 +551,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       if (lane == 0) FLOW_EV(5, h, item, x, 0);
 #ifdef TG_FLOW_DBG
       dbg_item = item;
-      if (lane == 0 && f.dbgc) {
+      if (lane == 0 && f.dbgc && ((item >> 24) & 15u) != Q_CLASSIFY) {
         const int it_l = (int)((item >> 28) * NLIST + ((item >> 24) & 15u));
         const uint32_t o = atomicAdd(&f.dbgc[(int64_t)f.C * 16 + ((int64_t)x * FLOW_MAX_K * NLIST + it_l) * f.jcap + (item & 0xFFFFFFu)], 1u);
         if (o && atomicCAS(f.dbg + 4094 * 4, 0u, 98u) == 0u) {
@@ -562,14 +561,32 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
         }
       }
 #endif
-      const unsigned long long rd = run(item, cl);
-      // (readfirstlane returns int: the low half is cast back to 32 bits before it widens, or
-      // lane 31's bit sign-extends over lanes 32-63 and the wave classifies chunks never ready)
-      ready = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rd >> 32)) << 32) |
-              (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rd);
-      tn = __builtin_amdgcn_readfirstlane((int)(item >> 28) + 1);
-      FLOW_DBG(4, h, item, (uint32_t)__popcll(ready));
-      continue;
+      t = (int)(item >> 28);
+      if (((item >> 24) & 15u) == Q_CLASSIFY) {  // a chunk another wave's run item completed
+        c = (int)(item & 0xFFFFFFu);
+      } else {
+        const unsigned long long rd = run(item, cl);
+        // (readfirstlane returns int: each half is cast back to 32 bits before it widens, or
+        // lane 31's bit sign-extends over lanes 32-63)
+        const unsigned long long ready =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rd >> 32)) << 32) |
+            (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rd);
+        FLOW_DBG(4, h, item, (uint32_t)__popcll(ready));
+        if (!ready) continue;
+        ++t;
+        if (t >= K) {  // chunks done with the last step
+          if (lane == 0) {
+            const int nr = __popcll(ready);
+            if (atomicAdd(fcw(ctl, FC_FIN), nr) + nr == Cx)
+              __hip_atomic_store(fcw(ctl, FC_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          continue;
+        }
+        // the first completed chunk is classified here, the others by whichever waves take them
+        const int l0 = __ffsll((long long)ready) - 1;
+        c = __builtin_amdgcn_readlane(cl, l0);
+        if (((ready >> lane) & 1ull) && lane != l0) push(t, Q_CLASSIFY, cl, 3);
+      }
     }
     // chunk c at step t: classified, or, past the last step, finished
     if (t >= K) {
@@ -580,8 +597,6 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     FLOW_DBG(10 + t, c, x, 0);
 #ifdef TG_FLOW_DBG
     if (lane == 0) FLOW_EV(1, c, t, path, x);
-#endif
-#ifdef TG_FLOW_DBG
     if (lane == 0 && f.dbgc) {
       const uint32_t o = atomicAdd(&f.dbgc[(int64_t)c * 16 + t], 1u);
       if (o) {  // a duplicate classification: the first one seen goes to slot 4095

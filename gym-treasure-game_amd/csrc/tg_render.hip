@@ -28,7 +28,6 @@
 // the reference (pygame is absent here); pinned against the oracle's restatement.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -46,17 +45,11 @@ struct RenderState {
   uint4* tiles = nullptr;        // static layer + each cell-aligned sprite, per cell
   uint32_t* spr = nullptr;       // [D_COUNT][48*48] ARGB
   uint64_t knob = 0;             // knob half widths + 1, 4 bits per row dy = -4..4
-  // the sweep form's per-env items (k_render_prep), for up to `cap` envs per call
-  void* items = nullptr;
-  uint16_t* rows = nullptr;
-  uint16_t* sels = nullptr;
-  int64_t cap = 0;
-  int sweep_grid = 0;
 };
 
 void render_free(RenderState* rs) {
   if (!rs) return;
-  void* bufs[] = {rs->bg, rs->tiles, rs->spr, rs->items, rs->rows, rs->sels};
+  void* bufs[] = {rs->bg, rs->tiles, rs->spr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   delete rs;
@@ -139,112 +132,6 @@ __global__ __launch_bounds__(RBLOCK) void k_render(RenderArgs A, const uint4* __
   }
 }
 
-// ---- the sweep form: every frame byte in address order ----------------------
-// k_render's workgroups each stream their own band pieces of 4 frames (~2,000 workgroups x 4
-// streams of 96 KB at once) and reach 0.65-0.68 of 8 TB/s against the 0.87 of a memset of the
-// same buffer, whose waves sweep one contiguous window.  Here a prep pass stores each env's
-// items once (its layers, live mask, the item mask of every pixel row and each band's cell
-// sources: ~2.6 KB per env), and the sweep's waves take 1-KB segments of the whole frame
-// buffer in address order (wave w: segments w, w + nw, ...): the bytes being written at any
-// moment are one window of nw KB, as a fill's.  A chunk is composited exactly as k_render
-// composites it (render_chunk, the same per-chunk code).
-struct EnvItems {
-  Layer lay[NLAYER];
-  uint32_t live, pad[3];
-};
-// one workgroup per env: its layers (thread i < NLAYER), then its row masks and cell sources
-__global__ __launch_bounds__(RBLOCK) void k_render_prep(RenderArgs A, const uint4* __restrict__ st4,
-                                                        const double2* __restrict__ angs,
-                                                        int64_t first, EnvItems* __restrict__ items,
-                                                        uint16_t* __restrict__ rows,
-                                                        uint16_t* __restrict__ sels) {
-  __shared__ Layer lay[NLAYER];
-  __shared__ uint32_t live;
-  const int64_t e = blockIdx.x;
-  if (threadIdx.x == 0) live = 0u;
-  __syncthreads();
-  if (threadIdx.x < NLAYER) {
-    Layer l;
-    bool on = false;
-    const int64_t g = first + e;
-    const uint32_t err = make_layer(A, (int)threadIdx.x, st4[g], angs[g], l, on);
-    if (err) atomicOr(A.err, err);
-    if (on && l.y1 > 0 && l.y0 < A.Hpx && l.x1 > 0 && l.x0 < A.Wpx) {
-      lay[threadIdx.x] = l;
-      atomicOr(&live, 1u << threadIdx.x);
-    }
-  }
-  __syncthreads();
-  const uint32_t lv = live;
-  EnvItems* const it = items + e;
-  if (threadIdx.x < NLAYER && ((lv >> threadIdx.x) & 1u)) it->lay[threadIdx.x] = lay[threadIdx.x];
-  if (threadIdx.x == 0) it->live = lv;
-  for (int y = threadIdx.x; y < A.Hpx; y += RBLOCK) rows[e * A.Hpx + y] = (uint16_t)row_items(lay, lv, y);
-  if ((int)threadIdx.x < A.H) cell_sources(lay, lv, (int)threadIdx.x, A.W, sels + (e * A.H + threadIdx.x) * A.W);
-}
-constexpr int SU = 4;  // the sweep's segments in flight per wave
-// wave gw of nw: 1-KB segments gw, gw + nw, ... of the frames [0, count) (16-B chunks, 64 per
-// segment; a frame is Hpx * CH chunks, whole lines of 16 B, and may end inside a segment)
-__global__ __launch_bounds__(RBLOCK) void k_render_sweep(RenderArgs A, const EnvItems* __restrict__ items,
-                                                         const uint16_t* __restrict__ rows,
-                                                         const uint16_t* __restrict__ sels, int64_t count,
-                                                         uint4* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * (RBLOCK / 64);
-  const int fc = A.Hpx * A.CH;  // chunks per frame
-  const int64_t nseg = (count * fc + 63) >> 6;
-  // SU segments per iteration (seg + u * nw), their loads issued together: one segment at a
-  // time left each wave a chain of dependent loads per KB stored.  Each segment start is kept
-  // as (frame, chunk of it) and advanced by SU * nw segments = dq frames + dr chunks (one 64-bit
-  // division per wave, not per segment).
-  const int64_t seg0 = (int64_t)blockIdx.x * (RBLOCK / 64) + (threadIdx.x >> 6);
-  int64_t fe[SU];
-  int ff[SU];
-#pragma unroll
-  for (int u = 0; u < SU; ++u) {
-    const int64_t c = (seg0 + u * nw) * 64;
-    fe[u] = c / fc;
-    ff[u] = (int)(c - fe[u] * fc);
-  }
-  const int64_t dq = SU * nw * 64 / fc;
-  const int dr = (int)(SU * nw * 64 - dq * fc);
-  for (int64_t seg = seg0; seg < nseg; seg += SU * nw) {
-    int64_t e[SU];
-    int ci[SU];
-    uint32_t rm[SU];
-    uint4 v[SU];
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      e[u] = fe[u];
-      ci[u] = ff[u] + lane;
-      if (ci[u] >= fc) {  // the segment runs into the next frame
-        ci[u] -= fc;
-        ++e[u];
-      }
-      fe[u] += dq;
-      ff[u] += dr;
-      if (ff[u] >= fc) {
-        ff[u] -= fc;
-        ++fe[u];
-      }
-      const bool ok = e[u] < count;
-      const int r = ci[u] / A.CH;
-      rm[u] = ok ? rows[e[u] * A.Hpx + r] : 0u;
-      v[u] = A.bg[ok ? ci[u] : 0];
-    }
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      if (e[u] >= count) continue;
-      uint4 o = v[u];
-      if (rm[u]) {
-        const int r = ci[u] / A.CH, q = ci[u] - r * A.CH, band = r / RS;
-        o = render_chunk(A, items[e[u]].lay, rm[u], sels + (e[u] * A.H + band) * A.W, band, r - band * RS, q, v[u]);
-      }
-      store16(out + (seg + u * nw) * 64 + lane, o);
-    }
-  }
-}
-
 }  // namespace
 }  // namespace tg
 
@@ -317,31 +204,6 @@ int tg_render(tg_batch* h, int64_t first, int64_t count, uint8_t* rgb, void* str
   for (int k = 0; k < 3; ++k) A.door_cx[k] = h->L.door_cx[k], A.door_cy[k] = h->L.door_cy[k];
   for (int k = 0; k < 2; ++k) A.handle_cx[k] = h->L.handle_cx[k], A.handle_cy[k] = h->L.handle_cy[k];
   A.bolt_cx = h->L.bolt_cx, A.bolt_cy = h->L.bolt_cy;
-  if (getenv("TG_RENDER_SWEEP")) {  // (A/B) the sweep form, below
-    RenderState* w = h->rs;
-    if (w->cap < count) {
-      for (void* b : {w->items, (void*)w->rows, (void*)w->sels})
-        if (b) (void)hipFree(b);
-      w->items = nullptr, w->rows = w->sels = nullptr, w->cap = 0;
-      if (hipMalloc(&w->items, sizeof(EnvItems) * (size_t)count) != hipSuccess ||
-          hipMalloc((void**)&w->rows, sizeof(uint16_t) * (size_t)count * rs->Hpx) != hipSuccess ||
-          hipMalloc((void**)&w->sels, sizeof(uint16_t) * (size_t)count * h->L.H * h->L.W) != hipSuccess)
-        return fail(TG_E_NOMEM, "tg_render: sweep buffers for %lld envs", (long long)count);
-      w->cap = count;
-    }
-    if (!w->sweep_grid) {
-      int nb = 0;
-      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k_render_sweep),
-                                                           RBLOCK, 0));
-      w->sweep_grid = (nb > 0 ? nb : 1) * h->cus;
-    }
-    hipLaunchKernelGGL(k_render_prep, dim3((unsigned)count), dim3(RBLOCK), 0, (hipStream_t)stream, A,
-                       h->S.st4, h->S.ang, first, (EnvItems*)w->items, w->rows, w->sels);
-    hipLaunchKernelGGL(k_render_sweep, dim3((unsigned)w->sweep_grid), dim3(RBLOCK), 0, (hipStream_t)stream,
-                       A, (const EnvItems*)w->items, w->rows, w->sels, count, reinterpret_cast<uint4*>(rgb));
-    HIP_TRY(hipGetLastError());
-    return TG_OK;
-  }
   const int64_t blocks = (count + RG - 1) / RG * h->L.H;
   if (blocks > 0x7FFFFFFF) return fail(TG_E_INVAL, "tg_render: too many envs in one call");
   hipLaunchKernelGGL(k_render, dim3((unsigned)blocks), dim3(RBLOCK), 0, (hipStream_t)stream, A,

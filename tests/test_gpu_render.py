@@ -138,29 +138,3 @@ def test_render_other_level_vs_oracle(tg, oracle):
     assert vec.errors() == 0
     vec.close()
 
-
-@pytest.mark.parametrize("case", ["default", "ragged", "corridor"])
-def test_render_sweep_equals_bands(tg, monkeypatch, case):
-    """The sweep form (k_render_prep + k_render_sweep, TG_RENDER_SWEEP) writes the same bytes
-    as k_render: frames of 1,257,984 B end inside a sweep segment, the corridor's do not."""
-    import os
-    level = None
-    n, steps = 48, 12
-    if case == "ragged":
-        n = 301
-    if case == "corridor":
-        level = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", "corridor")
-    vec = tg.TreasureGameVec(n, seed=4, autoreset=True, level_dir=level)
-    vec.render_init(tg.synthetic_sprites(seed=6))
-    vec.reset()
-    for t in range(steps):
-        vec.step(vec.policy_actions(t, 0x51, "masked"))
-    monkeypatch.delenv("TG_RENDER_SWEEP", raising=False)
-    bands = vec.render().clone()
-    monkeypatch.setenv("TG_RENDER_SWEEP", "1")
-    sweep = vec.render()
-    assert torch.equal(sweep, bands)
-    part = vec.render(first=7, count=n - 9)
-    assert torch.equal(part, bands[7:n - 2])
-    assert vec.errors() == 0
-    vec.close()
