@@ -322,26 +322,39 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       runs = k >= 0 && can_run(L, m, e, k);
       if (k < 0) e.f |= E_ACTION;
     }
-    if (live) st.valid[i] = (uint8_t)runs;  // every env's valid row, coalesced (as k_classify)
     const bool rst = AR && live && !runs && is_done(e);  // entering done: reset (L_RESET)
     const int bk = runs ? k : rst ? L_RESET : -1;
-    // stale MT halves not listed yet go on k_regen's list c % SHARDS
-    {
-      const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
-      const unsigned long long b = __ballot(stale);
-      if (b) {
-        const int sh = c % SHARDS;
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&f.rcnt[sh * CTR_STRIDE], __popcll(b));
-        base = __builtin_amdgcn_readlane(base, 0);
-        if (stale) {
-          f.refill[sh * f.rcap + base + __popcll(b & lt_mask)] =
-              (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
-          e.mti |= MT_LISTED;
-        }
+    // The atomics that reserve this chunk's places go out first, their round trips overlapping
+    // the rows below (each one on the chain cost a classification ~1 us, the r05h event log):
+    // stale MT halves not listed yet go on k_regen's list c % SHARDS ...
+    const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
+    const unsigned long long sb = __ballot(stale);
+    int sbase = 0;
+    if (sb && lane == 0) sbase = atomicAdd(&f.rcnt[(c % SHARDS) * CTR_STRIDE], __popcll(sb));
+    if (stale) e.mti |= MT_LISTED;
+    // ... and the listed lanes, grouped by list (rank in the group, its first lane and size),
+    // reserve their entries
+    const unsigned long long lb = __ballot(bk >= 0);
+    const int cnt = __popcll(lb);
+    int rank = 0, lead = 0, nb = 0;
+    unsigned long long pend = lb;
+    while (pend) {
+      const int first = __ffsll((long long)pend) - 1;
+      const int b0 = __builtin_amdgcn_readlane(bk, first);
+      const unsigned long long b = __ballot(bk == b0);
+      if (bk == b0) {
+        rank = __popcll(b & lt_mask);
+        lead = first;
+        nb = __popcll(b);
       }
+      pend &= ~b;
     }
-    // envs whose option cannot run: reward None, state unchanged (TG/:91-96, OP/:22-23)
+    const int lidx = t * NLIST + (bk >= 0 ? bk : 0);
+    int base = 0;
+    if (bk >= 0 && lane == lead) base = atomicAdd(fcw(ctl, FC_LTAIL + lidx), nb);
+    // every env's valid row, coalesced (as k_classify); the rows of the envs whose option cannot
+    // run: reward None, state unchanged (TG/:91-96, OP/:22-23)
+    if (live) st.valid[i] = (uint8_t)runs;
     const bool fin = live && !runs && !rst;
     double orow[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (fin) {
@@ -353,50 +366,37 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     }
     if (fin && (e.f & E_MASK)) atomicOr(err_or, e.f & E_MASK);
     store_obs_wave(st.obs, (int64_t)c * 64, __ballot(fin), orow, reinterpret_cast<double*>(warea));
+    // the handed-off bytes: refill entries, list entries, the state, the chunk's count
+    sbase = __builtin_amdgcn_readlane(sbase, 0);
+    if (stale)
+      f.refill[(c % SHARDS) * f.rcap + sbase + __popcll(sb & lt_mask)] =
+          (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
+    base = __shfl(base, lead, 64);
+    if (bk >= 0) st_sc1(list + (int64_t)lidx * f.lcap + base + rank, (int32_t)i);
     if (live) {
       const uint4 s4n = pack(e);
       if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w)
         st16_sc1(S.st4, (uint32_t)i * 16u, s4n);
     }
-    const unsigned long long lb = __ballot(bk >= 0);
-    const int cnt = __popcll(lb);
-    if (cnt) {
-      if (lane == 0) st_sc1(f.outst + c, cnt);
-      // the listed lanes, grouped by list: rank in the group, its first lane and size
-      int rank = 0, lead = 0, nb = 0;
-      unsigned long long pend = lb;
-      while (pend) {
-        const int first = __ffsll((long long)pend) - 1;
-        const int b0 = __builtin_amdgcn_readlane(bk, first);
-        const unsigned long long b = __ballot(bk == b0);
-        if (bk == b0) {
-          rank = __popcll(b & lt_mask);
-          lead = first;
-          nb = __popcll(b);
-        }
-        pend &= ~b;
-      }
-      const int lidx = t * NLIST + (bk >= 0 ? bk : 0);
-      int base = 0;
-      if (bk >= 0 && lane == lead) base = atomicAdd(fcw(ctl, FC_LTAIL + lidx), nb);
-      base = __shfl(base, lead, 64);
-      if (bk >= 0) st_sc1(list + (int64_t)lidx * f.lcap + base + rank, (int32_t)i);
-      // publish: this wave's stores (entries, state, rows, outst) first
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (bk >= 0 && lane == lead) {
-        int32_t* const fl = fill + (int64_t)lidx * f.jcap;
-        const int j0 = base >> 6, in0 = min(nb, 64 - (base & 63));
-        if (atomicAdd(&fl[j0], in0) + in0 == 64) push(t, bk, j0, 0);
-        if (nb > in0 && atomicAdd(&fl[j0 + 1], nb - in0) + (nb - in0) == 64) push(t, bk, j0 + 1, 1);
-      }
-    } else {
-      // the chain goes on with this chunk's next step in this wave: its stores land first
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (cnt && lane == 0) st_sc1(f.outst + c, cnt);
+    // publish: this wave's stores first (with no listed env, the chain goes on with the chunk's
+    // next step in this wave: its stores land first too); then the fill counts and the step's
+    // classified-chunk count together (the flush reads only the list tails, reserved above)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int32_t* const fl = fill + (int64_t)lidx * f.jcap;
+    const int j0 = base >> 6, in0 = min(nb, 64 - (base & 63));
+    int f0 = 0, f1 = 0, last = 0;
+    if (bk >= 0 && lane == lead) {
+      f0 = atomicAdd(&fl[j0], in0) + in0;
+      if (nb > in0) f1 = atomicAdd(&fl[j0 + 1], nb - in0) + (nb - in0);
+    }
+    if (lane == 0) last = atomicAdd(fcw(ctl, FC_CLS + t), 1) + 1 == Cx;
+    if (bk >= 0 && lane == lead) {
+      if (f0 == 64) push(t, bk, j0, 0);
+      if (f1 == 64) push(t, bk, j0 + 1, 1);
     }
     wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, 0, 0, false, slot);
     // the last chunk classified for step t flushes step t's partial list chunks
-    int last = 0;
-    if (lane == 0) last = atomicAdd(fcw(ctl, FC_CLS + t), 1) + 1 == Cx;
     if (lane == 0) FLOW_EV(2, c, t, cnt, x);
     if (__builtin_amdgcn_readlane(last, 0) && lane < NLIST) {
       const int tail = ld_sc1(fcw(ctl, FC_LTAIL + t * NLIST + lane));
