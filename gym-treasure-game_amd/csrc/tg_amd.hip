@@ -206,15 +206,15 @@ __device__ __noinline__ void regen_half(uint32_t* mt, uint8_t* mc, uint32_t h) {
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
 }
 // k_flow's form: the half's source words may have been written by another CU of the XCD in the
-// same launch (the env's previous item ran there), so this CU's L1 is invalidated first (an
-// agent-scope acquire, ~2 us on this rare path); the stores reach the XCD's L2, where the env's
-// next item, on whichever CU, reads them (tg_flow.h)
+// same launch (the env's previous item ran there), so this CU's L1 is invalidated first; the
+// stores go through the L1 (write-through) to the XCD's L2, where the env's next item, on
+// whichever CU of the XCD, reads them with L1-bypassing loads (tg_flow.h) once this wave's
+// stores are complete.  No L2 writeback: nothing crosses XCDs (an agent-scope release's
+// buffer_wbl2 here wrote back the XCD's whole L2 on every per-lane regeneration).
 __device__ __noinline__ void regen_half_flow(uint32_t* mt, uint8_t* mc, uint32_t h) {
   asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
   twist_half(mt, h, mc, false, GenCalls());
-  // its words and codes out of this CU (the env's next items may run on another CU of the XCD)
-  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_wbl2 sc1\n\ts_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\t"
-               "s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // a stored MT word read past this CU's L1 (an agent-scope relaxed load: global_load sc1), for

@@ -505,20 +505,6 @@ struct AirCells {
   }
 };
 
-// The same window from whole-column words (the level bitmasks): the OPEN and the blocker rows
-// of columns c0 and c0 + 1, every row (bit r + PAD), so that only a move to another column pair
-// rebuilds it (two loads of each kind, no cell reads); the 3-row masks at py are shifts.
-// (AirCells alone: a lane leaves its 2 x 3 window every ~7 air ticks, so in a 64-lane wave some
-// lane rebuilt it on nearly every tick)
-struct AirCols {
-  uint32_t oa, ob, ba, bb;  // columns c0 / c0 + 1: OPEN rows, WALL-or-closed-door rows
-  int bx;                   // first pixel of column c0 + 1
-  uint32_t dc;
-  TG_HD bool holds_x(uint32_t d, int px) const {
-    return (d == dc) & (px - (HALFW + INCR) < bx) & (px - (HALFW + INCR) >= bx - S);
-  }
-};
-
 // The air tick's predicates inside its window.  With s = bx - px and t = by1 - py the window
 // holds iff s in (-16, 32] and t in [-3, 44], so a probe at px + o lies in column B iff o >= s,
 // and one at py + o in row (o >= t) + (o >= t + 48): row 0 for o = -4, row 1 for o = 44, row 1 +
@@ -565,8 +551,8 @@ struct AirProbe {
 // staged with it; a predicate that would read several cells of one column or row reads one word
 // and tests bits (the ladder and go loops' span limits).  Null: the cell probes.
 constexpr int MK_DIM = 32;
-constexpr int MK_MAX_WORDS = 33 * MK_DIM;  // 9 column tables + 16 row tables + 8 column tables
-TG_HD int mk_words(int W, int H) { return 17 * (W + 2 * PAD) + 16 * (H + 2 * PAD); }
+constexpr int MK_MAX_WORDS = 25 * MK_DIM;  // 9 column tables + 16 row tables
+TG_HD int mk_words(int W, int H) { return 9 * (W + 2 * PAD) + 16 * (H + 2 * PAD); }
 
 struct Map {
   const uint8_t* g;  // LDS on device: (H + 2*PAD) rows of (W + 2*PAD) cells
@@ -582,8 +568,6 @@ struct Map {
   TG_HD uint32_t mk_rowblk(uint32_t dc, int r) const {
     return mk[9 * pw() + ph() * (8 + (int)dc) + r + PAD];
   }
-  // per door state and bordered column the WALL-or-closed-door rows (bit r + PAD)
-  TG_HD uint32_t mk_colblk(uint32_t dc, int c) const { return mk[9 * pw() + 16 * ph() + pw() * (int)dc + c + PAD]; }
   TG_HD uint32_t rbit(int y) const { return (uint32_t)(rowy(y) + PAD); }  // row bit of pixel y
   // object_type_at_cell (IM/:227-230) as cell bits; anything outside the grid is WALL
   TG_HD uint32_t cellb(int cx, int cy) const {
@@ -668,21 +652,6 @@ struct Map {
       bb |= (uint32_t)(is_wall(cb) | is_door(cb, dc)) << ri;
     }
     return AirCells{oa, ob, ba, bb, (c0 + 1) * S, (r0 + 1) * S, dc};
-  }
-  // AirCols at px (mk non-null; the second column clamped as air_cells does)
-  TG_HD AirCols air_cols(uint32_t dc, int px) const {
-    const int c0 = colx(px - (HALFW + INCR)), c1 = c0 + 1 < W + PAD ? c0 + 1 : c0;
-    return AirCols{mk_colopen(dc, c0), mk_colopen(dc, c1), mk_colblk(dc, c0), mk_colblk(dc, c1),
-                   (c0 + 1) * S, dc};
-  }
-  // the AirCells of (px, py) from the column words; false when rowy(py - 4) is clamped or its
-  // three rows pass the bordered grid (as a clamped air_cells window: the caller takes the full
-  // tick)
-  TG_HD bool air_rows(const AirCols& w, int py, AirCells& ac) const {
-    const int r0 = rowy(py - INCR), by1 = (r0 + 1) * S;
-    const uint32_t sh = (uint32_t)(r0 + PAD);
-    ac = AirCells{(w.oa >> sh) & 7u, (w.ob >> sh) & 7u, (w.ba >> sh) & 7u, (w.bb >> sh) & 7u, w.bx, by1, w.dc};
-    return (py - INCR < by1) & (py - INCR >= by1 - S) & (r0 + 2 < H + PAD);
   }
   // integrate y on a downward move of yd <= 4 px (IM/:341-348): with can_fall at py the player
   // falls pixel by pixel while can_fall holds, so the distance is the first k in 1..yd-1 with
@@ -1414,19 +1383,10 @@ TG_HD int ladder_plain_limit(const Map& m, const Env& e, const P& pr) {
 // changes cell column or row every ~12 ticks)
 template <int K, class R>
 TG_HD int air_tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, Opt& o, R& rng,
-                   AirCells& ac, AirCols& aw) {
+                   AirCells& ac) {
   constexpr int DIR = (K == O_JUMP_LEFT || K == O_DOWN_LEFT) ? -1 : 1;
   constexpr bool JUMP = K == O_JUMP_LEFT || K == O_JUMP_RIGHT;
   const uint32_t dc = Map::dc_of(e.f);
-#ifdef TG_AIR_COLS
-  if (m.mk) {  // (wave-uniform) the column-word window: rebuilt on a column change only
-    if (!aw.holds_x(dc, e.px)) aw = m.air_cols(dc, e.px);
-    if (!(m.air_rows(aw, e.py, ac) & aw.holds_x(dc, e.px))) {  // clamped: the full tick
-      const int prim = policy<K>(L, m, e, o);
-      return tick<prims_of(K), R>(L, trig, m, e, prim, rng);
-    }
-  } else
-#endif
   if (!ac.holds(dc, e.px, e.py)) {
     ac = m.air_cells(dc, e.px, e.py);
     if (!ac.holds(dc, e.px, e.py)) {  // a clamped window (a player past the border): full tick
@@ -1434,7 +1394,6 @@ TG_HD int air_tick(const Level& L, const uint32_t* trig, const Map& m, Env& e, O
       return tick<prims_of(K), R>(L, trig, m, e, prim, rng);
     }
   }
-  (void)aw;
   const AirProbe ap(ac, e.px, e.py);
   const bool cf0 = ap.can_fall();
   const bool fwd = ap.side(DIR);
@@ -1585,14 +1544,13 @@ TG_HD void run_option_k(const Level& L, const uint32_t* trig, const Map& m, Env&
   }
   if constexpr (K == O_JUMP_LEFT || K == O_JUMP_RIGHT || K == O_DOWN_LEFT || K == O_DOWN_RIGHT) {
     AirCells ac{0u, 0u, 0u, 0u, -0x40000000, 0, 0u};  // holds nothing: built on the first air tick
-    AirCols aw{0u, 0u, 0u, 0u, -0x40000000, 0u};      // (TG_AIR_COLS) the same
     do {
       rng.phase(0);
       rng.phase(1);
       rng.reserve(TICK_DRAWS);
       rng.phase(2);
       if (o.init) {
-        r.reward += air_tick<K>(L, trig, m, e, o, rng, ac, aw);
+        r.reward += air_tick<K>(L, trig, m, e, o, rng, ac);
       } else {  // the first tick (the jump itself; the drop's target)
         const int prim = policy<K>(L, m, e, o);
         r.reward += tick<prims_of(K), R>(L, trig, m, e, prim, rng);

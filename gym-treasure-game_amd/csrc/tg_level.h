@@ -272,10 +272,7 @@ inline std::vector<uint32_t> build_masks(const Level& L, const std::vector<uint8
           mk[PW * (1 + dc) + ci] |= 1u << ri;
           mk[9 * PW + PH * dc + ri] |= 1u << ci;
         }
-        if (Map::is_wall(c) | Map::is_door(c, dc)) {
-          mk[9 * PW + PH * (8 + dc) + ri] |= 1u << ci;
-          mk[9 * PW + 16 * PH + PW * dc + ci] |= 1u << ri;
-        }
+        if (Map::is_wall(c) | Map::is_door(c, dc)) mk[9 * PW + PH * (8 + dc) + ri] |= 1u << ci;
       }
     }
   return mk;
