@@ -619,6 +619,10 @@ def step_line(args, runner, dt, st, node, world, total):
         cls_b, run_b, regen_b = cls_b / args.groups, run_b / args.groups, regen_b / args.groups
     rl = st.get("regen_launches", 0)
     rt = st.get("regen_timed", 0)
+    grouped = bool(args.rollout and args.groups > 1)
+    if grouped:  #  only the handle's own k_regen launches stamp spans, while every
+        # group's drains count as launches: no regeneration figures for grouped runs
+        rl, rt, regen_b = 0, 0, 0.0
     regen_launch_s = st["regen_ms"] / 1e3 / rt if rt else 0.0
     regen_s = regen_launch_s * rl / launches    # per step
     surv = survey_bytes(st) / launches
@@ -668,6 +672,9 @@ def step_line(args, runner, dt, st, node, world, total):
                     "(the MT regeneration is k_regen's: step.kernels.regen; the whole step: "
                     "step.frac) (DESIGN.md 3.6)"}
     kernels = {"run": run_k}
+    if grouped:
+        kernels["regen"] = {"note": "not reported with --groups > 1: the groups' k_regen launches "
+                                    "are not stamped (the step figures leave it out)"}
     if args.mode != "direct":
         if not flow:
             kernels["classify"] = kern("k_classify", cls_b, cls_s, cls_pmc)

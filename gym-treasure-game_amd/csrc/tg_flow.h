@@ -316,6 +316,9 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     bool runs = false;
     if (live) {
       unpack_st4(s4, e);
+#ifdef TG_FLOW_WAVELOG
+      if (lane == 0) FLOW_EV(11, c, t, 0, 0);  // (timing log: the state loads returned)
+#endif
       const int act = policy_action(L, m, e, POL, io.a0, g0 + i, io.t0 + t);
       if (io.actions) io.actions[(int64_t)t * n + i] = act;
       k = option_index(act);
@@ -366,6 +369,9 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     }
     if (fin && (e.f & E_MASK)) atomicOr(err_or, e.f & E_MASK);
     store_obs_wave(st.obs, (int64_t)c * 64, __ballot(fin), orow, reinterpret_cast<double*>(warea));
+#ifdef TG_FLOW_WAVELOG
+    if (lane == 0) FLOW_EV(12, c, t, 0, 0);  // (timing log: the rows issued)
+#endif
     // the handed-off bytes: refill entries, list entries, the state, the chunk's count
     sbase = __builtin_amdgcn_readlane(sbase, 0);
     if (stale)
@@ -383,6 +389,9 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     // next step in this wave: its stores land first too); then the fill counts and the step's
     // classified-chunk count together (the flush reads only the list tails, reserved above)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef TG_FLOW_WAVELOG
+    if (lane == 0) FLOW_EV(13, c, t, 0, 0);  // (timing log: the stores complete)
+#endif
     int32_t* const fl = fill + (int64_t)lidx * f.jcap;
     const int j0 = base >> 6, in0 = min(nb, 64 - (base & 63));
     int f0 = 0, f1 = 0, last = 0;

@@ -120,6 +120,20 @@ def timing(path):
             continue
         print("  %-9s %5.1f %%  n %7d  median %7.2f us  p90 %7.2f us  max %8.2f us" % (
             k, 100 * tot[k] / allt, len(d), np.median(d), np.percentile(d, 90), d.max()))
+    # classification phases (TG_FLOW_WAVELOG builds: 11 loads returned, 12 rows issued, 13
+    # stores complete; 1 start, 2 end)
+    ph = defaultdict(list)
+    last = {}
+    for r, tm in zip(ev, clk):
+        ty, w = int(r[0]), int(r[5])
+        if ty in (1, 11, 12, 13, 2):
+            if ty != 1 and w in last:
+                ph[(last[w][0], ty)].append(tm - last[w][1])
+            last[w] = (ty, tm)
+    for (a, b), d in sorted(ph.items()):
+        if len(d) > 1000:
+            d = np.array(d) / 100
+            print("  classify phase %2d -> %2d: n %7d  median %6.2f us  p90 %6.2f us" % (a, b, len(d), np.median(d), np.percentile(d, 90)))
     print("  last classification of step t at (us):", " ".join("%d:%.0f" % (t, step_last[t] / 100) for t in sorted(step_last)))
 
 
