@@ -838,6 +838,13 @@ struct Work {
   int32_t* __restrict__ rcnt;
   int64_t rcap;
   int64_t shard_cap;
+  // TG_MODE_OVERLAP (tg_rollout): per env, listed in this step's worklists (written by every
+  // k_classify part) / in the previous step's (read by part 1); part 2's envs are the previous
+  // step's worklist entries (its lists and counters).  Null in the other modes.
+  uint8_t* __restrict__ lcur;
+  const uint8_t* __restrict__ lprev;
+  const int32_t* __restrict__ plists;
+  const int32_t* __restrict__ pctr;
 };
 // worklist order = the order the chunks' loads reach HBM at the kernel's start (all option
 // waves are resident at once and issue their loads together): the jump waves first, whose
@@ -855,13 +862,57 @@ __constant__ int kSegBase[NLIST] = {kRunPos.of[0] * SHARDS, kRunPos.of[1] * SHAR
 
 // 8 waves per SIMD: its 98-106 SGPRs (the level, the step's pointers) held it to 7; forced, 32-55
 // of them spill to VGPR lanes (no VGPR spills, 60 VGPRs).  A/B r04r: uniform 0.1246 vs 0.1258 ms
-// per step in each of 4 rounds; masked within its spread
-template <bool AUTORESET, bool FINAL, int POL = -1>
+// per step in each of 4 rounds; masked within its spread.
+// PART (TG_MODE_OVERLAP, tg_rollout): 0 every env; 1 the envs NOT listed in the previous step
+// (their state is final once that step's classification is done: run on a second stream while
+// the previous k_run's option chains finish); 2 the previous step's listed envs, one lane per
+// worklist entry, after that k_run
+template <bool AUTORESET, bool FINAL, int POL = -1, int PART = 0>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_classify(
     Soa S, int64_t n, Level L, const uint32_t* __restrict__ grid, StepIO io, EpQueue q, Work w,
     int64_t g0, unsigned long long* __restrict__ stats, uint32_t* __restrict__ err_or,
     unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
+  if (blockIdx.x == 0)  // the next step's counters (their last reader has finished)
+    for (int c = threadIdx.x; c < NCTR; c += BLOCK) w.ctr_next[c * CTR_STRIDE] = 0;
+  // part 2: this lane's entry of the previous step's worklists (a dense enumeration of their
+  // segments: pre[s] = entries before segment s)
+  __shared__ int ppre[PART == 2 ? NSEG + 1 : 1];
+  __shared__ int pwt[PART == 2 ? BLOCK / 64 : 1];
+  int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if constexpr (PART == 2) {
+    const int s0 = 2 * (int)threadIdx.x, ln = threadIdx.x & 63;
+    const int c0 = s0 < NSEG ? w.pctr[s0 * CTR_STRIDE] : 0;
+    const int c1 = s0 + 1 < NSEG ? w.pctr[(s0 + 1) * CTR_STRIDE] : 0;
+    int v = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(v, o, 64);
+      if (ln >= o) v += y;
+    }
+    if (ln == 63) pwt[threadIdx.x >> 6] = v;
+    __syncthreads();
+    for (int wv = 0; wv < (int)(threadIdx.x >> 6); ++wv) v += pwt[wv];
+    const int excl = v - c0 - c1;
+    if (s0 < NSEG) ppre[s0] = excl;
+    if (s0 + 1 < NSEG) ppre[s0 + 1] = excl + c0;
+    if (threadIdx.x == BLOCK - 1) ppre[NSEG] = v;
+    __syncthreads();
+    if ((int64_t)blockIdx.x * BLOCK >= ppre[NSEG]) {  // past the entries (the grid covers n)
+      kst_end(ks, kt0);
+      return;
+    }
+    const int g = (int)i;
+    i = n;  // (no entry: not live)
+    if (g < ppre[NSEG]) {
+      int lo = 0, hi = NSEG;  // ppre[lo] <= g < ppre[hi]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (ppre[mid] <= g) lo = mid; else hi = mid;
+      }
+      i = w.plists[(int64_t)lo * w.shard_cap + (g - ppre[lo])];
+    }
+  }
   __shared__ int bcnt[NLIST], bbase[NLIST];
   __shared__ int rwc[BLOCK / 64], rbase;  // stale halves per wave; the workgroup's list range
   // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
@@ -873,9 +924,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   LdsLevel& lv = lds.lv;
   double* const ostage = lds.ostage;
   double orow[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const bool live = i < n;
   const int lane = threadIdx.x & 63;
+  // part 1 leaves the previous step's listed envs to part 2 (loaded with the state below, so
+  // the test costs no round trip of its own)
+  bool live = i < n;
+  uint8_t was_listed = 0;
+  if constexpr (PART == 1)
+    if (live) was_listed = w.lprev[i];
   // every load this lane may need, issued before the level staging and the barriers so their
   // latencies overlap (the angles / episode words only matter if the option cannot run)
   uint4 s4 = make_uint4(0, 0, 0, 0);
@@ -889,9 +944,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     ep = S.ep[i];
   }
   if (threadIdx.x < NLIST) bcnt[threadIdx.x] = 0;
-  if (blockIdx.x == 0)
-    for (int c = threadIdx.x; c < NCTR; c += BLOCK) w.ctr_next[c * CTR_STRIDE] = 0;
   stage_level(lv, grid, L);  // includes the barrier
+  if constexpr (PART == 1) live = live && !was_listed;
   const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
   int k = -1;
   bool runs = false;
@@ -913,6 +967,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   // entering done with auto-reset on and no option to run: reset in k_run (L_RESET)
   const bool rst = AUTORESET && live && !runs && is_done(e);
   const int bk = runs ? k : rst ? L_RESET : -1;  // the env's worklist
+  if (w.lcur && live) w.lcur[i] = (uint8_t)(bk >= 0);
   // halves left stale and not listed yet go on this step's refill list (MT_LISTED); k_regen
   // regenerates the lists of several steps at once (a lane that needs a half first does it
   // itself: the ring leaves >= ~2,400 draws of slack, launch_step)
@@ -972,7 +1027,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   const int2 ep_in = ep;
-  store_obs_wave(io.obs, i - lane, __ballot(fin), orow, ostage + (threadIdx.x & ~63) * 9);
+  if constexpr (PART == 2) {  // (scattered envs: each lane its own row)
+    if (fin) store_obs(io.obs, i, orow);
+  } else {
+    store_obs_wave(io.obs, i - lane, __ballot(fin), orow, ostage + (threadIdx.x & ~63) * 9);
+  }
   if (fin) {
     const uint4 s4n = pack(e);
     if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w) {  // reset / flag
@@ -1614,14 +1673,14 @@ int alloc_ctx(StepCtx& c, int64_t off, int64_t n) {
   ALLOC_C(c.wst4, sizeof(uint4) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wang, sizeof(double2) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wep, sizeof(int2) * NSEG * (size_t)c.shard_cap);
-  ALLOC_C(c.wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
+  ALLOC_C(c.wctr, sizeof(int32_t) * 3 * NCTR * CTR_STRIDE);
   // a shard's list holds at most its workgroups' envs per pending step
   c.rcap = c.shard_cap * REGEN_STEPS;
   ALLOC_C(c.refill, sizeof(uint32_t) * SHARDS * (size_t)c.rcap);
   ALLOC_C(c.regen_ctr, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE);
 #undef ALLOC_C
   HIP_TRY(hipMemset(c.stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)));
-  HIP_TRY(hipMemset(c.wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE));
+  HIP_TRY(hipMemset(c.wctr, 0, sizeof(int32_t) * 3 * NCTR * CTR_STRIDE));
   HIP_TRY(hipMemset(c.regen_ctr, 0, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE));
   return TG_OK;
 }
@@ -1637,6 +1696,7 @@ void free_ctx(StepCtx& c) {
 
 namespace {
 void flow_free(tg_batch* h);  // TG_MODE_FLOW's buffers (below)
+void ov_free(tg_batch* h);    // TG_MODE_OVERLAP's (below)
 }
 
 extern "C" {
@@ -1745,6 +1805,7 @@ void tg_destroy(tg_batch* h) {
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   render_free(h->rs);
   flow_free(h);
+  ov_free(h);
   void* bufs[] = {h->grid, h->genrand, h->gotab, h->masks, h->obs_q, h->S.st4, h->S.ang, h->S.ep,
                   h->S.mt, h->S.mc, h->eps, h->eps_count, h->err, h->obs_scratch, h->kst};
   for (void* b : bufs)
@@ -1850,16 +1911,16 @@ int launch_step(tg_batch* h, StepCtx& c, const StepIO& io_in, bool ar, hipStream
     hipLaunchKernelGGL(kern, grid, block, 0, st, S, c.n, h->L, h->grid, io, q, g0, c.stats, h->err,
                        ks1);
   } else {
-    // counters double-buffered by step parity: k_classify zeroes the next step's set (the
-    // previous k_run, which read it, has finished), so no memset launch per step
-    int32_t* const cur = c.wctr + (c.parity ? NCTR * CTR_STRIDE : 0);
-    int32_t* const nxt = c.wctr + (c.parity ? 0 : NCTR * CTR_STRIDE);
-    c.parity ^= 1;
+    // counters in three sets by step: k_classify zeroes the next step's set (the k_run two
+    // steps back, which read it, has finished), so no memset launch per step
+    int32_t* const cur = c.wctr + c.cset * NCTR * CTR_STRIDE;
+    int32_t* const nxt = c.wctr + ((c.cset + 1) % 3) * NCTR * CTR_STRIDE;
+    c.cset = (c.cset + 1) % 3;
     // the refill lists append until k_regen drains them (every REGEN_STEPS steps), counted in
     // the set the next k_regen reads
     const Work w{c.wl,     c.wst4, c.wang, c.wep, cur, nxt, c.refill,
                  c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
-                 c.shard_cap};
+                 c.shard_cap, nullptr, nullptr, nullptr, nullptr};
     decltype(&k_classify<true, true>) kc;
     if (io.policy == TG_POLICY_UNIFORM)
       kc = ar ? (fo ? k_classify<true, true, 0> : k_classify<true, false, 0>)
@@ -1891,6 +1952,110 @@ int regen_all(tg_batch* h, hipStream_t st) {
   for (auto& c : h->grp)
     if (!rc) rc = launch_regen(h, c, st);
   return rc;
+}
+
+// ---- TG_MODE_OVERLAP (tg_rollout) -------------------------------------------------------------
+// A step's envs that were not listed in the previous step (its option could not run: reward
+// None, state unchanged) are final once the previous step's classification is done; their
+// classification for this step (k_classify part 1) runs on a second stream while the previous
+// k_run's slowest option chains finish.  The previous step's listed envs are classified after
+// that k_run (part 2, one lane per worklist entry), then this step's k_run waits for both.
+// Only inside tg_rollout, whose steps write distinct [K][N] output rows: with tg_step's shared
+// rows, part 1 of step t + 1 would overwrite rows of step t the caller may still be reading.
+void ov_free(tg_batch* h) {
+  auto& O = h->ov;
+  for (int k = 0; k < 2; ++k) {
+    void* bufs[] = {O.wl[k], O.wst4[k], O.wang[k], O.wep[k], O.listed[k]};
+    for (void* b : bufs)
+      if (b) (void)hipFree(b);
+  }
+  if (O.cls) (void)hipEventDestroy(O.cls);
+  if (O.p1) (void)hipEventDestroy(O.p1);
+  if (O.aux) (void)hipStreamDestroy(O.aux);
+  O = {};
+}
+int ov_init(tg_batch* h) {
+  auto& O = h->ov;
+  if (O.ready) return TG_OK;
+  const StepCtx& c = h->main;
+  O.cap = 2 * c.shard_cap;
+  const size_t ent = (size_t)NSEG * (size_t)O.cap;
+  bool ok = true;
+  for (int k = 0; k < 2 && ok; ++k)
+    ok = hipMalloc((void**)&O.wl[k], sizeof(int32_t) * ent) == hipSuccess &&
+         hipMalloc((void**)&O.wst4[k], sizeof(uint4) * ent) == hipSuccess &&
+         hipMalloc((void**)&O.wang[k], sizeof(double2) * ent) == hipSuccess &&
+         hipMalloc((void**)&O.wep[k], sizeof(int2) * ent) == hipSuccess &&
+         hipMalloc((void**)&O.listed[k], (size_t)h->n) == hipSuccess;
+  ok = ok && hipStreamCreateWithFlags(&O.aux, hipStreamNonBlocking) == hipSuccess &&
+       hipEventCreateWithFlags(&O.cls, hipEventDisableTiming) == hipSuccess &&
+       hipEventCreateWithFlags(&O.p1, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    ov_free(h);
+    return fail(TG_E_NOMEM, "overlap mode: worklists (%zu MB)", ent * 44 * 2 >> 20);
+  }
+  O.ready = true;
+  return TG_OK;
+}
+template <int PART>
+using KcPtr = decltype(&k_classify<true, false, 0, PART>);
+template <int PART>
+KcPtr<PART> kc_part(bool ar, int pol) {
+  return ar ? (pol ? k_classify<true, false, 1, PART> : k_classify<true, false, 0, PART>)
+            : (pol ? k_classify<false, false, 1, PART> : k_classify<false, false, 0, PART>);
+}
+// one overlapped step of tg_rollout (first: the rollout's first step, classified whole)
+int launch_step_ov(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st, uint32_t tstep,
+                   bool first) {
+  auto& O = h->ov;
+  StepCtx& c = h->main;
+  StepIO io = io_in;
+  io.tstep = tstep;
+  const int pol = io.policy == TG_POLICY_MASKED ? 1 : 0;
+  int rc = TG_OK;
+  unsigned long long *ks0 = nullptr, *ks1 = nullptr;
+  timing_begin(h, rc, ks0, ks1);
+  if (rc) return rc;
+  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
+  const dim3 grid(grid_for(c.n)), block(BLOCK);
+  const Soa S = soa_of(h, c);
+  int32_t* const cur = c.wctr + c.cset * NCTR * CTR_STRIDE;
+  int32_t* const nxt = c.wctr + ((c.cset + 1) % 3) * NCTR * CTR_STRIDE;
+  const int32_t* const prv = c.wctr + ((c.cset + 2) % 3) * NCTR * CTR_STRIDE;
+  c.cset = (c.cset + 1) % 3;
+  const int ls = O.set, lp = O.set ^ 1;
+  O.set ^= 1;
+  const Work w{O.wl[ls], O.wst4[ls], O.wang[ls], O.wep[ls], cur, nxt, c.refill,
+               c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
+               O.cap, O.listed[ls], O.listed[lp], O.wl[lp], prv};
+  if (first) {
+    hipLaunchKernelGGL(kc_part<0>(ar, pol), grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w,
+                       h->g0, c.stats, h->err, ks0);
+  } else {
+    // part 1 on the second stream, after the previous step's classification (and k_regen)
+    HIP_TRY(hipStreamWaitEvent(O.aux, O.cls, 0));
+    hipLaunchKernelGGL(kc_part<1>(ar, pol), grid, block, 0, O.aux, S, c.n, h->L, h->grid, io, q,
+                       w, h->g0, c.stats, h->err, nullptr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(O.p1, O.aux));
+    // part 2 after the previous k_run (stream order), then this step's k_run after part 1
+    hipLaunchKernelGGL(kc_part<2>(ar, pol), grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w,
+                       h->g0, c.stats, h->err, ks0);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamWaitEvent(st, O.p1, 0));
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(O.cls, st));  // the next step's part 1 may start
+  auto kr = ar ? k_run<true, false> : k_run<false, false>;
+  hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n) * (BLOCK / RUN_BLOCK)), dim3(RUN_BLOCK), 0, st, S,
+                     c.n, h->L, h->grid, io, q, w, h->g0, c.stats, h->err, ks1);
+  HIP_TRY(hipGetLastError());
+  if (++c.rpend == REGEN_STEPS) {
+    // k_regen rewrites state words: the next step's part 1 waits for it too
+    if ((rc = launch_regen(h, c, st))) return rc;
+    HIP_TRY(hipEventRecord(O.cls, st));
+  }
+  return TG_OK;
 }
 
 // ---- TG_MODE_FLOW (tg_flow.h) ----------------------------------------------------------------
@@ -2239,6 +2404,12 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
     }
     return rc;
   }
+  if (h->grp.empty() && h->mode == TG_MODE_OVERLAP) {
+    int rc = ov_init(h);
+    for (int32_t s = 0; s < steps && !rc; ++s)
+      rc = launch_step_ov(h, io_of(s), ar, cs, tb + (uint32_t)s, s == 0);
+    return rc;
+  }
   if (h->grp.empty() || h->mode != TG_MODE_COMPACT) {
     for (int32_t s = 0; s < steps; ++s) {
       const int rc = launch_step(h, h->main, io_of(s), ar, cs, tb + (uint32_t)s);
@@ -2367,7 +2538,8 @@ int tg_errors(tg_batch* h, uint32_t* out, void* stream) {
 
 int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
   BIND(h);
-  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT && mode != TG_MODE_FLOW)
+  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT && mode != TG_MODE_FLOW &&
+      mode != TG_MODE_OVERLAP)
     return fail(TG_E_INVAL, "tg_set_mode: unknown mode %d", mode);
   h->mode = mode;
   (void)run_blocks;  // reserved
