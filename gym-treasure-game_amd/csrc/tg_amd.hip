@@ -867,19 +867,34 @@ __constant__ int kSegBase[NLIST] = {kRunPos.of[0] * SHARDS, kRunPos.of[1] * SHAR
 // (their state is final once that step's classification is done: run on a second stream while
 // the previous k_run's option chains finish); 2 the previous step's listed envs, one lane per
 // worklist entry, after that k_run
-template <bool AUTORESET, bool FINAL, int POL = -1, int PART = 0>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_classify(
-    Soa S, int64_t n, Level L, const uint32_t* __restrict__ grid, StepIO io, EpQueue q, Work w,
-    int64_t g0, unsigned long long* __restrict__ stats, uint32_t* __restrict__ err_or,
-    unsigned long long* __restrict__ ks) {
+// k_classify's LDS (a struct, so that k_run_cls can overlay it on k_run's)
+struct ClsShared {
+  int bcnt[NLIST], bbase[NLIST];
+  int rwc[BLOCK / 64], rbase;  // stale halves per wave; the workgroup's list range
+  // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
+  // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
+  union {
+    LdsLevel lv;
+    double ostage[BLOCK * 9];
+  } u;
+  int ppre[NSEG + 1];  // part 2: entries before segment s of the previous step's worklists
+  int pwt[BLOCK / 64];
+};
+template <bool AUTORESET, bool FINAL, int POL, int PART>
+__device__ __forceinline__ void classify_body(ClsShared& sh, const int64_t bid, Soa S, int64_t n,
+                                              Level L, const uint32_t* __restrict__ grid,
+                                              StepIO io, EpQueue q, Work w, int64_t g0,
+                                              unsigned long long* __restrict__ stats,
+                                              uint32_t* __restrict__ err_or,
+                                              unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
-  if (blockIdx.x == 0)  // the next step's counters (their last reader has finished)
+  if (bid == 0)  // the next step's counters (their last reader has finished)
     for (int c = threadIdx.x; c < NCTR; c += BLOCK) w.ctr_next[c * CTR_STRIDE] = 0;
   // part 2: this lane's entry of the previous step's worklists (a dense enumeration of their
   // segments: pre[s] = entries before segment s)
-  __shared__ int ppre[PART == 2 ? NSEG + 1 : 1];
-  __shared__ int pwt[PART == 2 ? BLOCK / 64 : 1];
-  int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  int* const ppre = sh.ppre;
+  int* const pwt = sh.pwt;
+  int64_t i = bid * BLOCK + threadIdx.x;
   if constexpr (PART == 2) {
     const int s0 = 2 * (int)threadIdx.x, ln = threadIdx.x & 63;
     const int c0 = s0 < NSEG ? w.pctr[s0 * CTR_STRIDE] : 0;
@@ -898,7 +913,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     if (s0 + 1 < NSEG) ppre[s0 + 1] = excl + c0;
     if (threadIdx.x == BLOCK - 1) ppre[NSEG] = v;
     __syncthreads();
-    if ((int64_t)blockIdx.x * BLOCK >= ppre[NSEG]) {  // past the entries (the grid covers n)
+    if (bid * BLOCK >= ppre[NSEG]) {  // past the entries (the grid covers n)
       kst_end(ks, kt0);
       return;
     }
@@ -913,16 +928,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
       i = w.plists[(int64_t)lo * w.shard_cap + (g - ppre[lo])];
     }
   }
-  __shared__ int bcnt[NLIST], bbase[NLIST];
-  __shared__ int rwc[BLOCK / 64], rbase;  // stale halves per wave; the workgroup's list range
-  // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
-  // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
-  __shared__ union {
-    LdsLevel lv;
-    double ostage[BLOCK * 9];
-  } lds;
-  LdsLevel& lv = lds.lv;
-  double* const ostage = lds.ostage;
+  int* const bcnt = sh.bcnt;
+  int* const bbase = sh.bbase;
+  int* const rwc = sh.rwc;
+  int& rbase = sh.rbase;
+  LdsLevel& lv = sh.u.lv;
+  double* const ostage = sh.u.ostage;
   double orow[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   // part 1 leaves the previous step's listed envs to part 2 (loaded with the state below, so
@@ -1002,7 +1013,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   __syncthreads();
   // the workgroup's worklist ranges: issue the global atomics now, use them after the
   // reward-None envs are finished (their latency overlaps that work)
-  const int shard = blockIdx.x % SHARDS;
+  const int shard = (int)(bid % SHARDS);
   int my_base = 0;
   if (threadIdx.x < NLIST) {
     const int c = bcnt[threadIdx.x];
@@ -1056,8 +1067,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     w.wang[at] = a2;
     w.wep[at] = ep;
   }
-  wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, 0);
+  wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, 0, 0, false, bid);
   kst_end(ks, kt0);
+}
+template <bool AUTORESET, bool FINAL, int POL = -1, int PART = 0>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_classify(
+    Soa S, int64_t n, Level L, const uint32_t* __restrict__ grid, StepIO io, EpQueue q, Work w,
+    int64_t g0, unsigned long long* __restrict__ stats, uint32_t* __restrict__ err_or,
+    unsigned long long* __restrict__ ks) {
+  __shared__ ClsShared sh;
+  classify_body<AUTORESET, FINAL, POL, PART>(sh, blockIdx.x, S, n, L, grid, io, q, w, g0, stats,
+                                             err_or, ks);
 }
 
 #ifdef TG_DIAG_STAMPS
@@ -1072,20 +1092,32 @@ __device__ unsigned long long g_stamps[NSTAMP_WAVES * NSTAMP];
 #define TG_STAMP(v) (void)0
 #endif
 
+// k_run's LDS: the worklists' prefix, the waves' code windows (WIN_WAVE_BYTES each, at offset
+// 0: 16-B aligned for the LDS-DMA), then the level's grid words and bitmasks (Map::mk).  (Sized
+// at launch for the handle's level instead of the largest, with the rows' loads issued before
+// the staging barrier, it measured ~4 % slower for the masked policy: DESIGN.md §3.1.)
+struct RunShared {
+  uint4 lds[((RUN_BLOCK / 64) * WIN_WAVE_BYTES + MAX_CELLS + 4 * MK_MAX_WORDS) / 16];
+  uint32_t ltrig[12];
+  int pre[NSEG + 1];
+  int wtot[RUN_BLOCK / 64];
+  int ostart[NLIST + 1], oraw[NLIST + 1];
+};
 template <bool AUTORESET, bool FINAL>
-__global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
-                                                const uint32_t* __restrict__ grid, StepIO io,
-                                                EpQueue q, Work w, int64_t g0,
-                                                unsigned long long* __restrict__ stats,
-                                                uint32_t* __restrict__ err_or,
-                                                unsigned long long* __restrict__ ks) {
+__device__ __forceinline__ void run_body(RunShared& sh, const int64_t bid, Soa S, int64_t n,
+                                         Level L, const uint32_t* __restrict__ grid, StepIO io,
+                                         EpQueue q, Work w, int64_t g0,
+                                         unsigned long long* __restrict__ stats,
+                                         uint32_t* __restrict__ err_or,
+                                         unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
   // the worklists in run order: pre[s] = envs listed before segment s (exclusive prefix of the
   // counters, two segments per thread), then per option (run order j) its first segment's
   // prefix and its start in the chunk space, where each option is padded to whole chunks
-  __shared__ int pre[NSEG + 1];
-  __shared__ int wtot[RUN_BLOCK / 64];
-  __shared__ int ostart[NLIST + 1], oraw[NLIST + 1];
+  int* const pre = sh.pre;
+  int* const wtot = sh.wtot;
+  int* const ostart = sh.ostart;
+  int* const oraw = sh.oraw;
   {
     const int s0 = 2 * (int)threadIdx.x, ln = threadIdx.x & 63;
     const int c0 = s0 < NSEG ? w.ctr[s0 * CTR_STRIDE] : 0;
@@ -1107,7 +1139,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   __syncthreads();
   // a workgroup past every listed chunk (the grid covers n envs, a uniform step lists ~1 in 5;
   // the options' padding adds < 64 each) leaves before it stages the level: ~3/4 of the grid
-  if ((int)(blockIdx.x * RUN_BLOCK) >= pre[NSEG] + NLIST * 63) {
+  if ((int)(bid * RUN_BLOCK) >= pre[NSEG] + NLIST * 63) {
     kst_end(ks, kt0);
     return;
   }
@@ -1122,9 +1154,14 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     ostart[NLIST] = acc;
     oraw[NLIST] = pre[NSEG];
   }
-  RUN_LEVEL_IN_LDS();  // includes the barrier (ostart / oraw)
+  uint8_t* const win = reinterpret_cast<uint8_t*>(sh.lds);
+  uint32_t* const lgrid = reinterpret_cast<uint32_t*>(win + (RUN_BLOCK / 64) * WIN_WAVE_BYTES);
+  uint32_t* const lmk = lgrid + grid_words(L.W, L.H);
+  stage_cells<RUN_BLOCK>(lgrid, sh.ltrig, grid, L, lmk);  // includes the barrier (ostart / oraw)
+  const uint32_t* const trig = sh.ltrig;
+  const Map m{reinterpret_cast<const uint8_t*>(lgrid), L.W, L.H, L.masks ? lmk : nullptr};
   const int total = ostart[NLIST];
-  const int base = (blockIdx.x * RUN_BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
+  const int base = (int)(bid * RUN_BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
   int oj = 0;  // ostart[oj] <= base < ostart[oj + 1] (wave-uniform)
   while (oj + 1 < NLIST && ostart[oj + 1] <= base) ++oj;
   oj = __builtin_amdgcn_readfirstlane(oj);
@@ -1184,7 +1221,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   }
   // (k_run's grid has BLOCK / RUN_BLOCK workgroups per stats slot, as wave_stats below)
   if (AUTORESET)
-    record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats, (int64_t)blockIdx.x / (BLOCK / RUN_BLOCK));
+    record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats, bid / (BLOCK / RUN_BLOCK));
   if (live) {
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
@@ -1193,7 +1230,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   __builtin_amdgcn_s_setprio(0);
   wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
              regens + (__ballot(lregen != 0) ? wave_sum(lregen) : 0), true,
-             (int64_t)blockIdx.x / (BLOCK / RUN_BLOCK));
+             bid / (BLOCK / RUN_BLOCK));
   kst_end(ks, kt0);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
@@ -1205,7 +1242,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     const int src = bl ? __ffsll((long long)bl) - 1 : 0;
     const unsigned long long a1 = __shfl(t1, src, 64);
     const unsigned long long a2 = __shfl(t2, src, 64);
-    const int wv = (blockIdx.x * RUN_BLOCK + threadIdx.x) >> 6;
+    const int wv = (int)(bid * RUN_BLOCK + threadIdx.x) >> 6;
     const unsigned long long rt3 = __builtin_amdgcn_s_memrealtime();
     // the phases of the lane whose option loop ran longest (the wave's own time)
     int lmax = src;
@@ -1235,6 +1272,39 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
     }
   }
 #endif
+}
+template <bool AUTORESET, bool FINAL>
+__global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
+                                                const uint32_t* __restrict__ grid, StepIO io,
+                                                EpQueue q, Work w, int64_t g0,
+                                                unsigned long long* __restrict__ stats,
+                                                uint32_t* __restrict__ err_or,
+                                                unsigned long long* __restrict__ ks) {
+  __shared__ RunShared sh;
+  run_body<AUTORESET, FINAL>(sh, blockIdx.x, S, n, L, grid, io, q, w, g0, stats, err_or, ks);
+}
+// TG_MODE_OVERLAP (tg_rollout): step t's k_run and step t + 1's k_classify part 1 (the envs not
+// listed in step t, whose state step t's k_run does not touch) in one launch.  Its first rb
+// workgroups are k_run's (most of them leave at once: a uniform step lists ~1 env in 5), the
+// rest part 1's, dispatched behind them, so part 1's waves fill the CUs while the option waves'
+// long chains run.  The two parts share the workgroup's LDS.
+template <bool AUTORESET, int POL>
+__global__ __launch_bounds__(RUN_BLOCK) void k_run_cls(Soa S, int64_t n, Level L,
+                                                    const uint32_t* __restrict__ grid, StepIO io,
+                                                    EpQueue q, Work w, StepIO io1, Work w1,
+                                                    int64_t g0, unsigned long long* __restrict__ stats,
+                                                    uint32_t* __restrict__ err_or, int64_t rb,
+                                                    unsigned long long* __restrict__ ks) {
+  static_assert(RUN_BLOCK == BLOCK, "one workgroup shape for both parts");
+  __shared__ union {
+    RunShared r;
+    ClsShared c;
+  } sh;
+  if ((int64_t)blockIdx.x < rb)
+    run_body<AUTORESET, false>(sh.r, blockIdx.x, S, n, L, grid, io, q, w, g0, stats, err_or, ks);
+  else
+    classify_body<AUTORESET, false, POL, 1>(sh.c, (int64_t)blockIdx.x - rb, S, n, L, grid, io1, q,
+                                            w1, g0, stats, err_or, nullptr);
 }
 
 // ---- deferred regeneration of the listed stale MT halves (k_regen) ----------------------------
@@ -1956,12 +2026,14 @@ int regen_all(tg_batch* h, hipStream_t st) {
 
 // ---- TG_MODE_OVERLAP (tg_rollout) -------------------------------------------------------------
 // A step's envs that were not listed in the previous step (its option could not run: reward
-// None, state unchanged) are final once the previous step's classification is done; their
-// classification for this step (k_classify part 1) runs on a second stream while the previous
-// k_run's slowest option chains finish.  The previous step's listed envs are classified after
-// that k_run (part 2, one lane per worklist entry), then this step's k_run waits for both.
-// Only inside tg_rollout, whose steps write distinct [K][N] output rows: with tg_step's shared
-// rows, part 1 of step t + 1 would overwrite rows of step t the caller may still be reading.
+// None, state unchanged) are final once the previous step's classification is done, so their
+// classification for step t + 1 (k_classify part 1) runs in step t's k_run launch (k_run_cls:
+// its workgroups behind k_run's), filling the CUs while the option chains finish.  The step-t
+// listed envs are classified after it (part 2, one lane per worklist entry), then k_run_cls of
+// step t + 1.  Only inside tg_rollout, whose steps write distinct [K][N] output rows: with
+// tg_step's shared rows, part 1 of step t + 1 would overwrite rows of step t the caller may still
+// be reading.  (A first form ran part 1 as its own kernel on a second stream, waiting on events:
+// slower than the plain rollout, 0.128-0.132 vs 0.104-0.107 ms per uniform step, r05k.)
 void ov_free(tg_batch* h) {
   auto& O = h->ov;
   for (int k = 0; k < 2; ++k) {
@@ -1969,9 +2041,6 @@ void ov_free(tg_batch* h) {
     for (void* b : bufs)
       if (b) (void)hipFree(b);
   }
-  if (O.cls) (void)hipEventDestroy(O.cls);
-  if (O.p1) (void)hipEventDestroy(O.p1);
-  if (O.aux) (void)hipStreamDestroy(O.aux);
   O = {};
 }
 int ov_init(tg_batch* h) {
@@ -1987,9 +2056,6 @@ int ov_init(tg_batch* h) {
          hipMalloc((void**)&O.wang[k], sizeof(double2) * ent) == hipSuccess &&
          hipMalloc((void**)&O.wep[k], sizeof(int2) * ent) == hipSuccess &&
          hipMalloc((void**)&O.listed[k], (size_t)h->n) == hipSuccess;
-  ok = ok && hipStreamCreateWithFlags(&O.aux, hipStreamNonBlocking) == hipSuccess &&
-       hipEventCreateWithFlags(&O.cls, hipEventDisableTiming) == hipSuccess &&
-       hipEventCreateWithFlags(&O.p1, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     ov_free(h);
     return fail(TG_E_NOMEM, "overlap mode: worklists (%zu MB)", ent * 44 * 2 >> 20);
@@ -2004,57 +2070,65 @@ KcPtr<PART> kc_part(bool ar, int pol) {
   return ar ? (pol ? k_classify<true, false, 1, PART> : k_classify<true, false, 0, PART>)
             : (pol ? k_classify<false, false, 1, PART> : k_classify<false, false, 0, PART>);
 }
-// one overlapped step of tg_rollout (first: the rollout's first step, classified whole)
-int launch_step_ov(tg_batch* h, const StepIO& io_in, bool ar, hipStream_t st, uint32_t tstep,
-                   bool first) {
+// K steps of tg_rollout in the overlap form (io_of(s): step s's rows)
+template <class IoOf>
+int ov_rollout(tg_batch* h, int32_t steps, IoOf io_of, bool ar, int policy, hipStream_t st,
+               uint32_t tb) {
+  int rc = ov_init(h);
+  if (rc) return rc;
   auto& O = h->ov;
   StepCtx& c = h->main;
-  StepIO io = io_in;
-  io.tstep = tstep;
-  const int pol = io.policy == TG_POLICY_MASKED ? 1 : 0;
-  int rc = TG_OK;
-  unsigned long long *ks0 = nullptr, *ks1 = nullptr;
-  timing_begin(h, rc, ks0, ks1);
-  if (rc) return rc;
+  const int pol = policy == TG_POLICY_MASKED ? 1 : 0;
+  const int cs0 = c.cset, ls0 = O.set;
+  // step s's worklists (set parity), counters (three sets), listed flags; the previous step's
+  // (part 2's envs); the refill lists' counter of the set the next k_regen drains
+  auto work = [&](int32_t s) {
+    const int ls = (ls0 + s) & 1, lp = ls ^ 1;
+    return Work{O.wl[ls], O.wst4[ls], O.wang[ls], O.wep[ls],
+                c.wctr + ((cs0 + s) % 3) * NCTR * CTR_STRIDE,
+                c.wctr + ((cs0 + s + 1) % 3) * NCTR * CTR_STRIDE, c.refill,
+                c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap, O.cap,
+                O.listed[ls], O.listed[lp], O.wl[lp], c.wctr + ((cs0 + s + 2) % 3) * NCTR * CTR_STRIDE};
+  };
+  auto io_at = [&](int32_t s) {
+    StepIO io = io_of(s);
+    io.tstep = tb + (uint32_t)s;
+    return io;
+  };
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
   const dim3 grid(grid_for(c.n)), block(BLOCK);
+  const int64_t rb = (int64_t)run_grid_for(c.n) * (BLOCK / RUN_BLOCK);
   const Soa S = soa_of(h, c);
-  int32_t* const cur = c.wctr + c.cset * NCTR * CTR_STRIDE;
-  int32_t* const nxt = c.wctr + ((c.cset + 1) % 3) * NCTR * CTR_STRIDE;
-  const int32_t* const prv = c.wctr + ((c.cset + 2) % 3) * NCTR * CTR_STRIDE;
-  c.cset = (c.cset + 1) % 3;
-  const int ls = O.set, lp = O.set ^ 1;
-  O.set ^= 1;
-  const Work w{O.wl[ls], O.wst4[ls], O.wang[ls], O.wep[ls], cur, nxt, c.refill,
-               c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
-               O.cap, O.listed[ls], O.listed[lp], O.wl[lp], prv};
-  if (first) {
-    hipLaunchKernelGGL(kc_part<0>(ar, pol), grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w,
-                       h->g0, c.stats, h->err, ks0);
-  } else {
-    // part 1 on the second stream, after the previous step's classification (and k_regen)
-    HIP_TRY(hipStreamWaitEvent(O.aux, O.cls, 0));
-    hipLaunchKernelGGL(kc_part<1>(ar, pol), grid, block, 0, O.aux, S, c.n, h->L, h->grid, io, q,
-                       w, h->g0, c.stats, h->err, nullptr);
+  for (int32_t s = 0; s < steps; ++s) {
+    unsigned long long *ks0 = nullptr, *ks1 = nullptr;
+    timing_begin(h, rc, ks0, ks1);
+    if (rc) return rc;
+    const StepIO io = io_at(s);
+    const Work w = work(s);
+    // step s's classification: whole (the rollout's first step), or its part 2
+    if (s == 0)
+      hipLaunchKernelGGL(kc_part<0>(ar, pol), grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w,
+                         h->g0, c.stats, h->err, ks0);
+    else
+      hipLaunchKernelGGL(kc_part<2>(ar, pol), grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w,
+                         h->g0, c.stats, h->err, ks0);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(O.p1, O.aux));
-    // part 2 after the previous k_run (stream order), then this step's k_run after part 1
-    hipLaunchKernelGGL(kc_part<2>(ar, pol), grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w,
-                       h->g0, c.stats, h->err, ks0);
+    if (s + 1 < steps) {  // step s's k_run with step s + 1's part 1
+      auto kern = ar ? (pol ? k_run_cls<true, 1> : k_run_cls<true, 0>)
+                     : (pol ? k_run_cls<false, 1> : k_run_cls<false, 0>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)(rb + grid_for(c.n))), dim3(RUN_BLOCK), 0, st, S, c.n,
+                         h->L, h->grid, io, q, w, io_at(s + 1), work(s + 1), h->g0, c.stats,
+                         h->err, rb, ks1);
+    } else {
+      auto kr = ar ? k_run<true, false> : k_run<false, false>;
+      hipLaunchKernelGGL(kr, dim3((unsigned)rb), dim3(RUN_BLOCK), 0, st, S, c.n, h->L, h->grid, io,
+                         q, w, h->g0, c.stats, h->err, ks1);
+    }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamWaitEvent(st, O.p1, 0));
+    if (++c.rpend == REGEN_STEPS && (rc = launch_regen(h, c, st))) return rc;
   }
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(O.cls, st));  // the next step's part 1 may start
-  auto kr = ar ? k_run<true, false> : k_run<false, false>;
-  hipLaunchKernelGGL(kr, dim3(run_grid_for(c.n) * (BLOCK / RUN_BLOCK)), dim3(RUN_BLOCK), 0, st, S,
-                     c.n, h->L, h->grid, io, q, w, h->g0, c.stats, h->err, ks1);
-  HIP_TRY(hipGetLastError());
-  if (++c.rpend == REGEN_STEPS) {
-    // k_regen rewrites state words: the next step's part 1 waits for it too
-    if ((rc = launch_regen(h, c, st))) return rc;
-    HIP_TRY(hipEventRecord(O.cls, st));
-  }
+  c.cset = (cs0 + steps) % 3;
+  O.set = (ls0 + steps) & 1;
   return TG_OK;
 }
 
@@ -2404,12 +2478,8 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
     }
     return rc;
   }
-  if (h->grp.empty() && h->mode == TG_MODE_OVERLAP) {
-    int rc = ov_init(h);
-    for (int32_t s = 0; s < steps && !rc; ++s)
-      rc = launch_step_ov(h, io_of(s), ar, cs, tb + (uint32_t)s, s == 0);
-    return rc;
-  }
+  if (h->grp.empty() && h->mode == TG_MODE_OVERLAP)
+    return ov_rollout(h, steps, io_of, ar, policy, cs, tb);
   if (h->grp.empty() || h->mode != TG_MODE_COMPACT) {
     for (int32_t s = 0; s < steps; ++s) {
       const int rc = launch_step(h, h->main, io_of(s), ar, cs, tb + (uint32_t)s);

@@ -140,8 +140,7 @@ struct tg_batch {
   } fl;
   // TG_MODE_OVERLAP's work structures (allocated at the first overlapped rollout): two sets of
   // worklists (step parity; twice the per-segment capacity, as part 1 and part 2 of a step both
-  // append to their workgroups' shards), the per-env listed flags of two steps, the second
-  // stream and its events
+  // append to their workgroups' shards) and the per-env listed flags of two steps
   struct {
     bool ready = false;
     int64_t cap = 0;  // entries per segment
@@ -151,9 +150,6 @@ struct tg_batch {
     int2* wep[2] = {nullptr, nullptr};
     uint8_t* listed[2] = {nullptr, nullptr};
     int set = 0;
-    hipStream_t aux = nullptr;
-    hipEvent_t cls = nullptr;  // (caller's stream) the step's classification is complete
-    hipEvent_t p1 = nullptr;   // (aux stream) part 1 is complete
   } ov;
 };
 

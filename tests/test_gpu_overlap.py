@@ -1,7 +1,7 @@
 """TG_MODE_OVERLAP: tg_rollout with each step's classification split in two — the envs not
-listed in the previous step (k_classify part 1, on a second stream, while the previous k_run
-finishes) and the previous step's listed envs (part 2, one lane per worklist entry, after it)
-— against K x (tg_policy_actions + tg_step), bit for bit (outputs, states, MT streams, episodes,
+listed in the previous step (k_classify part 1, in the previous step's k_run launch: k_run_cls)
+and the previous step's listed envs (part 2, one lane per worklist entry, after it) — against
+K x (tg_policy_actions + tg_step), bit for bit (outputs, states, MT streams, episodes,
 counters).  DESIGN.md §9.3."""
 import pytest
 
