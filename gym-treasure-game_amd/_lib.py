@@ -18,7 +18,6 @@ TG_POLICY_MASKED = 1
 TG_MODE_DIRECT = 0
 TG_MODE_COMPACT = 1
 TG_MODE_FLOW = 2
-TG_MODE_OVERLAP = 3
 TG_ERR_TICKCAP = 1 << 24
 TG_ERR_BAG = 1 << 25
 TG_ERR_ACTION = 1 << 26

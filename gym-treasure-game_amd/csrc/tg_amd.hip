@@ -838,13 +838,6 @@ struct Work {
   int32_t* __restrict__ rcnt;
   int64_t rcap;
   int64_t shard_cap;
-  // TG_MODE_OVERLAP (tg_rollout): per env, listed in this step's worklists (written by every
-  // k_classify part) / in the previous step's (read by part 1); part 2's envs are the previous
-  // step's worklist entries (its lists and counters).  Null in the other modes.
-  uint8_t* __restrict__ lcur;
-  const uint8_t* __restrict__ lprev;
-  const int32_t* __restrict__ plists;
-  const int32_t* __restrict__ pctr;
 };
 // worklist order = the order the chunks' loads reach HBM at the kernel's start (all option
 // waves are resident at once and issue their loads together): the jump waves first, whose
@@ -862,86 +855,27 @@ __constant__ int kSegBase[NLIST] = {kRunPos.of[0] * SHARDS, kRunPos.of[1] * SHAR
 
 // 8 waves per SIMD: its 98-106 SGPRs (the level, the step's pointers) held it to 7; forced, 32-55
 // of them spill to VGPR lanes (no VGPR spills, 60 VGPRs).  A/B r04r: uniform 0.1246 vs 0.1258 ms
-// per step in each of 4 rounds; masked within its spread.
-// PART (TG_MODE_OVERLAP, tg_rollout): 0 every env; 1 the envs NOT listed in the previous step
-// (their state is final once that step's classification is done: run on a second stream while
-// the previous k_run's option chains finish); 2 the previous step's listed envs, one lane per
-// worklist entry, after that k_run
-// k_classify's LDS (a struct, so that k_run_cls can overlay it on k_run's)
-struct ClsShared {
-  int bcnt[NLIST], bbase[NLIST];
-  int rwc[BLOCK / 64], rbase;  // stale halves per wave; the workgroup's list range
+// per step in each of 4 rounds; masked within its spread
+template <bool AUTORESET, bool FINAL, int POL = -1>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_classify(
+    Soa S, int64_t n, Level L, const uint32_t* __restrict__ grid, StepIO io, EpQueue q, Work w,
+    int64_t g0, unsigned long long* __restrict__ stats, uint32_t* __restrict__ err_or,
+    unsigned long long* __restrict__ ks) {
+  const unsigned long long kt0 = kst_begin(ks);
+  __shared__ int bcnt[NLIST], bbase[NLIST];
+  __shared__ int rwc[BLOCK / 64], rbase;  // stale halves per wave; the workgroup's list range
   // the obs staging reuses the level's LDS: nothing reads the grid after the second barrier
   // below (finish_step / reset_env use only L), so 18.4 KB instead of 20.8 KB per workgroup
-  union {
+  __shared__ union {
     LdsLevel lv;
     double ostage[BLOCK * 9];
-  } u;
-  int ppre[NSEG + 1];  // part 2: entries before segment s of the previous step's worklists
-  int pwt[BLOCK / 64];
-};
-template <bool AUTORESET, bool FINAL, int POL, int PART>
-__device__ __forceinline__ void classify_body(ClsShared& sh, const int64_t bid, Soa S, int64_t n,
-                                              Level L, const uint32_t* __restrict__ grid,
-                                              StepIO io, EpQueue q, Work w, int64_t g0,
-                                              unsigned long long* __restrict__ stats,
-                                              uint32_t* __restrict__ err_or,
-                                              unsigned long long* __restrict__ ks) {
-  const unsigned long long kt0 = kst_begin(ks);
-  if (bid == 0)  // the next step's counters (their last reader has finished)
-    for (int c = threadIdx.x; c < NCTR; c += BLOCK) w.ctr_next[c * CTR_STRIDE] = 0;
-  // part 2: this lane's entry of the previous step's worklists (a dense enumeration of their
-  // segments: pre[s] = entries before segment s)
-  int* const ppre = sh.ppre;
-  int* const pwt = sh.pwt;
-  int64_t i = bid * BLOCK + threadIdx.x;
-  if constexpr (PART == 2) {
-    const int s0 = 2 * (int)threadIdx.x, ln = threadIdx.x & 63;
-    const int c0 = s0 < NSEG ? w.pctr[s0 * CTR_STRIDE] : 0;
-    const int c1 = s0 + 1 < NSEG ? w.pctr[(s0 + 1) * CTR_STRIDE] : 0;
-    int v = c0 + c1;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(v, o, 64);
-      if (ln >= o) v += y;
-    }
-    if (ln == 63) pwt[threadIdx.x >> 6] = v;
-    __syncthreads();
-    for (int wv = 0; wv < (int)(threadIdx.x >> 6); ++wv) v += pwt[wv];
-    const int excl = v - c0 - c1;
-    if (s0 < NSEG) ppre[s0] = excl;
-    if (s0 + 1 < NSEG) ppre[s0 + 1] = excl + c0;
-    if (threadIdx.x == BLOCK - 1) ppre[NSEG] = v;
-    __syncthreads();
-    if (bid * BLOCK >= ppre[NSEG]) {  // past the entries (the grid covers n)
-      kst_end(ks, kt0);
-      return;
-    }
-    const int g = (int)i;
-    i = n;  // (no entry: not live)
-    if (g < ppre[NSEG]) {
-      int lo = 0, hi = NSEG;  // ppre[lo] <= g < ppre[hi]
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (ppre[mid] <= g) lo = mid; else hi = mid;
-      }
-      i = w.plists[(int64_t)lo * w.shard_cap + (g - ppre[lo])];
-    }
-  }
-  int* const bcnt = sh.bcnt;
-  int* const bbase = sh.bbase;
-  int* const rwc = sh.rwc;
-  int& rbase = sh.rbase;
-  LdsLevel& lv = sh.u.lv;
-  double* const ostage = sh.u.ostage;
+  } lds;
+  LdsLevel& lv = lds.lv;
+  double* const ostage = lds.ostage;
   double orow[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = i < n;
   const int lane = threadIdx.x & 63;
-  // part 1 leaves the previous step's listed envs to part 2 (loaded with the state below, so
-  // the test costs no round trip of its own)
-  bool live = i < n;
-  uint8_t was_listed = 0;
-  if constexpr (PART == 1)
-    if (live) was_listed = w.lprev[i];
   // every load this lane may need, issued before the level staging and the barriers so their
   // latencies overlap (the angles / episode words only matter if the option cannot run)
   uint4 s4 = make_uint4(0, 0, 0, 0);
@@ -955,8 +889,9 @@ __device__ __forceinline__ void classify_body(ClsShared& sh, const int64_t bid, 
     ep = S.ep[i];
   }
   if (threadIdx.x < NLIST) bcnt[threadIdx.x] = 0;
+  if (blockIdx.x == 0)
+    for (int c = threadIdx.x; c < NCTR; c += BLOCK) w.ctr_next[c * CTR_STRIDE] = 0;
   stage_level(lv, grid, L);  // includes the barrier
-  if constexpr (PART == 1) live = live && !was_listed;
   const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
   int k = -1;
   bool runs = false;
@@ -978,7 +913,6 @@ __device__ __forceinline__ void classify_body(ClsShared& sh, const int64_t bid, 
   // entering done with auto-reset on and no option to run: reset in k_run (L_RESET)
   const bool rst = AUTORESET && live && !runs && is_done(e);
   const int bk = runs ? k : rst ? L_RESET : -1;  // the env's worklist
-  if (w.lcur && live) w.lcur[i] = (uint8_t)(bk >= 0);
   // halves left stale and not listed yet go on this step's refill list (MT_LISTED); k_regen
   // regenerates the lists of several steps at once (a lane that needs a half first does it
   // itself: the ring leaves >= ~2,400 draws of slack, launch_step)
@@ -1013,7 +947,7 @@ __device__ __forceinline__ void classify_body(ClsShared& sh, const int64_t bid, 
   __syncthreads();
   // the workgroup's worklist ranges: issue the global atomics now, use them after the
   // reward-None envs are finished (their latency overlaps that work)
-  const int shard = (int)(bid % SHARDS);
+  const int shard = blockIdx.x % SHARDS;
   int my_base = 0;
   if (threadIdx.x < NLIST) {
     const int c = bcnt[threadIdx.x];
@@ -1038,11 +972,7 @@ __device__ __forceinline__ void classify_body(ClsShared& sh, const int64_t bid, 
     if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
   }
   const int2 ep_in = ep;
-  if constexpr (PART == 2) {  // (scattered envs: each lane its own row)
-    if (fin) store_obs(io.obs, i, orow);
-  } else {
-    store_obs_wave(io.obs, i - lane, __ballot(fin), orow, ostage + (threadIdx.x & ~63) * 9);
-  }
+  store_obs_wave(io.obs, i - lane, __ballot(fin), orow, ostage + (threadIdx.x & ~63) * 9);
   if (fin) {
     const uint4 s4n = pack(e);
     if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w) {  // reset / flag
@@ -1067,17 +997,8 @@ __device__ __forceinline__ void classify_body(ClsShared& sh, const int64_t bid, 
     w.wang[at] = a2;
     w.wep[at] = ep;
   }
-  wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, 0, 0, false, bid);
+  wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, 0);
   kst_end(ks, kt0);
-}
-template <bool AUTORESET, bool FINAL, int POL = -1, int PART = 0>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_classify(
-    Soa S, int64_t n, Level L, const uint32_t* __restrict__ grid, StepIO io, EpQueue q, Work w,
-    int64_t g0, unsigned long long* __restrict__ stats, uint32_t* __restrict__ err_or,
-    unsigned long long* __restrict__ ks) {
-  __shared__ ClsShared sh;
-  classify_body<AUTORESET, FINAL, POL, PART>(sh, blockIdx.x, S, n, L, grid, io, q, w, g0, stats,
-                                             err_or, ks);
 }
 
 #ifdef TG_DIAG_STAMPS
@@ -1092,32 +1013,20 @@ __device__ unsigned long long g_stamps[NSTAMP_WAVES * NSTAMP];
 #define TG_STAMP(v) (void)0
 #endif
 
-// k_run's LDS: the worklists' prefix, the waves' code windows (WIN_WAVE_BYTES each, at offset
-// 0: 16-B aligned for the LDS-DMA), then the level's grid words and bitmasks (Map::mk).  (Sized
-// at launch for the handle's level instead of the largest, with the rows' loads issued before
-// the staging barrier, it measured ~4 % slower for the masked policy: DESIGN.md §3.1.)
-struct RunShared {
-  uint4 lds[((RUN_BLOCK / 64) * WIN_WAVE_BYTES + MAX_CELLS + 4 * MK_MAX_WORDS) / 16];
-  uint32_t ltrig[12];
-  int pre[NSEG + 1];
-  int wtot[RUN_BLOCK / 64];
-  int ostart[NLIST + 1], oraw[NLIST + 1];
-};
 template <bool AUTORESET, bool FINAL>
-__device__ __forceinline__ void run_body(RunShared& sh, const int64_t bid, Soa S, int64_t n,
-                                         Level L, const uint32_t* __restrict__ grid, StepIO io,
-                                         EpQueue q, Work w, int64_t g0,
-                                         unsigned long long* __restrict__ stats,
-                                         uint32_t* __restrict__ err_or,
-                                         unsigned long long* __restrict__ ks) {
+__global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
+                                                const uint32_t* __restrict__ grid, StepIO io,
+                                                EpQueue q, Work w, int64_t g0,
+                                                unsigned long long* __restrict__ stats,
+                                                uint32_t* __restrict__ err_or,
+                                                unsigned long long* __restrict__ ks) {
   const unsigned long long kt0 = kst_begin(ks);
   // the worklists in run order: pre[s] = envs listed before segment s (exclusive prefix of the
   // counters, two segments per thread), then per option (run order j) its first segment's
   // prefix and its start in the chunk space, where each option is padded to whole chunks
-  int* const pre = sh.pre;
-  int* const wtot = sh.wtot;
-  int* const ostart = sh.ostart;
-  int* const oraw = sh.oraw;
+  __shared__ int pre[NSEG + 1];
+  __shared__ int wtot[RUN_BLOCK / 64];
+  __shared__ int ostart[NLIST + 1], oraw[NLIST + 1];
   {
     const int s0 = 2 * (int)threadIdx.x, ln = threadIdx.x & 63;
     const int c0 = s0 < NSEG ? w.ctr[s0 * CTR_STRIDE] : 0;
@@ -1139,7 +1048,7 @@ __device__ __forceinline__ void run_body(RunShared& sh, const int64_t bid, Soa S
   __syncthreads();
   // a workgroup past every listed chunk (the grid covers n envs, a uniform step lists ~1 in 5;
   // the options' padding adds < 64 each) leaves before it stages the level: ~3/4 of the grid
-  if ((int)(bid * RUN_BLOCK) >= pre[NSEG] + NLIST * 63) {
+  if ((int)(blockIdx.x * RUN_BLOCK) >= pre[NSEG] + NLIST * 63) {
     kst_end(ks, kt0);
     return;
   }
@@ -1154,14 +1063,9 @@ __device__ __forceinline__ void run_body(RunShared& sh, const int64_t bid, Soa S
     ostart[NLIST] = acc;
     oraw[NLIST] = pre[NSEG];
   }
-  uint8_t* const win = reinterpret_cast<uint8_t*>(sh.lds);
-  uint32_t* const lgrid = reinterpret_cast<uint32_t*>(win + (RUN_BLOCK / 64) * WIN_WAVE_BYTES);
-  uint32_t* const lmk = lgrid + grid_words(L.W, L.H);
-  stage_cells<RUN_BLOCK>(lgrid, sh.ltrig, grid, L, lmk);  // includes the barrier (ostart / oraw)
-  const uint32_t* const trig = sh.ltrig;
-  const Map m{reinterpret_cast<const uint8_t*>(lgrid), L.W, L.H, L.masks ? lmk : nullptr};
+  RUN_LEVEL_IN_LDS();  // includes the barrier (ostart / oraw)
   const int total = ostart[NLIST];
-  const int base = (int)(bid * RUN_BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
+  const int base = (blockIdx.x * RUN_BLOCK + threadIdx.x) & ~63;  // wave w runs chunk w
   int oj = 0;  // ostart[oj] <= base < ostart[oj + 1] (wave-uniform)
   while (oj + 1 < NLIST && ostart[oj + 1] <= base) ++oj;
   oj = __builtin_amdgcn_readfirstlane(oj);
@@ -1221,7 +1125,7 @@ __device__ __forceinline__ void run_body(RunShared& sh, const int64_t bid, Soa S
   }
   // (k_run's grid has BLOCK / RUN_BLOCK workgroups per stats slot, as wave_stats below)
   if (AUTORESET)
-    record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats, bid / (BLOCK / RUN_BLOCK));
+    record_episodes(live && r.done, g0 + i, ep, io.tstep, q, stats, (int64_t)blockIdx.x / (BLOCK / RUN_BLOCK));
   if (live) {
     S.st4[i] = pack(e);
     S.ang[i] = make_double2(e.ang0, e.ang1);
@@ -1230,7 +1134,7 @@ __device__ __forceinline__ void run_body(RunShared& sh, const int64_t bid, Soa S
   __builtin_amdgcn_s_setprio(0);
   wave_stats(stats, 0, 0, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
              regens + (__ballot(lregen != 0) ? wave_sum(lregen) : 0), true,
-             bid / (BLOCK / RUN_BLOCK));
+             (int64_t)blockIdx.x / (BLOCK / RUN_BLOCK));
   kst_end(ks, kt0);
 #ifdef TG_DIAG_STAMPS
   TG_STAMP(t3);
@@ -1242,7 +1146,7 @@ __device__ __forceinline__ void run_body(RunShared& sh, const int64_t bid, Soa S
     const int src = bl ? __ffsll((long long)bl) - 1 : 0;
     const unsigned long long a1 = __shfl(t1, src, 64);
     const unsigned long long a2 = __shfl(t2, src, 64);
-    const int wv = (int)(bid * RUN_BLOCK + threadIdx.x) >> 6;
+    const int wv = (blockIdx.x * RUN_BLOCK + threadIdx.x) >> 6;
     const unsigned long long rt3 = __builtin_amdgcn_s_memrealtime();
     // the phases of the lane whose option loop ran longest (the wave's own time)
     int lmax = src;
@@ -1272,39 +1176,6 @@ __device__ __forceinline__ void run_body(RunShared& sh, const int64_t bid, Soa S
     }
   }
 #endif
-}
-template <bool AUTORESET, bool FINAL>
-__global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
-                                                const uint32_t* __restrict__ grid, StepIO io,
-                                                EpQueue q, Work w, int64_t g0,
-                                                unsigned long long* __restrict__ stats,
-                                                uint32_t* __restrict__ err_or,
-                                                unsigned long long* __restrict__ ks) {
-  __shared__ RunShared sh;
-  run_body<AUTORESET, FINAL>(sh, blockIdx.x, S, n, L, grid, io, q, w, g0, stats, err_or, ks);
-}
-// TG_MODE_OVERLAP (tg_rollout): step t's k_run and step t + 1's k_classify part 1 (the envs not
-// listed in step t, whose state step t's k_run does not touch) in one launch.  Its first rb
-// workgroups are k_run's (most of them leave at once: a uniform step lists ~1 env in 5), the
-// rest part 1's, dispatched behind them, so part 1's waves fill the CUs while the option waves'
-// long chains run.  The two parts share the workgroup's LDS.
-template <bool AUTORESET, int POL>
-__global__ __launch_bounds__(RUN_BLOCK) void k_run_cls(Soa S, int64_t n, Level L,
-                                                    const uint32_t* __restrict__ grid, StepIO io,
-                                                    EpQueue q, Work w, StepIO io1, Work w1,
-                                                    int64_t g0, unsigned long long* __restrict__ stats,
-                                                    uint32_t* __restrict__ err_or, int64_t rb,
-                                                    unsigned long long* __restrict__ ks) {
-  static_assert(RUN_BLOCK == BLOCK, "one workgroup shape for both parts");
-  __shared__ union {
-    RunShared r;
-    ClsShared c;
-  } sh;
-  if ((int64_t)blockIdx.x < rb)
-    run_body<AUTORESET, false>(sh.r, blockIdx.x, S, n, L, grid, io, q, w, g0, stats, err_or, ks);
-  else
-    classify_body<AUTORESET, false, POL, 1>(sh.c, (int64_t)blockIdx.x - rb, S, n, L, grid, io1, q,
-                                            w1, g0, stats, err_or, nullptr);
 }
 
 // ---- deferred regeneration of the listed stale MT halves (k_regen) ----------------------------
@@ -1743,14 +1614,14 @@ int alloc_ctx(StepCtx& c, int64_t off, int64_t n) {
   ALLOC_C(c.wst4, sizeof(uint4) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wang, sizeof(double2) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wep, sizeof(int2) * NSEG * (size_t)c.shard_cap);
-  ALLOC_C(c.wctr, sizeof(int32_t) * 3 * NCTR * CTR_STRIDE);
+  ALLOC_C(c.wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
   // a shard's list holds at most its workgroups' envs per pending step
   c.rcap = c.shard_cap * REGEN_STEPS;
   ALLOC_C(c.refill, sizeof(uint32_t) * SHARDS * (size_t)c.rcap);
   ALLOC_C(c.regen_ctr, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE);
 #undef ALLOC_C
   HIP_TRY(hipMemset(c.stats, 0, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n)));
-  HIP_TRY(hipMemset(c.wctr, 0, sizeof(int32_t) * 3 * NCTR * CTR_STRIDE));
+  HIP_TRY(hipMemset(c.wctr, 0, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE));
   HIP_TRY(hipMemset(c.regen_ctr, 0, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE));
   return TG_OK;
 }
@@ -1766,7 +1637,6 @@ void free_ctx(StepCtx& c) {
 
 namespace {
 void flow_free(tg_batch* h);  // TG_MODE_FLOW's buffers (below)
-void ov_free(tg_batch* h);    // TG_MODE_OVERLAP's (below)
 }
 
 extern "C" {
@@ -1875,7 +1745,6 @@ void tg_destroy(tg_batch* h) {
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   render_free(h->rs);
   flow_free(h);
-  ov_free(h);
   void* bufs[] = {h->grid, h->genrand, h->gotab, h->masks, h->obs_q, h->S.st4, h->S.ang, h->S.ep,
                   h->S.mt, h->S.mc, h->eps, h->eps_count, h->err, h->obs_scratch, h->kst};
   for (void* b : bufs)
@@ -1981,16 +1850,16 @@ int launch_step(tg_batch* h, StepCtx& c, const StepIO& io_in, bool ar, hipStream
     hipLaunchKernelGGL(kern, grid, block, 0, st, S, c.n, h->L, h->grid, io, q, g0, c.stats, h->err,
                        ks1);
   } else {
-    // counters in three sets by step: k_classify zeroes the next step's set (the k_run two
-    // steps back, which read it, has finished), so no memset launch per step
-    int32_t* const cur = c.wctr + c.cset * NCTR * CTR_STRIDE;
-    int32_t* const nxt = c.wctr + ((c.cset + 1) % 3) * NCTR * CTR_STRIDE;
-    c.cset = (c.cset + 1) % 3;
+    // counters double-buffered by step parity: k_classify zeroes the next step's set (the
+    // previous k_run, which read it, has finished), so no memset launch per step
+    int32_t* const cur = c.wctr + (c.parity ? NCTR * CTR_STRIDE : 0);
+    int32_t* const nxt = c.wctr + (c.parity ? 0 : NCTR * CTR_STRIDE);
+    c.parity ^= 1;
     // the refill lists append until k_regen drains them (every REGEN_STEPS steps), counted in
     // the set the next k_regen reads
     const Work w{c.wl,     c.wst4, c.wang, c.wep, cur, nxt, c.refill,
                  c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
-                 c.shard_cap, nullptr, nullptr, nullptr, nullptr};
+                 c.shard_cap};
     decltype(&k_classify<true, true>) kc;
     if (io.policy == TG_POLICY_UNIFORM)
       kc = ar ? (fo ? k_classify<true, true, 0> : k_classify<true, false, 0>)
@@ -2022,114 +1891,6 @@ int regen_all(tg_batch* h, hipStream_t st) {
   for (auto& c : h->grp)
     if (!rc) rc = launch_regen(h, c, st);
   return rc;
-}
-
-// ---- TG_MODE_OVERLAP (tg_rollout) -------------------------------------------------------------
-// A step's envs that were not listed in the previous step (its option could not run: reward
-// None, state unchanged) are final once the previous step's classification is done, so their
-// classification for step t + 1 (k_classify part 1) runs in step t's k_run launch (k_run_cls:
-// its workgroups behind k_run's), filling the CUs while the option chains finish.  The step-t
-// listed envs are classified after it (part 2, one lane per worklist entry), then k_run_cls of
-// step t + 1.  Only inside tg_rollout, whose steps write distinct [K][N] output rows: with
-// tg_step's shared rows, part 1 of step t + 1 would overwrite rows of step t the caller may still
-// be reading.  (A first form ran part 1 as its own kernel on a second stream, waiting on events:
-// slower than the plain rollout, 0.128-0.132 vs 0.104-0.107 ms per uniform step, r05k.)
-void ov_free(tg_batch* h) {
-  auto& O = h->ov;
-  for (int k = 0; k < 2; ++k) {
-    void* bufs[] = {O.wl[k], O.wst4[k], O.wang[k], O.wep[k], O.listed[k]};
-    for (void* b : bufs)
-      if (b) (void)hipFree(b);
-  }
-  O = {};
-}
-int ov_init(tg_batch* h) {
-  auto& O = h->ov;
-  if (O.ready) return TG_OK;
-  const StepCtx& c = h->main;
-  O.cap = 2 * c.shard_cap;
-  const size_t ent = (size_t)NSEG * (size_t)O.cap;
-  bool ok = true;
-  for (int k = 0; k < 2 && ok; ++k)
-    ok = hipMalloc((void**)&O.wl[k], sizeof(int32_t) * ent) == hipSuccess &&
-         hipMalloc((void**)&O.wst4[k], sizeof(uint4) * ent) == hipSuccess &&
-         hipMalloc((void**)&O.wang[k], sizeof(double2) * ent) == hipSuccess &&
-         hipMalloc((void**)&O.wep[k], sizeof(int2) * ent) == hipSuccess &&
-         hipMalloc((void**)&O.listed[k], (size_t)h->n) == hipSuccess;
-  if (!ok) {
-    ov_free(h);
-    return fail(TG_E_NOMEM, "overlap mode: worklists (%zu MB)", ent * 44 * 2 >> 20);
-  }
-  O.ready = true;
-  return TG_OK;
-}
-template <int PART>
-using KcPtr = decltype(&k_classify<true, false, 0, PART>);
-template <int PART>
-KcPtr<PART> kc_part(bool ar, int pol) {
-  return ar ? (pol ? k_classify<true, false, 1, PART> : k_classify<true, false, 0, PART>)
-            : (pol ? k_classify<false, false, 1, PART> : k_classify<false, false, 0, PART>);
-}
-// K steps of tg_rollout in the overlap form (io_of(s): step s's rows)
-template <class IoOf>
-int ov_rollout(tg_batch* h, int32_t steps, IoOf io_of, bool ar, int policy, hipStream_t st,
-               uint32_t tb) {
-  int rc = ov_init(h);
-  if (rc) return rc;
-  auto& O = h->ov;
-  StepCtx& c = h->main;
-  const int pol = policy == TG_POLICY_MASKED ? 1 : 0;
-  const int cs0 = c.cset, ls0 = O.set;
-  // step s's worklists (set parity), counters (three sets), listed flags; the previous step's
-  // (part 2's envs); the refill lists' counter of the set the next k_regen drains
-  auto work = [&](int32_t s) {
-    const int ls = (ls0 + s) & 1, lp = ls ^ 1;
-    return Work{O.wl[ls], O.wst4[ls], O.wang[ls], O.wep[ls],
-                c.wctr + ((cs0 + s) % 3) * NCTR * CTR_STRIDE,
-                c.wctr + ((cs0 + s + 1) % 3) * NCTR * CTR_STRIDE, c.refill,
-                c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap, O.cap,
-                O.listed[ls], O.listed[lp], O.wl[lp], c.wctr + ((cs0 + s + 2) % 3) * NCTR * CTR_STRIDE};
-  };
-  auto io_at = [&](int32_t s) {
-    StepIO io = io_of(s);
-    io.tstep = tb + (uint32_t)s;
-    return io;
-  };
-  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
-  const dim3 grid(grid_for(c.n)), block(BLOCK);
-  const int64_t rb = (int64_t)run_grid_for(c.n) * (BLOCK / RUN_BLOCK);
-  const Soa S = soa_of(h, c);
-  for (int32_t s = 0; s < steps; ++s) {
-    unsigned long long *ks0 = nullptr, *ks1 = nullptr;
-    timing_begin(h, rc, ks0, ks1);
-    if (rc) return rc;
-    const StepIO io = io_at(s);
-    const Work w = work(s);
-    // step s's classification: whole (the rollout's first step), or its part 2
-    if (s == 0)
-      hipLaunchKernelGGL(kc_part<0>(ar, pol), grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w,
-                         h->g0, c.stats, h->err, ks0);
-    else
-      hipLaunchKernelGGL(kc_part<2>(ar, pol), grid, block, 0, st, S, c.n, h->L, h->grid, io, q, w,
-                         h->g0, c.stats, h->err, ks0);
-    HIP_TRY(hipGetLastError());
-    if (s + 1 < steps) {  // step s's k_run with step s + 1's part 1
-      auto kern = ar ? (pol ? k_run_cls<true, 1> : k_run_cls<true, 0>)
-                     : (pol ? k_run_cls<false, 1> : k_run_cls<false, 0>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)(rb + grid_for(c.n))), dim3(RUN_BLOCK), 0, st, S, c.n,
-                         h->L, h->grid, io, q, w, io_at(s + 1), work(s + 1), h->g0, c.stats,
-                         h->err, rb, ks1);
-    } else {
-      auto kr = ar ? k_run<true, false> : k_run<false, false>;
-      hipLaunchKernelGGL(kr, dim3((unsigned)rb), dim3(RUN_BLOCK), 0, st, S, c.n, h->L, h->grid, io,
-                         q, w, h->g0, c.stats, h->err, ks1);
-    }
-    HIP_TRY(hipGetLastError());
-    if (++c.rpend == REGEN_STEPS && (rc = launch_regen(h, c, st))) return rc;
-  }
-  c.cset = (cs0 + steps) % 3;
-  O.set = (ls0 + steps) & 1;
-  return TG_OK;
 }
 
 // ---- TG_MODE_FLOW (tg_flow.h) ----------------------------------------------------------------
@@ -2478,8 +2239,6 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
     }
     return rc;
   }
-  if (h->grp.empty() && h->mode == TG_MODE_OVERLAP)
-    return ov_rollout(h, steps, io_of, ar, policy, cs, tb);
   if (h->grp.empty() || h->mode != TG_MODE_COMPACT) {
     for (int32_t s = 0; s < steps; ++s) {
       const int rc = launch_step(h, h->main, io_of(s), ar, cs, tb + (uint32_t)s);
@@ -2608,8 +2367,7 @@ int tg_errors(tg_batch* h, uint32_t* out, void* stream) {
 
 int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
   BIND(h);
-  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT && mode != TG_MODE_FLOW &&
-      mode != TG_MODE_OVERLAP)
+  if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT && mode != TG_MODE_FLOW)
     return fail(TG_E_INVAL, "tg_set_mode: unknown mode %d", mode);
   h->mode = mode;
   (void)run_blocks;  // reserved

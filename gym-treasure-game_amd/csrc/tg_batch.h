@@ -58,12 +58,11 @@ struct StepCtx {
   uint4* wst4 = nullptr;   // the listed envs' state in worklist order (k_classify -> k_run)
   double2* wang = nullptr;
   int2* wep = nullptr;
-  int32_t* wctr = nullptr; // sharded counters, three sets (step % 3: TG_MODE_OVERLAP's part 1
-                           // of step t + 1 fills its set while k_run of step t reads its own)
+  int32_t* wctr = nullptr; // sharded counters, two sets (step parity)
   uint32_t* refill = nullptr;  // stale MT halves listed by k_classify: SHARDS lists (k_regen)
   int64_t rcap = 0;            // entries per list: a shard's envs x REGEN_STEPS
   int64_t shard_cap = 0;
-  int cset = 0;    // which set of wctr this compact step counts in
+  int parity = 0;  // which half of wctr this compact step counts in
   int rpend = 0;   // compact steps whose refill lists k_regen has not drained
   int32_t* regen_ctr = nullptr;  // per XCD: k_regen's grab counters and the lists' lengths, two
                                  // sets (k_regen zeroes the other set for the next launch)
@@ -138,19 +137,6 @@ struct tg_batch {
     int bpc[2][2] = {{0, 0}, {0, 0}};  // k_flow<AR, POL> workgroups per CU (occupancy API)
     int64_t launches = 0;
   } fl;
-  // TG_MODE_OVERLAP's work structures (allocated at the first overlapped rollout): two sets of
-  // worklists (step parity; twice the per-segment capacity, as part 1 and part 2 of a step both
-  // append to their workgroups' shards) and the per-env listed flags of two steps
-  struct {
-    bool ready = false;
-    int64_t cap = 0;  // entries per segment
-    int32_t* wl[2] = {nullptr, nullptr};
-    uint4* wst4[2] = {nullptr, nullptr};
-    double2* wang[2] = {nullptr, nullptr};
-    int2* wep[2] = {nullptr, nullptr};
-    uint8_t* listed[2] = {nullptr, nullptr};
-    int set = 0;
-  } ov;
 };
 
 namespace tg {

@@ -304,7 +304,7 @@ class TreasureGameVec:
         runs in place) or "flow" (as compact per step; rollout() runs up to 16 steps per launch,
         chunks advancing without a batch-wide barrier between steps); all bit-identical."""
         m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT,
-             "flow": _lib.TG_MODE_FLOW, "overlap": _lib.TG_MODE_OVERLAP}[mode]
+             "flow": _lib.TG_MODE_FLOW}[mode]
         check(self._L.tg_set_mode(self.handle, m, int(run_blocks)), "tg_set_mode")
 
     def set_episode_capacity(self, cap):

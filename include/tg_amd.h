@@ -208,10 +208,6 @@ int tg_errors(tg_batch *h, uint32_t *or_of_flags, void *stream);
  *     done with step t (no batch-wide barrier between steps).  Results are
  *     identical to the other modes. */
 #define TG_MODE_FLOW 2
-/*   TG_MODE_OVERLAP: as TG_MODE_COMPACT for tg_step; in tg_rollout the envs not listed in step t
- *     (their option could not run) are classified for step t + 1 on a second stream while step
- *     t's k_run finishes, the listed ones after it.  Identical results. */
-#define TG_MODE_OVERLAP 3
 /*   (Round 2's TG_MODE_ASYNC, all K steps of tg_rollout in one persistent launch, was exact
  *     but slower, 0.214 vs 0.142 ms per step, and was removed in round 3: DESIGN.md §9.1.) */
 int tg_set_mode(tg_batch *h, int mode, int run_blocks);
