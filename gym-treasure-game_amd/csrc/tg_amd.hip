@@ -1897,9 +1897,6 @@ int regen_all(tg_batch* h, hipStream_t st) {
 void flow_free(tg_batch* h) {
   auto& F = h->fl;
   void* bufs[] = {F.ctl[0], F.ctl[1], F.q[0], F.q[1], F.fill[0], F.fill[1], F.list, F.outst};
-  if (F.fork) (void)hipEventDestroy(F.fork);
-  if (F.join) (void)hipEventDestroy(F.join);
-  if (F.aux) (void)hipStreamDestroy(F.aux);
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   F = {};
@@ -1933,7 +1930,6 @@ int flow_init(tg_batch* h) {
   F.lcap = cxm * 64;
   F.jcap = cxm + 1;
   F.qcap = (int64_t)FLOW_MAX_K * (2 * cxm + NLIST);  // run items + chunks to classify, per step
-  F.qrun = (int64_t)FLOW_MAX_K * (cxm + NLIST);      // (split launches: the run items' part)
   const size_t nctl = (size_t)F.P * CTL_WORDS, nq = (size_t)F.P * F.qcap,
                nfill = (size_t)F.P * FLOW_MAX_K * NLIST * F.jcap,
                nlist = (size_t)F.P * FLOW_MAX_K * NLIST * F.lcap;
@@ -1986,7 +1982,7 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   F.parity ^= 1;
   Flow f{F.ctl[p], F.q[p], F.fill[p], F.list, F.outst, F.ctl[p ^ 1], F.q[p ^ 1], F.fill[p ^ 1],
          c.refill, c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
-         F.qcap, F.jcap, F.lcap, F.qrun, F.C, F.P, k, F.xmap, nullptr, nullptr, nullptr};
+         F.qcap, F.jcap, F.lcap, F.C, F.P, k, F.xmap, nullptr, nullptr, nullptr};
 #ifdef TG_FLOW_DBG
   static uint32_t* dbg_host = nullptr;
   static uint32_t* dbg_dev = nullptr;
@@ -2023,35 +2019,8 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   if (getenv("TG_FLOW_DEBUG"))
     fprintf(stderr, "[flow] launching k %d grid %d x %d lcap %lld qcap %lld jcap %lld C %d\n", k, h->cus, bpc,
             (long long)F.lcap, (long long)F.qcap, (long long)F.jcap, F.C);
-  if (getenv("TG_FLOW_SPLIT")) {
-    // (A/B) two kernels side by side: the classifying waves (ROLE 1) on the caller's stream, the
-    // running waves (ROLE 2) on a second one, forked and joined with events; per CU rb + cb
-    // workgroups, sized to fit together (a kernel whose waves are not resident only leaves the
-    // other's waits to their bound)
-    if (!F.aux) {
-      HIP_TRY(hipStreamCreateWithFlags(&F.aux, hipStreamNonBlocking));
-      HIP_TRY(hipEventCreateWithFlags(&F.fork, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&F.join, hipEventDisableTiming));
-    }
-    auto kc = ar ? (pol ? k_flow<true, 1, 1> : k_flow<true, 0, 1>) : (pol ? k_flow<false, 1, 1> : k_flow<false, 0, 1>);
-    auto kr = ar ? (pol ? k_flow<true, 1, 2> : k_flow<true, 0, 2>) : (pol ? k_flow<false, 1, 2> : k_flow<false, 0, 2>);
-    const char* erb = getenv("TG_FLOW_RB");
-    const char* ecb = getenv("TG_FLOW_CB");
-    const int rb = erb ? atoi(erb) : 3, cb = ecb ? atoi(ecb) : 3;
-    HIP_TRY(hipEventRecord(F.fork, st));
-    HIP_TRY(hipStreamWaitEvent(F.aux, F.fork, 0));
-    hipLaunchKernelGGL(kr, dim3((unsigned)(h->cus * rb)), dim3(BLOCK), 0, F.aux, h->S, h->n, h->L,
-                       h->grid, io, q, f, h->g0, c.stats, stat_slots(h->n), h->err, nullptr);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(kc, dim3((unsigned)(h->cus * cb)), dim3(BLOCK), 0, st, h->S, h->n, h->L,
-                       h->grid, io, q, f, h->g0, c.stats, stat_slots(h->n), h->err, ks);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(F.join, F.aux));
-    HIP_TRY(hipStreamWaitEvent(st, F.join, 0));
-  } else {
-    hipLaunchKernelGGL(kern, dim3((unsigned)(h->cus * bpc)), dim3(BLOCK), 0, st, h->S, h->n, h->L,
-                       h->grid, io, q, f, h->g0, c.stats, stat_slots(h->n), h->err, ks);
-  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(h->cus * bpc)), dim3(BLOCK), 0, st, h->S, h->n, h->L,
+                     h->grid, io, q, f, h->g0, c.stats, stat_slots(h->n), h->err, ks);
   HIP_TRY(hipGetLastError());
   ++F.launches;
 #ifdef TG_FLOW_DBG

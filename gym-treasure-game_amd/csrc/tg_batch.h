@@ -127,9 +127,7 @@ struct tg_batch {
     int P = 0;                // sub-problems: the XCDs the census saw
     uint32_t xmap = 0;        // XCC id -> sub-problem (nibbles)
     int32_t C = 0;            // 64-env chunks
-    int64_t qcap = 0, jcap = 0, lcap = 0, qrun = 0;
-    hipStream_t aux = nullptr;    // (TG_FLOW_SPLIT) the running kernel's stream
-    hipEvent_t fork = nullptr, join = nullptr;
+    int64_t qcap = 0, jcap = 0, lcap = 0;
     int32_t* ctl[2] = {nullptr, nullptr};  // two parities: a launch zeroes the other's
     uint32_t* q[2] = {nullptr, nullptr};
     int32_t* fill[2] = {nullptr, nullptr};

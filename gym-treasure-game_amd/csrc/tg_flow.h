@@ -54,8 +54,6 @@ enum : int {
   FC_QTAIL,     //   slots pushed
   FC_FIN,       // chunks done with step K - 1
   FC_DONE,      // set when FC_FIN reaches the sub-problem's chunks (or on a deadline)
-  FC_CQHEAD,    // (split launches) classification queue: tickets taken
-  FC_CQTAIL,    //   slots pushed
   FC_CLS,       // + t: chunks classified for step t
   FC_LTAIL = FC_CLS + FLOW_MAX_K,  // + t * NLIST + k: entries reserved in list (t, k)
   FC_N = FC_LTAIL + FLOW_MAX_K * NLIST
@@ -82,7 +80,6 @@ struct Flow {
   uint32_t* refill;  // k_regen's lists (list c % SHARDS, as k_classify's shards)
   int32_t* rcnt;
   int64_t rcap, qcap, jcap, lcap;
-  int64_t qrun;      // (split launches) slots of the run queue; the classification queue after them
   int32_t C, P, K;   // chunks, sub-problems, steps
   uint32_t xmap;     // nibble x: the sub-problem of XCC id x (0xF: none)
   uint32_t* dbg;     // TG_FLOW_DBG builds: per-wave progress in mapped host memory (else null)
@@ -223,11 +220,7 @@ __global__ void k_census(uint32_t* mask) {
 #else
 #define FLOW_WAVES
 #endif
-// ROLE 0: one kernel does both kinds of work.  Split launches (TG_FLOW_SPLIT): ROLE 1 waves only
-// classify (the step-0 deal, completed chunks from the classification queue) and ROLE 2 waves
-// only run items, as two kernels resident side by side, each with its own registers
-// (classification needs ~60 VGPRs, the option loops ~92; one kernel doing both held 123-182)
-template <bool AR, int POL, int ROLE = 0>
+template <bool AR, int POL>
 __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Level L,
                                                 const uint32_t* __restrict__ grid, FlowIO io,
                                                 EpQueue eq, Flow f, int64_t g0,
@@ -297,13 +290,6 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     FLOW_EV(4, ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j, at, src, x);
     if ((int64_t)at < f.qcap) st_sc1(q + at, ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j);
     else atomicOr(err_or, E_FLOW);  // (capacity is the bound of the pushes: unreachable)
-  };
-  // (ROLE 2) a completed chunk on the classification queue
-  auto push_cls = [&](int t, int c) {
-    const int at = atomicAdd(fcw(ctl, FC_CQTAIL), 1);
-    if ((int64_t)at < f.qcap - f.qrun)
-      st_sc1(q + f.qrun + at, ((uint32_t)t << 28) | ((uint32_t)Q_CLASSIFY << 24) | (uint32_t)c);
-    else atomicOr(err_or, E_FLOW);
   };
   auto step_io = [&](int t) {
     return StepIO{nullptr, io.obs + (int64_t)t * io.obs_stride, io.reward + (int64_t)t * n,
@@ -529,7 +515,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       c = cc;
       t = ct;
       cc = -1;
-    } else if (ROLE != 2 && phase0) {
+    } else if (phase0) {
       int j = 0;
       if (lane == 0) j = atomicAdd(fcw(ctl, FC_INIT), 1);
       j = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(j, 0));
@@ -541,11 +527,8 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       t = 0;
     } else {
       // an item by ticket: wait for its slot (lane 0 polls, the wave reads its answer)
-      // (ROLE 1 waits on the classification queue, after the run queue's slots)
-      const int qhead = ROLE == 1 ? FC_CQHEAD : FC_QHEAD;
-      const int64_t qb = ROLE == 1 ? f.qrun : 0, qn = ROLE == 1 ? f.qcap - f.qrun : (ROLE == 2 ? f.qrun : f.qcap);
       int h = 0;
-      if (lane == 0) h = atomicAdd(fcw(ctl, qhead), 1);
+      if (lane == 0) h = atomicAdd(fcw(ctl, FC_QHEAD), 1);
       h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(h, 0));
       FLOW_DBG(2, h, x, 0);
       if (lane == 0) FLOW_EV(8, h, x, 0, 0);
@@ -555,7 +538,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
         uint32_t it = Q_EMPTY;
         int dn = 0;
         if (lane == 0) {
-          if ((int64_t)h < qn) it = ld_sc1(q + qb + h);
+          if ((int64_t)h < f.qcap) it = ld_sc1(q + h);
           if (it == Q_EMPTY) dn = ld_sc1(fcw(ctl, FC_DONE));
         }
         item = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(it, 0));
@@ -588,9 +571,9 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
       }
 #endif
       t = (int)(item >> 28);
-      if (ROLE != 2 && ((item >> 24) & 15u) == Q_CLASSIFY) {  // a chunk another wave's run item completed
+      if (((item >> 24) & 15u) == Q_CLASSIFY) {  // a chunk another wave's run item completed
         c = (int)(item & 0xFFFFFFu);
-      } else if constexpr (ROLE != 1) {
+      } else {
         const unsigned long long rd = run(item, cl);
         // (readfirstlane returns int: each half is cast back to 32 bits before it widens, or
         // lane 31's bit sign-extends over lanes 32-63)
@@ -608,22 +591,12 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
           }
           continue;
         }
-        if constexpr (ROLE == 2) {  // every completed chunk to the classifying kernel
-          if ((ready >> lane) & 1ull) push_cls(t, cl);
-          continue;
-        } else {
-          // the first completed chunk is classified here, the others by whichever waves take them
-          const int l0 = __ffsll((long long)ready) - 1;
-          c = __builtin_amdgcn_readlane(cl, l0);
-          if (((ready >> lane) & 1ull) && lane != l0) push(t, Q_CLASSIFY, cl, 3);
-        }
-      } else {
-        continue;  // (ROLE 1 takes only classification items)
+        // the first completed chunk is classified here, the others by whichever waves take them
+        const int l0 = __ffsll((long long)ready) - 1;
+        c = __builtin_amdgcn_readlane(cl, l0);
+        if (((ready >> lane) & 1ull) && lane != l0) push(t, Q_CLASSIFY, cl, 3);
       }
     }
-    if constexpr (ROLE == 2) {
-      continue;  // (unreachable: ROLE 2 classifies nothing)
-    } else {
     // chunk c at step t: classified, or, past the last step, finished
     if (t >= K) {
       if (lane == 0 && atomicAdd(fcw(ctl, FC_FIN), 1) + 1 == Cx)
@@ -649,7 +622,6 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
     if (cnt == 0) {  // no env of the chunk runs an option: its next step at once
       cc = c;
       ct = t + 1;
-    }
     }
   }
   FLOW_DBG(9, 0, 0, 0);
