@@ -210,18 +210,8 @@ __global__ void k_census(uint32_t* mask) {
   if (threadIdx.x == 0) atomicOr(mask, 1u << (xcc_id() & 31u));
 }
 
-#ifdef TG_FLOW_NOINL
-#define FLOW_NOINL __attribute__((noinline))
-#else
-#define FLOW_NOINL
-#endif
-#ifdef TG_FLOW_W
-#define FLOW_WAVES __attribute__((amdgpu_waves_per_eu(TG_FLOW_W, TG_FLOW_W)))
-#else
-#define FLOW_WAVES
-#endif
 template <bool AR, int POL>
-__global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Level L,
+__global__ __launch_bounds__(BLOCK) void k_flow(Soa S, int64_t n, Level L,
                                                 const uint32_t* __restrict__ grid, FlowIO io,
                                                 EpQueue eq, Flow f, int64_t g0,
                                                 unsigned long long* __restrict__ stats, int nstat,
@@ -298,7 +288,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
   };
 
   // classify chunk c for step t (k_classify's per-env work); returns the envs it listed
-  auto classify = [&](int c, int t) FLOW_NOINL -> int {
+  auto classify = [&](int c, int t) -> int {
     const int64_t i = (int64_t)c * 64 + lane;
     const bool live = i < n;
     const StepIO st = step_io(t);
@@ -415,7 +405,7 @@ __global__ __launch_bounds__(BLOCK) FLOW_WAVES void k_flow(Soa S, int64_t n, Lev
   };
   // one run item: the option loops of a 64-entry list chunk (k_run's per-env work); returns the
   // lanes whose env's chunk became ready (its chunk in cl)
-  auto run = [&](uint32_t item, int& cl) FLOW_NOINL -> unsigned long long {
+  auto run = [&](uint32_t item, int& cl) -> unsigned long long {
       const int t = (int)(item >> 28), k = (int)((item >> 24) & 15u), j = (int)(item & 0xFFFFFFu);
       const int lidx = t * NLIST + k;
       int tail = 0;

@@ -6,7 +6,7 @@
 
 writes gym-treasure-game_amd/libtg_amd_NAME.so (timed by scripts/ab.py).  Every replacement
 must match exactly once in one of the csrc files.  EXTRA_FLAGS (environment) is appended to
-the compiler flags (e.g. '-mllvm -disable-machine-licm' or '-DTG_FLOW_W=4')."""
+the compiler flags (e.g. '-mllvm -disable-machine-licm')."""
 import os
 import shutil
 import subprocess
