@@ -1775,15 +1775,6 @@ Soa soa_of(const tg_batch* h, const StepCtx& c) {
   return Soa{h->S.st4 + c.off, h->S.ang + c.off, h->S.ep + c.off, h->S.mt + c.off * (int64_t)MT_STORE,
              h->S.mc + c.off * (int64_t)MT_CODES};
 }
-// the N = 1 calls' wait for their one launch: polled, not a blocking synchronisation (whose
-// wake-up after the kernel's completion costs microseconds of the ~25-us call)
-int spin_sync(hipStream_t st) {
-  hipError_t e;
-  while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
-  }
-  if (e != hipSuccess) return fail(TG_E_HIP, "stream wait: %s", hipGetErrorString(e));
-  return TG_OK;
-}
 int launch_regen(tg_batch* h, StepCtx& c, hipStream_t st) {
   if (!c.rpend) return TG_OK;
   unsigned long long* ks = nullptr;
@@ -2140,7 +2131,7 @@ int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t*
   hipLaunchKernelGGL((k_step<false, false, POL_IMMEDIATE>), dim3(1), dim3(BLOCK), 0, st, h->S,
                      h->n, h->L, h->grid, io, q, h->g0, h->main.stats, h->err, nullptr);
   HIP_TRY(hipGetLastError());
-  if (const int rc = spin_sync(st)) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
   memcpy(obs, h->one->obs, sizeof h->one->obs);
   *reward = h->one->reward;
   *valid = h->one->valid;
@@ -2183,7 +2174,7 @@ int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) 
                      h->py_dev, warm ? h->pyc : nullptr, h->pyc, st->index, (int)st->has_gauss,
                      st->gauss_next, h->one_dev, tstep, h->main.stats, h->err);
   HIP_TRY(hipGetLastError());
-  if (const int rc = spin_sync(stream)) return rc;
+  HIP_TRY(hipStreamSynchronize(stream));
   memcpy(st, h->py, sizeof(tg_pystate));
   h->py_last = *st;
   h->py_warm = true;
