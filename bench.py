@@ -440,8 +440,7 @@ class Runner:
         if K:
             raise AssertionError("rollout mode steps through advance()")
         elif self.timing and self.pre is not None:  # actions generated before timing
-            a = self.pre[t - self.pre_t0]
-            chk(L.tg_step(self.h, p(a), *self.args_step[2:]), "tg_step")
+            chk(L.tg_step(self.h, self.pre_ptr[t - self.pre_t0], *self.args_step[2:]), "tg_step")
         else:
             chk(L.tg_policy_actions(self.h, ACTION_SEED, t, self.pol, p(self.vec._act),
                                     self.stream), "actions")
@@ -502,6 +501,10 @@ class Runner:
         self.render_on = True
         if self.pre is not None:  # the timed steps' inputs, resident before timing
             self.pre_t0 = t
+            # their device addresses as call arguments, made once (a torch view and a ctypes
+            # pointer per step cost the host ~10 us, most visibly before the region's first
+            # launch)
+            self.pre_ptr = [self.p(self.pre[j]) for j in range(steps)]
             for j in range(steps):
                 self.tg._lib.check(self.L.tg_policy_actions(
                     self.h, ACTION_SEED, t + j, self.pol, self.p(self.pre[j]), self.stream),
