@@ -29,9 +29,11 @@
 #include "tg_batch.h"
 #include "tg_twist.h"
 
+#ifndef TG_FLOW_TU  // (tg_flow.hip includes this file for the device code only)
 namespace tg {
 thread_local std::string g_err;
 }
+#endif
 using namespace tg;
 
 namespace {
@@ -1523,6 +1525,15 @@ __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4,
 
 }  // namespace
 
+// k_flow<AR, POL> is instantiated in its own translation unit, tg_flow.hip, which is built
+// without MachineLICM (the pass hoisted values out of the flow's work loop and
+// held them live across it, 123-182 VGPRs; without it 121-129, 4 waves per SIMD)
+namespace tg {
+const void* flow_kernel(bool ar, int pol);
+}
+
+#ifndef TG_FLOW_TU
+
 namespace {
 int grid_for(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 // k_run needs one wave per 64-lane chunk of the worklists, each option padded to whole chunks:
@@ -1961,11 +1972,10 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
     const int rc = launch_regen(h, c, st);
     if (rc) return rc;
   }
-  decltype(&k_flow<true, 0>) kern = ar ? (pol ? k_flow<true, 1> : k_flow<true, 0>)
-                                       : (pol ? k_flow<false, 1> : k_flow<false, 0>);
+  const void* const kern = tg::flow_kernel(ar, pol);
   int& bpc = F.bpc[ar ? 1 : 0][pol ? 1 : 0];
   if (!bpc) {
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(kern), BLOCK, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, BLOCK, 0));
     if (bpc < 1) bpc = 1;
   }
   unsigned long long* ks = nullptr;
@@ -2019,8 +2029,22 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   if (getenv("TG_FLOW_DEBUG"))
     fprintf(stderr, "[flow] launching k %d grid %d x %d lcap %lld qcap %lld jcap %lld C %d\n", k, h->cus, bpc,
             (long long)F.lcap, (long long)F.qcap, (long long)F.jcap, F.C);
-  hipLaunchKernelGGL(kern, dim3((unsigned)(h->cus * bpc)), dim3(BLOCK), 0, st, h->S, h->n, h->L,
-                     h->grid, io, q, f, h->g0, c.stats, stat_slots(h->n), h->err, ks);
+  {  // k_flow's arguments, in its parameter order and types
+    Soa a_s = h->S;
+    int64_t a_n = h->n;
+    Level a_l = h->L;
+    const uint32_t* a_grid = h->grid;
+    FlowIO a_io = io;
+    EpQueue a_q = q;
+    int64_t a_g0 = h->g0;
+    unsigned long long* a_stats = c.stats;
+    int a_nstat = stat_slots(h->n);
+    uint32_t* a_err = h->err;
+    unsigned long long* a_ks = ks;
+    void* args[] = {&a_s, &a_n, &a_l, &a_grid, &a_io, &a_q, &f,
+                    &a_g0, &a_stats, &a_nstat, &a_err, &a_ks};
+    HIP_TRY(hipLaunchKernel(kern, dim3((unsigned)(h->cus * bpc)), dim3(BLOCK), args, 0, st));
+  }
   HIP_TRY(hipGetLastError());
   ++F.launches;
 #ifdef TG_FLOW_DBG
@@ -2637,3 +2661,4 @@ int tg_diag_stamps(unsigned long long* out, int n_waves) {
 #endif
 
 }  // extern "C"
+#endif  // TG_FLOW_TU

@@ -210,8 +210,11 @@ __global__ void k_census(uint32_t* mask) {
   if (threadIdx.x == 0) atomicOr(mask, 1u << (xcc_id() & 31u));
 }
 
+// 4 waves per SIMD (<= 128 VGPRs; built without MachineLICM, tg_flow.hip: 123-131 VGPRs
+// unconstrained) — r05j A/B: uniform 0.1111 vs 0.1163 ms per step at 3 waves, masked 0.3309 vs
+// 0.3491
 template <bool AR, int POL>
-__global__ __launch_bounds__(BLOCK) void k_flow(Soa S, int64_t n, Level L,
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_flow(Soa S, int64_t n, Level L,
                                                 const uint32_t* __restrict__ grid, FlowIO io,
                                                 EpQueue eq, Flow f, int64_t g0,
                                                 unsigned long long* __restrict__ stats, int nstat,

@@ -9,7 +9,6 @@ must match exactly once in one of the csrc files.  EXTRA_FLAGS (environment) is 
 the compiler flags (e.g. '-mllvm -disable-machine-licm')."""
 import os
 import shutil
-import subprocess
 import sys
 import tempfile
 
@@ -32,9 +31,7 @@ def main():
         t = open(hits[0]).read().replace(old, new)
         open(hits[0], "w").write(t)
     out = os.path.join(ROOT, "gym-treasure-game_amd", "libtg_amd_%s.so" % name)
-    srcs = [os.path.join(src, "tg_amd.hip"), os.path.join(src, "tg_render.hip")]
-    extra = os.environ.get("EXTRA_FLAGS", "").split()
-    subprocess.check_call([B.HIPCC] + B.FLAGS + extra + ["-o", out] + srcs)
+    B.compile_lib(out, csrc=src, extra=os.environ.get("EXTRA_FLAGS", "").split())
     shutil.rmtree(tmp)
     print(out)
 

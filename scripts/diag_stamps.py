@@ -4,7 +4,6 @@ cycles spent loading its envs (+ RNG window), running the option loop and in the
 with the loop's iteration count (max ticks over its lanes).  Not the product library."""
 import ctypes
 import os
-import subprocess
 import sys
 
 import numpy as np
@@ -23,7 +22,7 @@ SO = os.path.join(ROOT, "gym-treasure-game_amd",
 def main():
     from gym_treasure_game_amd import build as B
     if not (os.environ.get("NOBUILD") and os.path.exists(SO)):
-        subprocess.check_call([B.HIPCC] + B.FLAGS + ["-DTG_DIAG_STAMPS"] + FLAGS + ["-o", SO] + B.SRCS)
+        B.compile_lib(SO, extra=["-DTG_DIAG_STAMPS"] + FLAGS)
     _lib._lib = None
     _lib.LIB_PATH = SO
     L = _lib.load()
