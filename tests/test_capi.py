@@ -42,6 +42,27 @@ def test_library_has_gfx950_code_object(tg):
     assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the .hip_fatbin bundle id
 
 
+def test_library_links_the_flow_unit(tg):
+    """k_flow comes from its own unit (csrc/tg_flow.hip, built without MachineLICM): the
+    library exports its handle accessor, and the build compiles that unit with FLOW_FLAGS and
+    links the object with the other sources."""
+    out = subprocess.check_output(["nm", "-D", "--defined-only", tg._lib.LIB_PATH]).decode()
+    assert any("flow_kernel" in ln for ln in out.splitlines())
+    from gym_treasure_game_amd import build as B
+    calls = []
+    orig = B.subprocess.check_call
+    B.subprocess.check_call = lambda cmd: calls.append(cmd)
+    try:
+        B.compile_lib("/tmp/never_built.so")
+    finally:
+        B.subprocess.check_call = orig
+    flow, lib = calls
+    assert flow[-1].endswith("tg_flow.hip") and "-c" in flow
+    assert " ".join(B.FLOW_FLAGS) in " ".join(flow) and " ".join(B.FLOW_FLAGS) not in " ".join(lib)
+    assert lib[-3:] == ["-x", "none", "/tmp/never_built.so.flow.o"]
+    assert any(a.endswith("tg_amd.hip") for a in lib) and "-shared" in lib
+
+
 def test_bad_level_is_rejected_before_touching_a_device(tg):
     lib = tg._lib.load()
     h = ctypes.c_void_p()
