@@ -9,6 +9,7 @@ with -D flags); per policy and round, every variant runs the bench's workload (1
 seed 0, auto-reset, the bench's action stream) from construction through BURN untimed steps,
 then STEPS steps timed with HIP events (tg_step's kernels) and the wall clock.  Variants are
 interleaved and the best round (by wall clock) is reported, so that box-to-box spread cancels."""
+import ctypes
 import json
 import os
 import sys
@@ -49,10 +50,22 @@ def time_one(path, policy, n, burn, steps, mode="compact", K=0):
     torch.cuda.synchronize()
     vec.stats_reset()
     vec.set_timing(int(os.environ.get("TIMING", "0")))  # 0: the wall clock only (no events / stamps)
+    # DIRECT=1: the bench's call (bench.py step): tg_step through ctypes with the pointers made
+    # before timing and no final_obs rows, so that the host's per-call cost (a Python
+    # TreasureGameVec.step: ~0.12 ms) does not bound the uniform line
+    direct = os.environ.get("DIRECT") == "1" and acts is not None
+    if direct:
+        p = lambda x: ctypes.c_void_p(x.data_ptr())
+        ptrs = [p(a) for a in acts]
+        rest = (p(vec._obs), p(vec._rew), p(vec._valid), p(vec._done), None,
+                _lib.TG_STEP_AUTORESET, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     t0 = time.perf_counter()
     out = None
     for j in range(steps):
-        out = vec.step(acts[j] if acts is not None else vec.policy_actions(burn + j, ACTION_SEED, policy))
+        if direct:
+            _lib.check(vec._L.tg_step(vec.handle, ptrs[j], *rest), "tg_step")
+        else:
+            out = vec.step(acts[j] if acts is not None else vec.policy_actions(burn + j, ACTION_SEED, policy))
         if j % 10 == 9:
             vec.drain_episodes(rec, cnt)
     if regen:
@@ -61,7 +74,7 @@ def time_one(path, policy, n, burn, steps, mode="compact", K=0):
     dt = time.perf_counter() - t0
     st = vec.stats()
     # the last step's rows and the run's counts: equal for every variant (same results)
-    obs = out[0].contiguous().view(torch.int64)
+    obs = (vec._obs if out is None else out[0]).contiguous().view(torch.int64)
     digest = "%x/%d/%d" % (int((obs * torch.arange(1, obs.numel() + 1, device=obs.device,
                                                        dtype=torch.int64).view_as(obs)).sum()) & (2**64 - 1),
                           st["ticks"], st["draws"])
