@@ -8,7 +8,7 @@ The step path runs in libtg_amd.so (hand-written HIP for gfx950, C ABI in includ
 there is no CPU fallback.  Registration with gym / gymnasium happens on import when either is
 installed, mirroring gym_treasure_game/__init__.py:3-6.
 """
-from ._lib import TgError  # noqa: F401
+from ._lib import TG_ERR_FLOW, TgError  # noqa: F401
 from .envs import (OPTION_NAMES, STATE_NAMES, GpuOption, ObservationWrapper,  # noqa: F401
                    TreasureGame, TreasureGameVec, TreasureGameVectorEnv, make_vec, read_level)
 from .render import load_sprites, synthetic_sprites  # noqa: F401

@@ -477,6 +477,7 @@ __device__ __forceinline__ void kst_end(unsigned long long* ks, unsigned long lo
     atomicMax(s + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 }
+#ifndef TG_FLOW_TU  // (the other kernels: the main unit only; tg_flow.hip compiles k_flow alone)
 __global__ void k_kst_init(unsigned long long* ks, int64_t slots) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < slots) {
@@ -558,6 +559,8 @@ __global__ __launch_bounds__(BLOCK) void k_reset(Soa S, int64_t n, Level L,
     S.ep[i] = make_int2(0, (int32_t)tstep);  // the episode starts with the next step
   }
 }
+
+#endif  // TG_FLOW_TU
 
 struct StepIO {
   int32_t* __restrict__ actions;   // input; with policy >= 0 the step's actions are written here
@@ -1198,6 +1201,7 @@ constexpr int REGEN_STEPS = 16;
 // regen_ctr, per set: the 8 grab counters, then the 8 list lengths (k_classify's rcnt)
 constexpr int RCTR_LIST = 8;
 constexpr int RCTR_N = 16;
+#ifndef TG_FLOW_TU  // (the other kernels: the main unit only; tg_flow.hip compiles k_flow alone)
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  int64_t rcap, int32_t* __restrict__ ctr,
                                                  int32_t* __restrict__ ctr_next,
@@ -1266,8 +1270,11 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
   kst_end(ks, kt0);
 }
 
+#endif  // TG_FLOW_TU
+
 #include "tg_flow.h"
 
+#ifndef TG_FLOW_TU  // (the other kernels: the main unit only; tg_flow.hip compiles k_flow alone)
 __global__ __launch_bounds__(BLOCK) void k_mask(Soa S, int64_t n, Level L,
                                                  const uint32_t* __restrict__ grid,
                                                  uint16_t* __restrict__ out) {
@@ -1522,6 +1529,7 @@ __global__ __launch_bounds__(BLOCK) void k_errors(const uint4* __restrict__ st4,
   const uint32_t f = i < n ? (st4[i].y & E_MASK) : 0u;
   if (f) atomicOr(out, f);
 }
+#endif  // TG_FLOW_TU
 
 }  // namespace
 
@@ -1691,6 +1699,8 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   h->g0 = global_offset;
   h->seed0 = seed_base;
   h->domain = dom;
+  h->flow_debug = getenv("TG_FLOW_DEBUG") != nullptr;
+  if (const char* sp = getenv("TG_FLOW_SKIP_PART")) h->flow_skip = atoi(sp);
   // completed-episode queue: drained by tg_episodes; records beyond it are counted as dropped
   const int64_t cap = 4 * n > (1 << 16) ? 4 * n : (1 << 16);
   h->eps_cap = (int32_t)(cap < (1 << 28) ? cap : (1 << 28));
@@ -1934,7 +1944,7 @@ int flow_init(tg_batch* h) {
   for (int id = 0; id < 8; ++id)
     if ((mask >> id) & 1u) F.xmap = (F.xmap & ~(0xFu << (4 * id))) | ((uint32_t)F.P++ << (4 * id));
   if (F.P == 0) return fail(TG_E_HIP, "flow census: no XCC id in 0..7");
-  if (getenv("TG_FLOW_DEBUG")) fprintf(stderr, "[flow] census mask %08x P %d\n", mask, F.P);
+  if (h->flow_debug) fprintf(stderr, "[flow] census mask %08x P %d\n", mask, F.P);
   const int64_t C = (h->n + 63) / 64, cxm = (C + F.P - 1) / F.P;
   if (C > 0xFFFFFF) return fail(TG_E_INVAL, "flow mode: at most 2^24 chunks of 64 envs");
   F.C = (int32_t)C;
@@ -1992,41 +2002,12 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   F.parity ^= 1;
   Flow f{F.ctl[p], F.q[p], F.fill[p], F.list, F.outst, F.ctl[p ^ 1], F.q[p ^ 1], F.fill[p ^ 1],
          c.refill, c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
-         F.qcap, F.jcap, F.lcap, F.C, F.P, k, F.xmap, nullptr, nullptr, nullptr};
+         F.qcap, F.jcap, F.lcap, F.C, F.P, k, F.xmap, h->flow_skip, nullptr, nullptr, nullptr};
 #ifdef TG_FLOW_DBG
-  static uint32_t* dbg_host = nullptr;
-  static uint32_t* dbg_dev = nullptr;
-  if (!dbg_host) {
-    HIP_TRY(hipHostMalloc((void**)&dbg_host, 4096 * 4 * sizeof(uint32_t), hipHostMallocMapped));
-    HIP_TRY(hipHostGetDevicePointer((void**)&dbg_dev, dbg_host, 0));
-  }
-  memset(dbg_host, 0, 4096 * 4 * sizeof(uint32_t));
-  f.dbg = dbg_dev;
-  static uint32_t* dbgc = nullptr;
-  const size_t ndc = (size_t)F.C * 16 + 2 * (size_t)F.P * FLOW_MAX_K * NLIST * F.jcap;
-  if (!dbgc) HIP_TRY(hipMalloc((void**)&dbgc, sizeof(uint32_t) * ndc));
-  HIP_TRY(hipMemset(dbgc, 0, sizeof(uint32_t) * ndc));
-  f.dbgc = dbgc;
-#ifdef TG_FLOW_WAVELOG
-  f.dbg = nullptr;  // a timing log: no host-mapped progress words, no duplicate counters
-  f.dbgc = nullptr;
-#endif
-  static uint32_t* dbgl = nullptr;
-  const char* logp = getenv("TG_FLOW_LOG");
-  if (logp) {
-#ifdef TG_FLOW_WAVELOG
-    const size_t evb = 64 + 32 * (size_t)FLOW_EVW * (size_t)h->cus * 8 * (BLOCK / 64);
-    if (!dbgl) HIP_TRY(hipMalloc((void**)&dbgl, evb));
-    HIP_TRY(hipMemset(dbgl, 0, evb));
-#else
-    if (!dbgl) HIP_TRY(hipMalloc((void**)&dbgl, 64 + 32 * (size_t)FLOW_EVCAP));
-    HIP_TRY(hipMemset(dbgl, 0, 64));
-#endif
-    f.dbgl = dbgl;
-  }
+  if (const int rc = flow_diag_setup(h, f)) return rc;
 #endif
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
-  if (getenv("TG_FLOW_DEBUG"))
+  if (h->flow_debug)
     fprintf(stderr, "[flow] launching k %d grid %d x %d lcap %lld qcap %lld jcap %lld C %d\n", k, h->cus, bpc,
             (long long)F.lcap, (long long)F.qcap, (long long)F.jcap, F.C);
   {  // k_flow's arguments, in its parameter order and types
@@ -2047,63 +2028,13 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   }
   HIP_TRY(hipGetLastError());
   ++F.launches;
+  // every sub-problem's chunks finished (no XCD the census saw went without waves)
+  hipLaunchKernelGGL(k_flow_check, dim3(1), dim3(64), 0, st, F.ctl[p], F.P, F.C, h->err);
+  HIP_TRY(hipGetLastError());
 #ifdef TG_FLOW_DBG
-  {  // watch the waves' progress for up to 8 s
-    for (int ms = 0; ms < 8000 && hipStreamQuery(st) == hipErrorNotReady; ms += 10) usleep(10000);
-    const bool hung = hipStreamQuery(st) == hipErrorNotReady;
-    int hist[64] = {0};
-    for (int w = 0; w < 4096; ++w) hist[dbg_host[w * 4] & 63]++;
-    fprintf(stderr, "[flowdbg] launch %lld %s; waves by code:", (long long)F.launches, hung ? "HUNG" : "done");
-    for (int c = 0; c < 64; ++c)
-      if (hist[c]) fprintf(stderr, " %d:%d", c, hist[c]);
-    fprintf(stderr, "\n");
-    int shown = 0;
-    for (int w = 0; w < 4090 && shown < 40; ++w) {
-      const uint32_t c = dbg_host[w * 4];
-      if (c && c != 9 && c != 1) {
-        fprintf(stderr, "[flowdbg]  wave %d code %u %u %u %u\n", w, c, dbg_host[w * 4 + 1], dbg_host[w * 4 + 2],
-                dbg_host[w * 4 + 3]);
-        ++shown;
-      }
-    }
-    for (int w = 4091; w < 4096; ++w)
-      if (dbg_host[w * 4])
-        fprintf(stderr, "[flowdbg]  DUP slot %d: code %u %u %08x %08x\n", w, dbg_host[w * 4], dbg_host[w * 4 + 1],
-                dbg_host[w * 4 + 2], dbg_host[w * 4 + 3]);
-    if (logp && !hung) {  // the event log, for scripts/flow_log.py
-      uint32_t cnt = 0;
-#ifdef TG_FLOW_WAVELOG
-      std::vector<uint32_t> ev((size_t)FLOW_EVW * h->cus * bpc * (BLOCK / 64) * 8);
-      HIP_TRY(hipMemcpy(ev.data(), dbgl + 16, ev.size() * 4, hipMemcpyDeviceToHost));
-      for (size_t r = 0; r < ev.size() / 8; ++r)  // the non-empty records, in place
-        if (ev[r * 8]) {
-          std::copy(ev.begin() + r * 8, ev.begin() + r * 8 + 8, ev.begin() + (size_t)cnt * 8);
-          ++cnt;
-        }
-      ev.resize((size_t)cnt * 8);
-#else
-      HIP_TRY(hipMemcpy(&cnt, dbgl, 4, hipMemcpyDeviceToHost));
-      if (cnt > FLOW_EVCAP) cnt = FLOW_EVCAP;
-      std::vector<uint32_t> ev((size_t)cnt * 8);
-      HIP_TRY(hipMemcpy(ev.data(), dbgl + 16, ev.size() * 4, hipMemcpyDeviceToHost));
+  if (const int rc = flow_diag_after(h, f, k, bpc, st)) return rc;
 #endif
-      char path[512];
-      snprintf(path, sizeof path, "%s.%lld.bin", logp, (long long)F.launches);
-      if (FILE* fp = fopen(path, "wb")) {
-        const uint32_t hdr[8] = {cnt, (uint32_t)F.C, (uint32_t)F.P, (uint32_t)k, F.xmap, (uint32_t)F.jcap, 0, 0};
-        fwrite(hdr, 4, 8, fp);
-        fwrite(ev.data(), 4, ev.size(), fp);
-        fclose(fp);
-      }
-      fprintf(stderr, "[flowdbg] %u events -> %s\n", cnt, path);
-    }
-    if (hung) {
-      fflush(stderr);
-      _exit(3);
-    }
-  }
-#endif
-  if (getenv("TG_FLOW_DEBUG")) {  // diagnostics: the census and every sub-problem's counters
+  if (h->flow_debug) {  // diagnostics: the census and every sub-problem's counters
     HIP_TRY(hipDeviceSynchronize());
     std::vector<int32_t> cw((size_t)F.P * CTL_WORDS);
     HIP_TRY(hipMemcpy(cw.data(), F.ctl[p], sizeof(int32_t) * cw.size(), hipMemcpyDeviceToHost));
@@ -2251,7 +2182,7 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
                   reward + (size_t)s * n, valid + (size_t)s * n, done + (size_t)s * n,
                   nullptr, policy, action_seed, t0 + s};
   };
-  if (h->grp.empty() && h->mode == TG_MODE_FLOW) {  // k_flow, up to FLOW_MAX_K steps per launch
+  if (h->mode == TG_MODE_FLOW) {  // k_flow, up to FLOW_MAX_K steps per launch (no groups: tg_set_mode)
     int rc = flow_init(h);
     for (int32_t s = 0; s < steps && !rc; s += FLOW_MAX_K) {
       const int k = steps - s < FLOW_MAX_K ? steps - s : FLOW_MAX_K;
@@ -2296,6 +2227,9 @@ int tg_rollout(tg_batch* h, int32_t steps, uint64_t action_seed, int64_t t0, int
 
 int tg_set_groups(tg_batch* h, int32_t groups, int32_t stagger) {
   BIND(h);
+  if (groups > 1 && h->mode == TG_MODE_FLOW)
+    return fail(TG_E_INVAL, "tg_set_groups: groups are a TG_MODE_COMPACT rollout form (TG_MODE_FLOW "
+                            "steps the whole batch in one k_flow launch)");
   if (groups < 1 || groups > 16 || (int64_t)groups * 4096 > h->n)
     return fail(TG_E_INVAL, "tg_set_groups: %d groups of %lld envs (1..16, >= 4096 envs each)",
                 groups, (long long)h->n);
@@ -2393,6 +2327,9 @@ int tg_set_mode(tg_batch* h, int mode, int run_blocks) {
   BIND(h);
   if (mode != TG_MODE_DIRECT && mode != TG_MODE_COMPACT && mode != TG_MODE_FLOW)
     return fail(TG_E_INVAL, "tg_set_mode: unknown mode %d", mode);
+  if (mode == TG_MODE_FLOW && !h->grp.empty())
+    return fail(TG_E_INVAL, "tg_set_mode: TG_MODE_FLOW steps the whole batch in one k_flow launch; "
+                            "call tg_set_groups(h, 1, 0) first");
   h->mode = mode;
   (void)run_blocks;  // reserved
   return TG_OK;

@@ -137,6 +137,11 @@ struct tg_batch {
     int bpc[2][2] = {{0, 0}, {0, 0}};  // k_flow<AR, POL> workgroups per CU (occupancy API)
     int64_t launches = 0;
   } fl;
+  // read once at tg_create: TG_FLOW_DEBUG (print the census and every k_flow launch's
+  // sub-problem counters; synchronises after each launch) and the test hook TG_FLOW_SKIP_PART
+  // (sub-problem x's waves leave at once: tests/test_gpu_flow.py checks TG_ERR_FLOW is raised)
+  bool flow_debug = false;
+  int flow_skip = -1;
 };
 
 namespace tg {

@@ -34,8 +34,12 @@
 // their stores (`s_waitcnt vmcnt(0)`) before the atomic that publishes them; every load of
 // handed-off bytes (env state, list entries, queue slots, the MT codes and words, which an
 // env's per-lane regeneration may have rewritten on another CU) bypasses L1 (sc1 loads, sc1
-// LDS-DMA; regen_half_flow invalidates L1 first).  Placement decides speed only where it is
-// read from the hardware; nothing assumes blockIdx -> XCD.
+// LDS-DMA; regen_half_flow invalidates L1 first).  Nothing assumes blockIdx -> XCD, but the
+// chunks of sub-problem x are stepped only by waves running on XCD x: a launch that places no
+// workgroup on an XCD the census saw (a CU-masked stream, another partition layout) leaves that
+// sub-problem unstepped, and no wave of it waits to time out.  k_flow_check, launched after every
+// k_flow on its stream, compares each sub-problem's finished chunks with its chunk count and
+// sets TG_ERR_FLOW on a mismatch.
 //
 // Every spin is bounded (FLOW_DEADLINE of the 100 MHz clock): a wave that waits longer sets
 // TG_ERR_FLOW and its sub-problem's done word, so a bug ends the launch instead of hanging it.
@@ -82,57 +86,12 @@ struct Flow {
   int64_t rcap, qcap, jcap, lcap;
   int32_t C, P, K;   // chunks, sub-problems, steps
   uint32_t xmap;     // nibble x: the sub-problem of XCC id x (0xF: none)
+  int32_t skip;      // test hook (TG_FLOW_SKIP_PART): this sub-problem's waves leave at once, as
+                     // if its XCD had no workgroup (k_flow_check must flag it); -1: none
   uint32_t* dbg;     // TG_FLOW_DBG builds: per-wave progress in mapped host memory (else null)
   uint32_t* dbgc;    // TG_FLOW_DBG builds: [C][16] classifications, [P][16][NLIST][jcap] runs
   uint32_t* dbgl;    // TG_FLOW_DBG builds: event log (count at [0], 32-B records from [16])
 };
-#ifdef TG_FLOW_DBG
-// DIAGNOSTIC BUILD ONLY: lane 0 of wave gw < 4096 publishes (code, a, b, c) to host memory
-#define FLOW_DBG(code, a, b, c)                                                                  \
-  do {                                                                                           \
-    const int64_t gw_ = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;                        \
-    if (f.dbg && lane == 0 && gw_ < 4096) {                                                      \
-      __hip_atomic_store(f.dbg + gw_ * 4 + 0, (uint32_t)(code), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
-      __hip_atomic_store(f.dbg + gw_ * 4 + 1, (uint32_t)(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);    \
-      __hip_atomic_store(f.dbg + gw_ * 4 + 2, (uint32_t)(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);    \
-      __hip_atomic_store(f.dbg + gw_ * 4 + 3, (uint32_t)(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);    \
-    }                                                                                            \
-  } while (0)
-// DIAGNOSTIC BUILD ONLY: one 32-B event record (type, a, b, c, d, wave, clock) per calling lane
-constexpr uint32_t FLOW_EVCAP = 1u << 22;
-#ifdef TG_FLOW_WAVELOG
-// (wave-local form: each wave's lane 0 appends to its own FLOW_EVW slots, no shared counter;
-// the lane-level events 3 and 4 are left out)
-constexpr uint32_t FLOW_EVW = 1024;
-#define FLOW_EV(ty, a, b, c, d)                                                                   \
-  do {                                                                                           \
-    if (f.dbgl && (ty) != 3 && (ty) != 4 && evn_ < FLOW_EVW) {                                   \
-      const int64_t gw_ = ((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;                      \
-      const unsigned long long tm_ = realtime();                                                 \
-      uint4* r_ = reinterpret_cast<uint4*>(f.dbgl + 16) + 2 * (gw_ * FLOW_EVW + evn_++);           \
-      r_[0] = make_uint4((uint32_t)(ty), (uint32_t)(a), (uint32_t)(b), (uint32_t)(c));            \
-      r_[1] = make_uint4((uint32_t)(d), (uint32_t)gw_, (uint32_t)tm_, (uint32_t)(tm_ >> 32));     \
-    }                                                                                            \
-  } while (0)
-#else
-#define FLOW_EV(ty, a, b, c, d)                                                                   \
-  do {                                                                                           \
-    if (f.dbgl) {                                                                                \
-      const uint32_t k_ = atomicAdd(f.dbgl, 1u);                                                 \
-      if (k_ < FLOW_EVCAP) {                                                                     \
-        const unsigned long long tm_ = realtime();                                               \
-        uint4* r_ = reinterpret_cast<uint4*>(f.dbgl + 16) + 2 * (int64_t)k_;                      \
-        r_[0] = make_uint4((uint32_t)(ty), (uint32_t)(a), (uint32_t)(b), (uint32_t)(c));          \
-        r_[1] = make_uint4((uint32_t)(d), (uint32_t)(((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6), \
-                           (uint32_t)tm_, (uint32_t)(tm_ >> 32));                                \
-      }                                                                                          \
-    }                                                                                            \
-  } while (0)
-#endif
-#else
-#define FLOW_DBG(code, a, b, c) (void)0
-#define FLOW_EV(ty, a, b, c, d) (void)0
-#endif
 // the rollout's outputs, step-major [K][N] (obs_stride 0: one scratch row set for all steps)
 struct FlowIO {
   int32_t* actions;  // may be null
@@ -205,10 +164,38 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x;
 }
 
+#ifdef TG_FLOW_DBG
+#include "tg_flow_diag.h"  // (diagnostic builds only: the bring-up instrumentation)
+#else
+// the product: every diagnostic hook is a no-op
+#define FLOW_DBG(code, a, b, c) (void)0
+#define FLOW_EV(ty, a, b, c, d) (void)0
+#define FLOW_EV_WAVE(ty, a, b) (void)0
+#define FLOW_EV_LANE(ty, a, b, c, d) (void)0
+#define FLOW_DIAG_WAVE_STATE (void)0
+#define FLOW_DIAG_PUSH(t, k, j) (void)0
+#define FLOW_DIAG_RUN(item, i, live, mcnt, tail, lidx, j) (void)0
+#define FLOW_DIAG_TAKE(item, h) (void)0
+#define FLOW_DIAG_PATH(p) (void)0
+#define FLOW_DIAG_CLASSIFY(c, t) (void)0
+#endif
+
+#ifndef TG_FLOW_TU  // (launched by tg_amd.hip's host code: the main unit only)
 // the XCC ids the device's workgroups run on (one bit each): the flow's sub-problems
 __global__ void k_census(uint32_t* mask) {
   if (threadIdx.x == 0) atomicOr(mask, 1u << (xcc_id() & 31u));
 }
+// after every k_flow launch, on its stream (one wave): a sub-problem whose chunks did not all
+// finish step K - 1 sets TG_ERR_FLOW (no wave ran on its XCD; see "Coherence" above)
+__global__ void k_flow_check(const int32_t* __restrict__ ctl, int P, int32_t C,
+                             uint32_t* __restrict__ err_or) {
+  const int x = (int)threadIdx.x;
+  if (x < P) {
+    const int Cx = (C - x + P - 1) / P;
+    if (Cx > 0 && ctl[(int64_t)x * CTL_WORDS + FC_FIN * FC_STRIDE] != Cx) atomicOr(err_or, E_FLOW);
+  }
+}
+#endif
 
 // 4 waves per SIMD (<= 128 VGPRs; built without MachineLICM, tg_flow.hip: 123-131 VGPRs
 // unconstrained) — r05j A/B: uniform 0.1111 vs 0.1163 ms per step at 3 waves, masked 0.3309 vs
@@ -243,7 +230,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   uint8_t* const warea = wall + (threadIdx.x >> 6) * FLOW_WAVE_BYTES;
   const int x = (int)((f.xmap >> (4u * (xcc_id() & 7u))) & 0xFu);
   FLOW_DBG(1, x, 0, 0);
-  if (x >= f.P) {  // an XCD the census did not see: no sub-problem (the whole workgroup)
+  if (x >= f.P || x == f.skip) {  // an XCD the census did not see: no sub-problem (the workgroup)
     kst_end(ks, kt0);
     return;
   }
@@ -259,26 +246,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   int32_t* const list = f.list + (int64_t)x * FLOW_MAX_K * NLIST * f.lcap;
   const int64_t slot = (int64_t)blockIdx.x % nstat;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
-#ifdef TG_FLOW_DBG
-  uint32_t evn_ = 0;  // (TG_FLOW_WAVELOG: this wave's events logged)
-  (void)evn_;
-#endif
+  FLOW_DIAG_WAVE_STATE;
   if (lane == 0) FLOW_EV(10, x, 0, 0, 0);
 
   // a run item on the queue (by the lane that calls it)
   auto push = [&](int t, int k, int j, int src) {
-#ifdef TG_FLOW_DBG
-    if (f.dbgc && k != Q_CLASSIFY) {  // pushes per list chunk: a second push of one goes to slot 4093
-      const int64_t base2 = (int64_t)f.C * 16 + (int64_t)f.P * FLOW_MAX_K * NLIST * f.jcap;
-      const uint32_t o = atomicAdd(&f.dbgc[base2 + ((int64_t)x * FLOW_MAX_K * NLIST + t * NLIST + k) * f.jcap + j], 1u);
-      if (o && atomicCAS(f.dbg + 4093 * 4, 0u, 97u) == 0u) {
-        f.dbg[4093 * 4 + 1] = ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j;
-        f.dbg[4093 * 4 + 2] = (uint32_t)ld_sc1(fcw(ctl, FC_LTAIL + t * NLIST + k)) | ((uint32_t)x << 24);
-        f.dbg[4093 * 4 + 3] = (uint32_t)ld_sc1(fill + (int64_t)(t * NLIST + k) * f.jcap + j) |
-                              ((uint32_t)ld_sc1(fcw(ctl, FC_CLS + t)) << 16);
-      }
-    }
-#endif
+    FLOW_DIAG_PUSH(t, k, j);
     const int at = atomicAdd(fcw(ctl, FC_QTAIL), 1);
     FLOW_EV(4, ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j, at, src, x);
     if ((int64_t)at < f.qcap) st_sc1(q + at, ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j);
@@ -309,9 +282,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     bool runs = false;
     if (live) {
       unpack_st4(s4, e);
-#ifdef TG_FLOW_WAVELOG
-      if (lane == 0) FLOW_EV(11, c, t, 0, 0);  // (timing log: the state loads returned)
-#endif
+      FLOW_EV_WAVE(11, c, t);  // (timing log: the state loads returned)
       const int act = policy_action(L, m, e, POL, io.a0, g0 + i, io.t0 + t);
       if (io.actions) io.actions[(int64_t)t * n + i] = act;
       k = option_index(act);
@@ -362,9 +333,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     }
     if (fin && (e.f & E_MASK)) atomicOr(err_or, e.f & E_MASK);
     store_obs_wave(st.obs, (int64_t)c * 64, __ballot(fin), orow, reinterpret_cast<double*>(warea));
-#ifdef TG_FLOW_WAVELOG
-    if (lane == 0) FLOW_EV(12, c, t, 0, 0);  // (timing log: the rows issued)
-#endif
+    FLOW_EV_WAVE(12, c, t);  // (timing log: the rows issued)
     // the handed-off bytes: refill entries, list entries, the state, the chunk's count
     sbase = __builtin_amdgcn_readlane(sbase, 0);
     if (stale)
@@ -382,9 +351,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     // next step in this wave: its stores land first too); then the fill counts and the step's
     // classified-chunk count together (the flush reads only the list tails, reserved above)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef TG_FLOW_WAVELOG
-    if (lane == 0) FLOW_EV(13, c, t, 0, 0);  // (timing log: the stores complete)
-#endif
+    FLOW_EV_WAVE(13, c, t);  // (timing log: the stores complete)
     int32_t* const fl = fill + (int64_t)lidx * f.jcap;
     const int j0 = base >> 6, in0 = min(nb, 64 - (base & 63));
     int f0 = 0, f1 = 0, last = 0;
@@ -410,34 +377,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   // lanes whose env's chunk became ready (its chunk in cl)
   auto run = [&](uint32_t item, int& cl) -> unsigned long long {
       const int t = (int)(item >> 28), k = (int)((item >> 24) & 15u), j = (int)(item & 0xFFFFFFu);
-      const int lidx = t * NLIST + k;
+      // a cheap guard: an item or entry out of range is a protocol bug; it sets
+      // TG_ERR_FLOW and runs nothing instead of addressing memory with it
+      const bool item_ok = t < K && k < NLIST && (int64_t)j < f.jcap;
+      const int lidx = item_ok ? t * NLIST + k : 0;
       int tail = 0;
-      if (lane == 0) tail = ld_sc1(fcw(ctl, FC_LTAIL + lidx));
+      if (lane == 0 && item_ok) tail = ld_sc1(fcw(ctl, FC_LTAIL + lidx));
       tail = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(tail, 0));
-      const int mcnt = min(64, tail - 64 * j);
-      const bool live = lane < mcnt;
+      const int mcnt = item_ok ? min(64, tail - 64 * j) : 0;
+      bool live = lane < mcnt;
       int64_t i = 0;
       if (live) i = ld_sc1(list + (int64_t)lidx * f.lcap + 64 * j + lane);
-#ifdef TG_FLOW_DBG
-      if (f.dbgc) {
-        // every entry an env of this sub-problem; the chunk's fill count = the entries run
-        const bool bad = live && (i < 0 || i >= n || (int)((i >> 6) % P) != x);
-        if (__ballot(bad) && lane == __ffsll((long long)__ballot(bad)) - 1 &&
-            atomicCAS(f.dbg + 4092 * 4, 0u, 96u) == 0u) {
-          f.dbg[4092 * 4 + 1] = item;
-          f.dbg[4092 * 4 + 2] = (uint32_t)i;
-          f.dbg[4092 * 4 + 3] = (uint32_t)lane | ((uint32_t)mcnt << 8) | ((uint32_t)x << 16);
-        }
-        if (lane == 0) {
-          const int fl = ld_sc1(fill + (int64_t)lidx * f.jcap + j);
-          if (fl != mcnt && atomicCAS(f.dbg + 4091 * 4, 0u, 95u) == 0u) {
-            f.dbg[4091 * 4 + 1] = item;
-            f.dbg[4091 * 4 + 2] = (uint32_t)fl | ((uint32_t)x << 24);
-            f.dbg[4091 * 4 + 3] = (uint32_t)tail;
-          }
-        }
-      }
-#endif
+      const bool bad = live && (i < 0 || i >= n || (int)((i >> 6) % P) != x);
+      if (lane == 0 && (!item_ok || __ballot(bad))) atomicOr(err_or, E_FLOW);
+      live = live && !bad;
+      FLOW_DIAG_RUN(item, i, live, mcnt, tail, lidx, j);
       const StepIO st = step_io(t);
       StepResult r{0, 0, 0, 0};
       Env e;
@@ -473,9 +427,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       int old = 0;
       if (live) old = atomicSub(&f.outst[i >> 6], 1);
-#ifdef TG_FLOW_LANES
-      if (live) FLOW_EV(3, item, (uint32_t)i, (uint32_t)old, (uint32_t)lane | ((uint32_t)mcnt << 8) | ((uint32_t)x << 16));
-#endif
+      if (live) FLOW_EV_LANE(3, item, (uint32_t)i, (uint32_t)old, (uint32_t)lane | ((uint32_t)mcnt << 8) | ((uint32_t)x << 16));
       unsigned long long ready = __ballot(live && old == 1);
       if (lane == 0) FLOW_EV(7, item, (uint32_t)__popcll(ready), (uint32_t)mcnt, x);
       cl = (int)(i >> 6);
@@ -495,15 +447,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   bool phase0 = true;
   int cl = 0;                    // (per lane) the chunk of the lane's env in the last run item
   int cc = -1, ct = 0;           // the carried chunk and its step
-#ifdef TG_FLOW_DBG
-  int path = 0;
-  uint32_t dbg_item = 0;
-#endif
   while (true) {
     int c, t;
-#ifdef TG_FLOW_DBG
-    path = cc >= 0 ? 1 : phase0 ? 3 : 2;
-#endif
+    FLOW_DIAG_PATH(cc >= 0 ? 1 : phase0 ? 3 : 2);
     if (cc >= 0) {
       c = cc;
       t = ct;
@@ -551,21 +497,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       if (item == Q_EMPTY) break;
       FLOW_DBG(3, h, item, x);
       if (lane == 0) FLOW_EV(5, h, item, x, 0);
-#ifdef TG_FLOW_DBG
-      dbg_item = item;
-      if (lane == 0 && f.dbgc && ((item >> 24) & 15u) != Q_CLASSIFY) {
-        const int it_l = (int)((item >> 28) * NLIST + ((item >> 24) & 15u));
-        const uint32_t o = atomicAdd(&f.dbgc[(int64_t)f.C * 16 + ((int64_t)x * FLOW_MAX_K * NLIST + it_l) * f.jcap + (item & 0xFFFFFFu)], 1u);
-        if (o && atomicCAS(f.dbg + 4094 * 4, 0u, 98u) == 0u) {
-          f.dbg[4094 * 4 + 1] = item;
-          f.dbg[4094 * 4 + 2] = (uint32_t)h;
-          f.dbg[4094 * 4 + 3] = (uint32_t)x;
-        }
-      }
-#endif
+      FLOW_DIAG_TAKE(item, h);
       t = (int)(item >> 28);
       if (((item >> 24) & 15u) == Q_CLASSIFY) {  // a chunk another wave's run item completed
         c = (int)(item & 0xFFFFFFu);
+        if (t >= K || c >= f.C || c % P != x) {  // (the guard above, for classification items)
+          if (lane == 0) atomicOr(err_or, E_FLOW);
+          continue;
+        }
       } else {
         const unsigned long long rd = run(item, cl);
         // (readfirstlane returns int: each half is cast back to 32 bits before it widens, or
@@ -597,19 +536,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       continue;
     }
     FLOW_DBG(10 + t, c, x, 0);
-#ifdef TG_FLOW_DBG
-    if (lane == 0) FLOW_EV(1, c, t, path, x);
-    if (lane == 0 && f.dbgc) {
-      const uint32_t o = atomicAdd(&f.dbgc[(int64_t)c * 16 + t], 1u);
-      if (o) {  // a duplicate classification: the first one seen goes to slot 4095
-        if (atomicCAS(f.dbg + 4095 * 4, 0u, 99u) == 0u) {
-          f.dbg[4095 * 4 + 1] = (uint32_t)c;
-          f.dbg[4095 * 4 + 2] = (uint32_t)t | ((uint32_t)path << 8) | ((uint32_t)x << 16);
-          f.dbg[4095 * 4 + 3] = dbg_item;
-        }
-      }
-    }
-#endif
+    FLOW_DIAG_CLASSIFY(c, t);
     const int cnt = __builtin_amdgcn_readfirstlane(classify(c, t));
     FLOW_DBG(30 + t, c, x, cnt);
     if (cnt == 0) {  // no env of the chunk runs an option: its next step at once

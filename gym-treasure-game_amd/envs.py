@@ -158,6 +158,7 @@ class TreasureGameVec:
         self.action_space = Discrete(_lib.NUM_ACTIONS)
         self.observation_space = Box(np.float32(0.0), np.float32(1.0), shape=(_lib.OBS_DIM,))
         self.option_names = list(OPTION_NAMES)
+        self._mode = "compact"
         if mode != "compact":
             self.set_mode(mode)
 
@@ -214,12 +215,17 @@ class TreasureGameVec:
                 self._out(self._done), info)
 
     def rollout(self, steps, t0=0, action_seed=0x5EED0001, policy="uniform", obs=True,
-                actions=True):
+                actions=True, check_flow=True):
         """``steps`` env-steps in one call with the on-device synthetic policy (tg_rollout):
         step t0 + s takes ``policy_actions(t0 + s, action_seed, policy)``, evaluated inside the
         step kernels.  Returns step-major device tensors: reward i32 [K, N], valid / done u8
         [K, N], and (optionally) obs f64 [K, N, 9], actions i32 [K, N].  With auto-reset the
-        obs rows are the post-reset ones and finished episodes queue for ``episodes()``."""
+        obs rows are the post-reset ones and finished episodes queue for ``episodes()``.
+
+        In "flow" mode a k_flow launch that fails its protocol checks (a wait past its bound,
+        a sub-problem left unstepped, an item out of range) sets TG_ERR_FLOW and its rows are
+        not valid: with ``check_flow`` (the default) the call then synchronises on
+        ``errors()`` and raises TgError."""
         pol = {"uniform": _lib.TG_POLICY_UNIFORM, "masked": _lib.TG_POLICY_MASKED}[policy]
         k, n, dev = int(steps), self.num_envs, self.device
         out = {"reward": torch.empty((k, n), dtype=torch.int32, device=dev),
@@ -234,6 +240,8 @@ class TreasureGameVec:
                                  _ptr(out.get("actions")), _ptr(out.get("obs")),
                                  _ptr(out["reward"]), _ptr(out["valid"]), _ptr(out["done"]),
                                  self._stream()), "tg_rollout")
+        if check_flow and self._mode == "flow" and self.errors() & _lib.TG_ERR_FLOW:
+            raise TgError("tg_rollout: a k_flow launch set TG_ERR_FLOW (its rows are not valid)")
         return out
 
     def set_groups(self, groups=1, stagger=False):
@@ -306,6 +314,7 @@ class TreasureGameVec:
         m = {"direct": _lib.TG_MODE_DIRECT, "compact": _lib.TG_MODE_COMPACT,
              "flow": _lib.TG_MODE_FLOW}[mode]
         check(self._L.tg_set_mode(self.handle, m, int(run_blocks)), "tg_set_mode")
+        self._mode = mode
 
     def set_episode_capacity(self, cap):
         """Resize the completed-episode queue (discards what it holds)."""

@@ -97,3 +97,39 @@ def test_flow_equals_oracle(tg, oracle):
         assert np.array_equal(r[key].cpu().numpy().T, ref[key][:, 1:]), key
     assert v.errors() == 0
     v.close()
+
+
+def test_flow_unstepped_subproblem_is_flagged(tg, monkeypatch):
+    """chunks x, x + P, ... are stepped only by waves on XCD x; a launch that leaves
+    a sub-problem without waves must not pass silently.  The test hook TG_FLOW_SKIP_PART (read
+    at tg_create) makes sub-problem 3's waves leave at once; k_flow_check sets TG_ERR_FLOW and
+    rollout() raises"""
+    monkeypatch.setenv("TG_FLOW_SKIP_PART", "3")
+    v = tg.TreasureGameVec(4096, seed=2, autoreset=True, mode="flow")
+    monkeypatch.delenv("TG_FLOW_SKIP_PART")
+    v.reset()
+    with pytest.raises(tg.TgError, match="TG_ERR_FLOW"):
+        v.rollout(4, t0=0, action_seed=5, policy="uniform")
+    v.rollout(4, t0=4, action_seed=5, policy="uniform", check_flow=False)
+    assert v.errors() & tg.TG_ERR_FLOW
+    v.close()
+    # a handle created without the hook steps every sub-problem
+    w = tg.TreasureGameVec(4096, seed=2, autoreset=True, mode="flow")
+    w.reset()
+    w.rollout(4, t0=0, action_seed=5, policy="uniform")
+    assert w.errors() == 0
+    w.close()
+
+
+def test_flow_rejects_groups(tg):
+    """TG_MODE_FLOW steps the whole batch in one k_flow launch; env groups are a
+    compact-mode rollout form, so the two are refused together instead of one being ignored"""
+    v = tg.TreasureGameVec(8192, seed=1)
+    v.set_groups(2)
+    with pytest.raises(tg.TgError, match="groups"):
+        v.set_mode("flow")
+    v.set_groups(1)
+    v.set_mode("flow")
+    with pytest.raises(tg.TgError, match="groups"):
+        v.set_groups(2)
+    v.close()
