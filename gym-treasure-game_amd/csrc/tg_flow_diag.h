@@ -70,7 +70,7 @@ constexpr uint32_t FLOW_EVW = 1024;
 // a second push of one list chunk (slot 4093)
 #define FLOW_DIAG_PUSH(t, k, j)                                                                   \
   do {                                                                                           \
-    if (f.dbgc && (k) != Q_CLASSIFY) {                                                           \
+    if (f.dbgc) {                                                                                \
       const int64_t base2_ = (int64_t)f.C * 16 + (int64_t)f.P * FLOW_MAX_K * NLIST * f.jcap;      \
       const uint32_t o_ = atomicAdd(&f.dbgc[base2_ + ((int64_t)x * FLOW_MAX_K * NLIST + (t) * NLIST + (k)) * f.jcap + (j)], 1u); \
       if (o_ && atomicCAS(f.dbg + 4093 * 4, 0u, 97u) == 0u) {                                    \
@@ -96,7 +96,8 @@ constexpr uint32_t FLOW_EVW = 1024;
       }                                                                                          \
       if (lane == 0) {                                                                           \
         const int fl_ = ld_sc1(fill + (int64_t)(lidx) * f.jcap + (j));                           \
-        if (fl_ != (mcnt) && atomicCAS(f.dbg + 4091 * 4, 0u, 95u) == 0u) {                       \
+        if (((fl_ & 0xFF) != 64 || ((fl_ >> 8) ? (fl_ >> 8) : 64) != (mcnt)) &&                   \
+            atomicCAS(f.dbg + 4091 * 4, 0u, 95u) == 0u) {                                         \
           f.dbg[4091 * 4 + 1] = (item);                                                          \
           f.dbg[4091 * 4 + 2] = (uint32_t)fl_ | ((uint32_t)x << 24);                              \
           f.dbg[4091 * 4 + 3] = (uint32_t)(tail);                                                \
@@ -109,9 +110,9 @@ constexpr uint32_t FLOW_EVW = 1024;
 #define FLOW_DIAG_TAKE(item, h)                                                                   \
   do {                                                                                           \
     item_ = (item);                                                                              \
-    if (lane == 0 && f.dbgc && (((item) >> 24) & 15u) != Q_CLASSIFY) {                           \
+    if (lane == 0 && f.dbgc) {                                                                   \
       const int it_l_ = (int)(((item) >> 28) * NLIST + (((item) >> 24) & 15u));                  \
-      const uint32_t o_ = atomicAdd(&f.dbgc[(int64_t)f.C * 16 + ((int64_t)x * FLOW_MAX_K * NLIST + it_l_) * f.jcap + ((item) & 0xFFFFFFu)], 1u); \
+      const uint32_t o_ = atomicAdd(&f.dbgc[(int64_t)f.C * 16 + ((int64_t)x * FLOW_MAX_K * NLIST + it_l_) * f.jcap + ((item) & 0x3FFFFu)], 1u); \
       if (o_ && atomicCAS(f.dbg + 4094 * 4, 0u, 98u) == 0u) {                                    \
         f.dbg[4094 * 4 + 1] = (item);                                                            \
         f.dbg[4094 * 4 + 2] = (uint32_t)(h);                                                     \
@@ -121,6 +122,7 @@ constexpr uint32_t FLOW_EVW = 1024;
   } while (0)
 
 #define FLOW_DIAG_PATH(p) (path_ = (p))
+#define FLOW_DIAG_TAIL(v) const int v = 0  // (FLOW_DIAG_RUN's tail word: unused by the run-ahead form)
 
 // a chunk classified twice for one step (slot 4095)
 #define FLOW_DIAG_CLASSIFY(c, t)                                                                  \
