@@ -1917,7 +1917,7 @@ int regen_all(tg_batch* h, hipStream_t st) {
 // ---- TG_MODE_FLOW (tg_flow.h) ----------------------------------------------------------------
 void flow_free(tg_batch* h) {
   auto& F = h->fl;
-  void* bufs[] = {F.ctl[0], F.ctl[1], F.q[0], F.q[1], F.fill[0], F.fill[1], F.list};
+  void* bufs[] = {F.ctl[0], F.ctl[1], F.q[0], F.q[1], F.fill[0], F.fill[1], F.list, F.outst, F.cstep};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   F = {};
@@ -1950,13 +1950,14 @@ int flow_init(tg_batch* h) {
   // chunk only below list chunk cxm, so a list's places stay below 2 cxm * 64 and its chunks
   // below 2 cxm + 1
   const int64_t C = (h->n + 63) / 64, cxm = (C + F.P - 1) / F.P;
-  if (C > 0xFFFFFF || 2 * cxm + 1 > FLOW_MAX_JCAP)
-    return fail(TG_E_INVAL, "flow mode: at most %d envs per XCD sub-problem", (FLOW_MAX_JCAP / 2 - 1) * 64);
+  if (C > FLOW_MAX_JCAP || 4 * cxm + 1 > FLOW_MAX_JCAP)
+    return fail(TG_E_INVAL, "flow mode: at most %d envs per XCD sub-problem", (FLOW_MAX_JCAP / 4 - 1) * 64);
   F.C = (int32_t)C;
-  F.seal_below = (int32_t)cxm;
-  F.lcap = 2 * cxm * 64;
-  F.jcap = 2 * cxm + 1;
-  F.qcap = (int64_t)FLOW_MAX_K * NLIST * F.jcap;  // run items: every list chunk of every step
+  F.seal_below = (int32_t)(3 * cxm);
+  F.lcap = 4 * cxm * 64;
+  F.jcap = 4 * cxm + 1;
+  // run items (every list chunk of every step) + chunks readied for a round (one per step at most)
+  F.qcap = (int64_t)FLOW_MAX_K * (NLIST * F.jcap + cxm);
   const size_t nctl = (size_t)F.P * CTL_WORDS, nq = (size_t)F.P * F.qcap,
                nfill = (size_t)F.P * FLOW_MAX_K * NLIST * F.jcap,
                nlist = (size_t)F.P * FLOW_MAX_K * NLIST * F.lcap;
@@ -1968,7 +1969,9 @@ int flow_init(tg_batch* h) {
          hipMemset(F.ctl[k], 0, sizeof(int32_t) * nctl) == hipSuccess &&
          hipMemset(F.q[k], 0xFF, sizeof(uint32_t) * nq) == hipSuccess &&
          hipMemset(F.fill[k], 0, sizeof(int32_t) * nfill) == hipSuccess;
-  ok = ok && hipMalloc((void**)&F.list, sizeof(int32_t) * nlist) == hipSuccess;
+  ok = ok && hipMalloc((void**)&F.list, sizeof(int32_t) * nlist) == hipSuccess &&
+       hipMalloc((void**)&F.outst, sizeof(int32_t) * (size_t)C) == hipSuccess &&
+       hipMalloc((void**)&F.cstep, sizeof(int32_t) * (size_t)h->n) == hipSuccess;
   if (!ok) {
     flow_free(h);
     return fail(TG_E_NOMEM, "flow work structures (%zu MB of lists)", nlist * 4 >> 20);
@@ -2005,7 +2008,7 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   }
   const int p = F.parity;
   F.parity ^= 1;
-  Flow f{F.ctl[p], F.q[p], F.fill[p], F.list, F.ctl[p ^ 1], F.q[p ^ 1], F.fill[p ^ 1],
+  Flow f{F.ctl[p], F.q[p], F.fill[p], F.list, F.outst, F.cstep, F.ctl[p ^ 1], F.q[p ^ 1], F.fill[p ^ 1],
          c.refill, c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
          F.qcap, F.jcap, F.lcap, F.seal_below, F.C, F.P, k, F.xmap, h->flow_skip, nullptr, nullptr, nullptr};
 #ifdef TG_FLOW_DBG
@@ -2034,7 +2037,7 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   HIP_TRY(hipGetLastError());
   ++F.launches;
   // every sub-problem's chunks finished (no XCD the census saw went without waves)
-  hipLaunchKernelGGL(k_flow_check, dim3(1), dim3(64), 0, st, F.ctl[p], F.P, F.C, h->n, h->err);
+  hipLaunchKernelGGL(k_flow_check, dim3(1), dim3(64), 0, st, F.ctl[p], F.P, F.C, h->err);
   HIP_TRY(hipGetLastError());
 #ifdef TG_FLOW_DBG
   if (const int rc = flow_diag_after(h, f, k, bpc, st)) return rc;

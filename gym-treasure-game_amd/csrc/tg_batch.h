@@ -133,6 +133,8 @@ struct tg_batch {
     uint32_t* q[2] = {nullptr, nullptr};
     int32_t* fill[2] = {nullptr, nullptr};
     int32_t* list = nullptr;
+    int32_t* outst = nullptr;
+    int32_t* cstep = nullptr;
     int parity = 0;
     int bpc[2][2] = {{0, 0}, {0, 0}};  // k_flow<AR, POL> workgroups per CU (occupancy API)
     int64_t launches = 0;

@@ -58,8 +58,8 @@ enum : int {
   FC_INIT = 0,  // step-0 classification: next chunk to deal out
   FC_QHEAD,     // run queue: tickets taken
   FC_QTAIL,     //   slots pushed
-  FC_FIN,       // envs done with step K - 1
-  FC_DONE,      // set when FC_FIN reaches the sub-problem's envs (or on a deadline)
+  FC_FIN,       // chunks done with the launch (every env past step K - 1)
+  FC_DONE,      // set when FC_FIN reaches the sub-problem's chunks (or on a deadline)
   FC_CLS,       // + t: envs classified for step t (listed at t, or finished t in place)
   FC_LTAIL = FC_CLS + FLOW_MAX_K,  // + t * NLIST + k: entries reserved in list (t, k)
   FC_N = FC_LTAIL + FLOW_MAX_K * NLIST
@@ -69,8 +69,10 @@ constexpr int CTL_WORDS = FC_N * FC_STRIDE;
 // per-wave LDS: the option loop's code window, or the classification's obs-row staging
 constexpr int FLOW_WAVE_BYTES = (WIN_WAVE_BYTES > 64 * 9 * 8 ? WIN_WAVE_BYTES : 64 * 9 * 8);
 static_assert(FLOW_WAVE_BYTES % 16 == 0, "16-B aligned windows for the LDS-DMA");
-// queue item: step (4 bits), list (4 bits), entries - 1 (6 bits), list chunk (18 bits)
-static_assert(FLOW_MAX_K <= 16 && NLIST < 16, "item fields");
+// queue item: step (4 bits), list (4 bits), entries - 1 (6 bits), list chunk (18 bits); or
+// (0, Q_CLASSIFY, 0, chunk): a chunk made ready for its next round
+constexpr int Q_CLASSIFY = 15;
+static_assert(FLOW_MAX_K <= 16 && NLIST < Q_CLASSIFY, "item fields");
 constexpr int FLOW_MAX_JCAP = 1 << 18;
 // the first-in-line wave seals a partial list chunk after waiting this long with nothing to run
 // (s_memrealtime ticks: 10 ns)
@@ -84,6 +86,8 @@ struct Flow {
   uint32_t* q;       // [P][qcap] run items (Q_EMPTY until pushed)
   int32_t* fill;     // [P][FLOW_MAX_K][NLIST][jcap] entries written per list chunk (zero)
   int32_t* list;     // [P][FLOW_MAX_K][NLIST][lcap] env indices
+  int32_t* outst;    // [C] envs of chunk c listed in its current round whose option has not run
+  int32_t* cstep;    // [N] the env's next step (written by its run item, or K by its round)
   // the other parity's control words, run queue and fill counters: the previous launch's,
   // zeroed here for the next one (grid-stride, at the start)
   int32_t* ctl_next;
@@ -206,14 +210,14 @@ __device__ __forceinline__ uint32_t xcc_id() {
 __global__ void k_census(uint32_t* mask) {
   if (threadIdx.x == 0) atomicOr(mask, 1u << (xcc_id() & 31u));
 }
-// after every k_flow launch, on its stream (one wave): a sub-problem whose envs did not all
-// finish step K - 1 sets TG_ERR_FLOW (no wave ran on its XCD; see "Coherence" above)
-__global__ void k_flow_check(const int32_t* __restrict__ ctl, int P, int32_t C, int64_t n,
+// after every k_flow launch, on its stream (one wave): a sub-problem whose chunks did not all
+// finish the launch sets TG_ERR_FLOW (no wave ran on its XCD; see "Coherence" above)
+__global__ void k_flow_check(const int32_t* __restrict__ ctl, int P, int32_t C,
                              uint32_t* __restrict__ err_or) {
   const int x = (int)threadIdx.x;
   if (x < P) {
-    const int32_t nx = flow_envs(C, P, n, x);
-    if (nx > 0 && ctl[(int64_t)x * CTL_WORDS + FC_FIN * FC_STRIDE] != nx) atomicOr(err_or, E_FLOW);
+    const int Cx = (C - x + P - 1) / P;
+    if (Cx > 0 && ctl[(int64_t)x * CTL_WORDS + FC_FIN * FC_STRIDE] != Cx) atomicOr(err_or, E_FLOW);
   }
 }
 #endif
@@ -304,163 +308,105 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                   io.t0 + t, io.tb + (uint32_t)t};
   };
 
-  // The wave's work loop: one unit per iteration, chosen by wave-uniform values only (each read
-  // back with readfirstlane, so the loop's branches stay scalar: with the work in nested loops
-  // whose exits the compiler did not prove uniform, round 5's bring-up saw a divergent loop
-  // nest).  A unit is a chunk of the step-0 deal (64 envs, coalesced loads, every lane at step
-  // 0) or a run item (64 entries of list (t, k): the option loops of step t); after either,
-  // each lane runs its own env ahead.
-  bool deal = true;
-  while (true) {
+  // one run item: chunk j of list (t, k), cnt entries, one lane per entry, as k_run: the option
+  // loops of step t, the rows and the state; each lane then records its env's next step
+  // (cstep) and decrements its env's chunk's `outst`; returns the lanes whose env's chunk became
+  // ready (its chunk in cl)
+  auto run = [&](uint32_t item, int& cl) -> unsigned long long {
+    const int t = (int)(item >> 28), k = (int)((item >> 24) & 15u), j = (int)(item & 0x3FFFFu);
+    // a cheap guard: an item or entry out of range is a protocol bug; it sets
+    // TG_ERR_FLOW and runs nothing instead of addressing memory with it
+    const bool item_ok = t < K && k < NLIST && (int64_t)j < f.jcap;
+    const int lidx = item_ok ? t * NLIST + k : 0;
+    FLOW_DIAG_TAIL(tail);
+    const int mcnt = item_ok ? (int)((item >> 18) & 63u) + 1 : 0;
+    bool live = lane < mcnt;
     int64_t i = 0;
-    bool live = false;
+    if (live) i = ld_sc1(list + (int64_t)lidx * f.lcap + 64 * j + lane);
+    const bool bad = live && (i < 0 || i >= n || (int)((i >> 6) % P) != x);
+    if (lane == 0 && (!item_ok || __ballot(bad))) atomicOr(err_or, E_FLOW);
+    live = live && !bad;
+    FLOW_DIAG_RUN(item, i, live, mcnt, tail, lidx, j);
+    const StepIO st = step_io(t);
+    StepResult r{0, 0, 0, 0};
+    Env e;
+    e.mti = 0u;
+    int2 ep = make_int2(0, 0);
+    uint32_t draws = 0;
+    int lregen = 0;
+    if (live) {
+      unpack(ld16_sc1(S.st4, (uint32_t)i * 16u), ld_ang_sc1(S.ang, i), e);
+      ep = ld_ep_sc1(S.ep, i);
+      RngCodesT<true> rng(S.mt + i * MT_STORE, S.mc + i * MT_CODES, e.mti, (lds_u8*)warea);
+      rng.prime();
+      if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
+      if (k != L_RESET) run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform
+      r.done = is_done(e);
+      finish_step<AR, false, false>(level_div(L), e, rng, i, r, ep, st);  // valid: at listing
+      e.mti = rng.finish();
+      draws = rng.draws;
+      lregen = (int)rng.regens;
+      if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+    }
+    if (AR) record_episodes(live && r.done, g0 + i, ep, st.tstep, eq, stats, slot);
+    if (live) {
+      st16_sc1(S.st4, (uint32_t)i * 16u, pack(e));
+      st16_sc1(S.ang, (uint32_t)i * 16u, d2u4(make_double2(e.ang0, e.ang1)));
+      st_ep_sc1(S.ep, i, ep);
+      st_sc1(f.cstep + i, t + 1);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    wave_stats(stats, 0, 0, r.ticks, (int)draws, AR ? (live && r.done) : 0,
+               __ballot(lregen != 0) ? wave_sum(lregen) : 0, true, slot);
+    // this wave's stores first, then the chunks' counters: the lane that takes its env's chunk
+    // to 0 hands the chunk to the wave (its next round below, in lane order)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (live) old = atomicSub(&f.outst[i >> 6], 1);
+    const unsigned long long ready = __ballot(live && old == 1);
+    if (lane == 0) FLOW_EV(7, item, (uint32_t)__popcll(ready), (uint32_t)mcnt, x);
+    cl = (int)(i >> 6);
+    return ready;
+  };
+
+  // One round of chunk c: every env of the chunk not yet done with step K - 1, one lane per env
+  // (coalesced loads), at its own next step (0 in the first round, the deal; later the step
+  // after the one its last option ran at, cstep).  Run-ahead (TG/:91-96 -> OP/:20-36: env i's
+  // step t + 1 depends on env i's step t alone): each lane classifies its env for its step t,
+  // t + 1, ... as k_classify would — the policy's action, can_run — and finishes every step
+  // whose option cannot run in place (reward None, state and MT stream untouched, OP/:22-23),
+  // until an option can run (the env is listed at (t', k)) or the launch's last step is past.
+  // The lanes advance in lockstep, so the rows of one step's lanes are adjacent.  The state is
+  // the same at every step of a run-ahead, so what depends on it alone is evaluated once: the 9
+  // options' can_run (available_mask, TG/:83-89), the obs row (get_state, TG/:94), done, and
+  // the policy's hash keyed by the env alone (policy_action's inner two rounds).  An env
+  // entering done with auto-reset on and no option to run goes on L_RESET (first round only: a
+  // run with auto-reset resets the env it finishes).  Returns the envs listed (0: the chunk is
+  // done with the launch).
+  auto round = [&](int c, bool first) -> int {
+    const int64_t i = (int64_t)c * 64 + lane;
+    bool live = i < n;
+    int t = 0;
+    if (live && !first) t = ld_sc1(f.cstep + i);
+    live = live && t < K;
     Env e;
     e.mti = 0u;
     e.ang0 = e.ang1 = 0.0;
     int2 ep = make_int2(0, 0);
-    int t = 0;  // (per lane) the first step the lane classifies below
-    if (deal) {
-      int j = 0;
-      if (lane == 0) j = atomicAdd(fcw(ctl, FC_INIT), 1);
-      j = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(j, 0));
-      if (j >= Cx) {
-        deal = false;
-        continue;
-      }
-      FLOW_DIAG_PATH(3);
-      FLOW_EV_WAVE(16, j, 0);  // (timing log: a deal chunk)
-      // chunk x + P j: the envs' first touch in this launch (the previous kernel's stores are
-      // visible: plain, coalesced loads)
-      i = (int64_t)(x + P * j) * 64 + lane;
-      live = i < n;
-      if (live) {
-        unpack(S.st4[i], S.ang[i], e);
-        ep = S.ep[i];
-      }
-    } else {
-      // a run item by ticket: wait for its slot (lane 0 polls, the wave reads its answer)
-      int h = 0;
-      if (lane == 0) h = atomicAdd(fcw(ctl, FC_QHEAD), 1);
-      h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(h, 0));
-      FLOW_DBG(2, h, x, 0);
-      if (lane == 0) FLOW_EV(8, h, x, 0, 0);
-      uint32_t item = Q_EMPTY;
-      int stop = 0;
-      unsigned long long t_wait = realtime();
-      while (!stop) {
-        uint32_t it = Q_EMPTY;
-        int dn = 0, head = 0;
-        if (lane == 0) {
-          if ((int64_t)h < f.qcap) it = ld_sc1(q + h);
-          if (it == Q_EMPTY) {
-            dn = ld_sc1(fcw(ctl, FC_DONE));
-            head = h == ld_sc1(fcw(ctl, FC_QTAIL));
-          }
-        }
-        item = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(it, 0));
-        dn = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(dn, 0));
-        head = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(head, 0));
-        if (item != Q_EMPTY || dn) {
-          stop = 1;
-        } else if (head && realtime() - t_wait > FLOW_SEAL_AFTER) {
-          // first in line and nothing to run: seal the fullest partial list chunk of the
-          // lowest steps not yet classified by every env (their envs are the laggards)
-          int open = 0;
-          if (lane < K) open = ld_sc1(fcw(ctl, FC_CLS + lane)) < nx;
-          const unsigned long long ob = __ballot(open);
-          if (ob) {
-            const int t_lo = __ffsll((long long)ob) - 1;
-            const int tc = t_lo + lane / NLIST, kc = lane % NLIST;
-            int r = -1;
-            if (lane < 4 * NLIST && tc < K) {
-              const int v = ld_sc1(fcw(ctl, FC_LTAIL + tc * NLIST + kc));
-              if ((v & 63) && (v >> 6) < f.seal_below) r = v & 63;
-            }
-            const int best = wave_max(r);
-            const unsigned long long bl = __ballot(r == best && best > 0);
-            if (bl && lane == __ffsll((long long)bl) - 1) seal(tc, kc, true);
-          }
-          t_wait = realtime();
-        } else if (realtime() - t_start > FLOW_DEADLINE) {
-          if (lane == 0) {
-            atomicOr(err_or, E_FLOW);
-            __hip_atomic_store(fcw(ctl, FC_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          stop = 1;
-        } else {
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      if (item == Q_EMPTY) break;
-      FLOW_DBG(3, h, item, x);
-      if (lane == 0) FLOW_EV(5, h, item, x, 0);
-      FLOW_DIAG_TAKE(item, h);
-      FLOW_DIAG_PATH(2);
-      // the run item: 64-entry chunk j of list (t, k), one lane per entry, as k_run.  A cheap
-      // guard: an item or entry out of range is a protocol bug; it sets
-      // TG_ERR_FLOW and runs nothing instead of addressing memory with it
-      const int tt = (int)(item >> 28), k = (int)((item >> 24) & 15u), j = (int)(item & 0x3FFFFu);
-      const bool item_ok = tt < K && k < NLIST && (int64_t)j < f.jcap;
-      const int lidx = item_ok ? tt * NLIST + k : 0;
-      FLOW_DIAG_TAIL(tail);
-      const int mcnt = item_ok ? (int)((item >> 18) & 63u) + 1 : 0;
-      live = lane < mcnt;
-      if (live) i = ld_sc1(list + (int64_t)lidx * f.lcap + 64 * j + lane);
-      FLOW_DIAG_RUN(item, i, live, mcnt, tail, lidx, j);
-      const bool bad = live && (i < 0 || i >= n || (int)((i >> 6) % P) != x);
-      if (lane == 0 && (!item_ok || __ballot(bad))) atomicOr(err_or, E_FLOW);
-      live = live && !bad;
-      const StepIO st = step_io(tt);
-      StepResult r{0, 0, 0, 0};
-      uint32_t draws = 0;
-      int lregen = 0;
-      if (live) {
-        unpack(ld16_sc1(S.st4, (uint32_t)i * 16u), ld_ang_sc1(S.ang, i), e);
-        ep = ld_ep_sc1(S.ep, i);
-        RngCodesT<true> rng(S.mt + i * MT_STORE, S.mc + i * MT_CODES, e.mti, (lds_u8*)warea);
-        rng.prime();
-        if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
-        if (k != L_RESET) run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform
-        r.done = is_done(e);
-        finish_step<AR, false, false>(level_div(L), e, rng, i, r, ep, st);  // valid: at listing
-        e.mti = rng.finish();
-        draws = rng.draws;
-        lregen = (int)rng.regens;
-      }
-      if (AR) record_episodes(live && r.done, g0 + i, ep, st.tstep, eq, stats, slot);
-      __builtin_amdgcn_s_setprio(0);
-      wave_stats(stats, 0, 0, r.ticks, (int)draws, AR ? (live && r.done) : 0,
-                 __ballot(lregen != 0) ? wave_sum(lregen) : 0, true, slot);
-      if (lane == 0) FLOW_EV(7, item, 0u, (uint32_t)mcnt, x);
-      t = tt + 1;
+    if (live) {
+      unpack(ld16_sc1(S.st4, (uint32_t)i * 16u), ld_ang_sc1(S.ang, i), e);
+      ep = ld_ep_sc1(S.ep, i);
     }
-    // A stale MT half the env left (in this run, or before the launch) goes on k_regen's list
-    // c % SHARDS of the env's 64-env chunk c, as k_classify's, once (MT_LISTED)
-    {
-      const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
-      if (stale) {
-        const int sh = (int)((i >> 6) % SHARDS);
-        const int at = atomicAdd(&f.rcnt[sh * CTR_STRIDE], 1);
-        f.refill[sh * f.rcap + at] = (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
-        e.mti |= MT_LISTED;
-      }
-    }
-    // Run-ahead (TG/:91-96 -> OP/:20-36: env i's step t + 1 depends on env i's step t alone):
-    // each lane classifies its own env for steps t, t + 1, ... as k_classify would — the
-    // policy's action, can_run — and finishes every step whose option cannot run in place
-    // (reward None, state and MT stream untouched: OP/:22-23), until an option can run (the env
-    // is listed at (tl, k)) or the launch's last step is past (tl = K).  An env entering done
-    // with auto-reset on and no option to run goes on L_RESET (only at the deal: a run with
-    // auto-reset resets the env it finishes).  The state is the same at every step of a run-
-    // ahead, so what depends on it alone is evaluated once, before the loop: the 9 options'
-    // can_run (available_mask, TG/:83-89: the same predicates can_run(k) evaluates), the obs row
-    // (get_state, TG/:94) and done; and the policy's hash keyed by the env alone (sm64 of the
-    // seed and the env, policy_action's inner two rounds).  A step is then one hash round, a
-    // bit test and the row stores.
+    const uint32_t f0 = e.f, mt0 = e.mti;
+    // a stale MT half not listed yet goes on k_regen's list c % SHARDS (MT_LISTED), as k_classify
+    const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
+    const unsigned long long sb = __ballot(stale);
+    int sbase = 0;
+    if (sb && lane == 0) sbase = atomicAdd(&f.rcnt[(c % SHARDS) * CTR_STRIDE], __popcll(sb));
+    if (stale) e.mti |= MT_LISTED;
     const int tf = t;  // the lane's first classified step
-    int kl = -1;
-    int nvalid = 0;
-    if (live && t < K) {
+    int kl = -1, nvalid = 0;
+    if (live) {
       const uint32_t avail = available_mask(L, m, e);
       const bool done0 = is_done(e);
       double orow[9];
@@ -497,62 +443,175 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       }
       if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
     }
+    FLOW_EV_WAVE(14, c, 0);  // (timing log: the run-ahead done)
     const int tl = t;  // the listing step, or K
     const bool listed = live && tl < K;
-    FLOW_EV_WAVE(14, 0, 0);  // (timing log: the run-ahead done)
-    // the entries: lanes grouped by list (tl, k), one reservation per group (issued together,
-    // their round trips overlapping the state stores), then the entry, the env's state (for its
-    // run item, or final), and publish: this wave's stores first; then the fill counts (the
-    // writer whose entries complete a list chunk pushes it), the steps passed (the wave that
-    // completes a step's count flushes its partial list chunks) and the finished envs
+    // the entries: lanes grouped by list (tl, k), one reservation per group (one atomic
+    // instruction of the groups' leads)
     const int key = listed ? tl * NLIST + kl : -1;
     int rank = 0, lead = 0, nb = 0, base = 0;
     {
       unsigned long long pend = __ballot(listed);
       while (pend) {
-        const int first = __ffsll((long long)pend) - 1;
-        const int k0 = __builtin_amdgcn_readlane(key, first);
+        const int first_l = __ffsll((long long)pend) - 1;
+        const int k0 = __builtin_amdgcn_readlane(key, first_l);
         const unsigned long long b = __ballot(key == k0);
         if (key == k0) {
           rank = __popcll(b & ((1ull << lane) - 1ull));
-          lead = first;
+          lead = first_l;
           nb = __popcll(b);
         }
         pend &= ~b;
       }
     }
-    // one atomic instruction: each group's lead reserves its group's places (an atomic per
-    // group inside the loop above waited for each return before the next group: ~35 dependent
-    // round trips per wave at the uniform policy)
     if (listed && lane == lead) base = atomicAdd(fcw(ctl, FC_LTAIL + key), nb);
-    if (live) {
-      st16_sc1(S.st4, (uint32_t)i * 16u, pack(e));
-      st16_sc1(S.ang, (uint32_t)i * 16u, d2u4(make_double2(e.ang0, e.ang1)));
-      st_ep_sc1(S.ep, i, ep);
-    }
+    const int cnt = __popcll(__ballot(listed));
+    // the handed-off bytes: refill entries, the state (when classification changed its flags:
+    // the env's run item loads it), the finished envs' next step (K), the list entries, the
+    // chunk's count; then publish: this wave's stores first; then the fill counts (the writer
+    // whose entries complete a list chunk pushes it), the steps classified (the wave that
+    // completes a step's count flushes its partial list chunks), a finished chunk
+    sbase = __builtin_amdgcn_readlane(sbase, 0);
+    if (stale)
+      f.refill[(c % SHARDS) * f.rcap + sbase + __popcll(sb & ((1ull << lane) - 1ull))] =
+          (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
+    if (live && (e.f != f0 || e.mti != mt0)) st16_sc1(S.st4, (uint32_t)i * 16u, pack(e));
+    if (live && !listed) st_sc1(f.cstep + i, K);
     const int gbase = __shfl(base, lead, 64);
     if (listed) st_sc1(list + (int64_t)key * f.lcap + gbase + rank, (int32_t)i);
+    if (cnt && lane == 0) st_sc1(f.outst + c, cnt);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (listed && lane == lead) {
       const int j0 = base >> 6, in0 = min(nb, 64 - (base & 63));
       fill_add(tl, kl, j0, in0);
       if (nb > in0) fill_add(tl, kl, j0 + 1, nb - in0);
     }
-    // steps passed: tf .. min(tl, K - 1) (the listing step's entry is written)
+    // steps classified: tf .. min(tl, K - 1) (the listing step's entry is written)
     const int thi = live ? min(tl, K - 1) : -1;
     const int s0 = __builtin_amdgcn_readfirstlane(wave_min_i(live && tf <= thi ? tf : K));
     const int s1 = __builtin_amdgcn_readfirstlane(wave_max(thi));
     for (int sp = s0; sp <= s1; ++sp) {
-      const int c = __popcll(__ballot(live && tf <= sp && sp <= thi));
+      const int cs = __popcll(__ballot(live && tf <= sp && sp <= thi));
       int last = 0;
-      if (c && lane == 0) last = atomicAdd(fcw(ctl, FC_CLS + sp), c) + c == nx;
+      if (cs && lane == 0) last = atomicAdd(fcw(ctl, FC_CLS + sp), cs) + cs == nx;
       if (__builtin_amdgcn_readlane(last, 0) && lane < NLIST) seal(sp, lane, false);  // step sp's partial chunks
     }
-    const int nfin = __popcll(__ballot(live && tl >= K));
-    if (nfin && lane == 0 && atomicAdd(fcw(ctl, FC_FIN), nfin) + nfin == nx)
-      __hip_atomic_store(fcw(ctl, FC_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     wave_stats(stats, live ? thi - tf + 1 : 0, nvalid, 0, 0, 0, 0, false, slot);
-    FLOW_EV_WAVE(15, 0, 0);  // (timing log: published)
+    FLOW_EV_WAVE(15, c, cnt);  // (timing log: published)
+    return cnt;
+  };
+
+  // The wave's work loop: one unit per iteration, chosen by wave-uniform values only (each read
+  // back with readfirstlane, so the loop's branches stay scalar: with the work in nested loops
+  // whose exits the compiler did not prove uniform, round 5's bring-up saw a divergent loop
+  // nest).  In order: the first rounds of the chunks, dealt out by a counter; then the queue:
+  // run items, and the chunks other waves' run items made ready (a run item's envs come from up
+  // to 64 chunks; the first it readies runs its next round in this wave, the others go on the
+  // queue for any wave).  A chunk whose round lists no env is done with the launch.
+  bool deal = true;
+  int cl = 0;  // (per lane) the chunk of the lane's env in the last run item
+  while (true) {
+    int c;
+    bool first = false;
+    if (deal) {
+      int j = 0;
+      if (lane == 0) j = atomicAdd(fcw(ctl, FC_INIT), 1);
+      j = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(j, 0));
+      if (j >= Cx) {
+        deal = false;
+        continue;
+      }
+      FLOW_DIAG_PATH(3);
+      FLOW_EV_WAVE(16, j, 0);  // (timing log: a deal chunk)
+      c = x + P * j;
+      first = true;
+    } else {
+      // an item by ticket: wait for its slot (lane 0 polls, the wave reads its answer)
+      int h = 0;
+      if (lane == 0) h = atomicAdd(fcw(ctl, FC_QHEAD), 1);
+      h = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(h, 0));
+      FLOW_DBG(2, h, x, 0);
+      if (lane == 0) FLOW_EV(8, h, x, 0, 0);
+      uint32_t item = Q_EMPTY;
+      int stop = 0;
+      unsigned long long t_wait = realtime();
+      while (!stop) {
+        uint32_t it = Q_EMPTY;
+        int dn = 0, head = 0;
+        if (lane == 0) {
+          if ((int64_t)h < f.qcap) it = ld_sc1(q + h);
+          if (it == Q_EMPTY) {
+            dn = ld_sc1(fcw(ctl, FC_DONE));
+            head = h == ld_sc1(fcw(ctl, FC_QTAIL));
+          }
+        }
+        item = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(it, 0));
+        dn = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(dn, 0));
+        head = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(head, 0));
+        if (item != Q_EMPTY || dn) {
+          stop = 1;
+        } else if (head && realtime() - t_wait > FLOW_SEAL_AFTER) {
+          // first in line and nothing to run: seal the partial list chunk of the lowest step
+          // (the fullest of that step's lists).  Besides latency this is what keeps a launch
+          // live: an env listed at a far step waits for that step's flush, which waits for a
+          // chunk-mate's next round, which waits for the far env's run (tests/native/flow_sim)
+          int best = -1, bt = K, bk = 0;
+          for (int t0 = 0; t0 < K && best < 0; t0 += 64 / NLIST) {
+            const int tc = t0 + lane / NLIST, kc = lane % NLIST;
+            int r = -1;
+            if (lane < (64 / NLIST) * NLIST && tc < K) {
+              const int v = ld_sc1(fcw(ctl, FC_LTAIL + tc * NLIST + kc));
+              if ((v & 63) && (v >> 6) < f.seal_below) r = ((K - tc) << 6) | (v & 63);
+            }
+            best = wave_max(r);
+            if (best >= 0) {
+              const unsigned long long bl = __ballot(r == best);
+              const int bl0 = __ffsll((long long)bl) - 1;
+              bt = __builtin_amdgcn_readlane(tc, bl0);
+              bk = __builtin_amdgcn_readlane(kc, bl0);
+            }
+          }
+          if (best >= 0 && lane == 0) seal(bt, bk, true);
+          t_wait = realtime();
+        } else if (realtime() - t_start > FLOW_DEADLINE) {
+          if (lane == 0) {
+            atomicOr(err_or, E_FLOW);
+            __hip_atomic_store(fcw(ctl, FC_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          stop = 1;
+        } else {
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      if (item == Q_EMPTY) break;
+      FLOW_DBG(3, h, item, x);
+      if (lane == 0) FLOW_EV(5, h, item, x, 0);
+      FLOW_DIAG_TAKE(item, h);
+      FLOW_DIAG_PATH(2);
+      if (((item >> 24) & 15u) == Q_CLASSIFY) {  // a chunk another wave's run item made ready
+        c = (int)(item & 0x3FFFFu);
+        if (c >= f.C || c % P != x) {  // (the run item's guard, for these items)
+          if (lane == 0) atomicOr(err_or, E_FLOW);
+          continue;
+        }
+      } else {
+        const unsigned long long rd = run(item, cl);
+        // (readfirstlane returns int: each half is cast back to 32 bits before it widens, or
+        // lane 31's bit sign-extends over lanes 32-63)
+        const unsigned long long ready =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rd >> 32)) << 32) |
+            (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rd);
+        if (!ready) continue;
+        // the first readied chunk's next round runs here, the others by whichever waves take them
+        const int l0 = __ffsll((long long)ready) - 1;
+        c = __builtin_amdgcn_readlane(cl, l0);
+        if (((ready >> lane) & 1ull) && lane != l0) push(0, Q_CLASSIFY, cl, 1);
+      }
+    }
+    FLOW_DIAG_CLASSIFY(c, 0);
+    if (__builtin_amdgcn_readfirstlane(round(c, first)) == 0 && lane == 0 &&
+        atomicAdd(fcw(ctl, FC_FIN), 1) + 1 == Cx)  // the chunk is done with the launch
+      __hip_atomic_store(fcw(ctl, FC_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   FLOW_DBG(9, 0, 0, 0);
   if (lane == 0) FLOW_EV(9, x, 0, 0, 0);

@@ -70,7 +70,7 @@ constexpr uint32_t FLOW_EVW = 1024;
 // a second push of one list chunk (slot 4093)
 #define FLOW_DIAG_PUSH(t, k, j)                                                                   \
   do {                                                                                           \
-    if (f.dbgc) {                                                                                \
+    if (f.dbgc && (k) != Q_CLASSIFY) {                                                           \
       const int64_t base2_ = (int64_t)f.C * 16 + (int64_t)f.P * FLOW_MAX_K * NLIST * f.jcap;      \
       const uint32_t o_ = atomicAdd(&f.dbgc[base2_ + ((int64_t)x * FLOW_MAX_K * NLIST + (t) * NLIST + (k)) * f.jcap + (j)], 1u); \
       if (o_ && atomicCAS(f.dbg + 4093 * 4, 0u, 97u) == 0u) {                                    \
@@ -110,7 +110,7 @@ constexpr uint32_t FLOW_EVW = 1024;
 #define FLOW_DIAG_TAKE(item, h)                                                                   \
   do {                                                                                           \
     item_ = (item);                                                                              \
-    if (lane == 0 && f.dbgc) {                                                                   \
+    if (lane == 0 && f.dbgc && (((item) >> 24) & 15u) != Q_CLASSIFY) {                           \
       const int it_l_ = (int)(((item) >> 28) * NLIST + (((item) >> 24) & 15u));                  \
       const uint32_t o_ = atomicAdd(&f.dbgc[(int64_t)f.C * 16 + ((int64_t)x * FLOW_MAX_K * NLIST + it_l_) * f.jcap + ((item) & 0x3FFFFu)], 1u); \
       if (o_ && atomicCAS(f.dbg + 4094 * 4, 0u, 98u) == 0u) {                                    \

@@ -1,14 +1,15 @@
-// CPU model of k_flow's work protocol (gym-treasure-game_amd/csrc/tg_flow.h, the run-ahead form
-// of round 6), threads for waves and seq_cst atomics for the device's: the step-0 deal of 64-env
-// chunks, each env run ahead by its lane (classified step after step, finished in place while
-// its option cannot run) until it is listed at (t', k) or done with step K - 1; (step, option)
-// lists filled per 64-entry chunk and pushed by the writer that completes one; per-step counts of
-// classified envs, the wave that completes a step's count flushing its partial chunks; run items
-// by ticket, each env run ahead again after its option; a waiting wave first in line seals the
-// fullest partial chunk of the lowest open steps (the tail moved past it by CAS, the chunk pushed
-// with its entries by whoever completes its fill word).  Checks: every env-step classified
-// exactly once, every env run exactly once per step it runs in, fill counts equal to the entries
-// run, termination.  Test infrastructure (tests/test_flow_protocol.py), not the product.
+// CPU model of k_flow's work protocol (gym-treasure-game_amd/csrc/tg_flow.h, round 6's chunk
+// rounds), threads for waves and seq_cst atomics for the device's: rounds of 64-env chunks (the
+// first dealt out by a counter), in which each env not yet past step K - 1 runs ahead from its
+// own next step, finished in place while its option cannot run, until it is listed at (t', k);
+// (step, option) lists filled per 64-entry chunk and pushed by the writer that completes one;
+// per-step counts of classified envs, the wave that completes a step's count sealing its
+// partial chunks; run items by ticket, each env's next step recorded and its chunk's
+// outstanding count decremented, the chunks a run item readies given their next round (the
+// first by its wave, the rest pushed as classify items); a waiting wave first in line seals the
+// fullest partial chunk of the lowest open steps.  Checks: every env-step classified exactly
+// once, every env run exactly once per step it runs in, fill counts equal to the entries run,
+// termination.  Test infrastructure (tests/test_flow_protocol.py), not the product.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -28,7 +29,8 @@ struct Sub {
   std::vector<std::atomic<unsigned>> q;
 };
 int N, C, P, K, jcap, lcap, qcap, seal_below;
-std::vector<std::atomic<int>> ccount, rcount;
+constexpr int QCLS = 15;
+std::vector<std::atomic<int>> ccount, rcount, outst, cstep;
 std::atomic<int> errors{0};
 std::vector<Sub*> subs;
 
@@ -69,10 +71,18 @@ void wave(int x, int seed, int runpct) {
     const int r = v & 63;
     fill_add(t, k, v >> 6, (64 - r) + (r << 8));
   };
-  // the lanes' run-ahead and the wave's publishing (k_flow after a deal or a run item)
-  auto ahead = [&](const std::vector<int>& envs, const std::vector<int>& from) {
+  // a round of chunk c (k_flow round): returns the envs listed
+  auto round = [&](int c, bool first) -> int {
+    std::vector<int> envs, from;
+    for (int l = 0; l < 64; ++l) {
+      const int i = c * 64 + l;
+      if (i >= N) continue;
+      const int t = first ? 0 : cstep[i].load();
+      if (t < K) { envs.push_back(i); from.push_back(t); }
+    }
     const int m = (int)envs.size();
     std::vector<int> tl(m), kl(m, -1), pos(m);
+    int cnt = 0;
     for (int l = 0; l < m; ++l) {
       int t = from[l];
       for (; t < K; ++t) {
@@ -82,6 +92,7 @@ void wave(int x, int seed, int runpct) {
         if ((kl[l] = opt_of(envs[l], t, runpct)) >= 0) break;
       }
       tl[l] = t;
+      cnt += t < K;
     }
     for (int l = 0; l < m; ++l)  // reserve, write the entry ...
       if (tl[l] < K) {
@@ -89,33 +100,31 @@ void wave(int x, int seed, int runpct) {
         pos[l] = S->ltail[lidx].fetch_add(1);
         if (pos[l] >= lcap) { errors++; fprintf(stderr, "lcap\n"); tl[l] = K; continue; }
         S->list[(size_t)lidx * lcap + pos[l]].store(envs[l]);
+      } else {
+        cstep[envs[l]].store(K);
       }
+    if (cnt) outst[c].store(cnt);
     if (rng() % 8 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 100));
     for (int l = 0; l < m; ++l)  // ... then the fill counts (the completing writer pushes)
-      if (tl[l] < K) {
-        fill_add(tl[l], kl[l], pos[l] >> 6, 1);
-      }
-    for (int sp = 0; sp < K; ++sp) {  // steps passed: from .. min(tl, K - 1)
-      int c = 0;
-      for (int l = 0; l < m; ++l) c += from[l] <= sp && sp <= std::min(tl[l], K - 1);
-      if (c && S->cls[sp].fetch_add(c) + c == nx)
+      if (tl[l] < K) fill_add(tl[l], kl[l], pos[l] >> 6, 1);
+    for (int sp = 0; sp < K; ++sp) {  // steps classified: from .. min(tl, K - 1)
+      int cs = 0;
+      for (int l = 0; l < m; ++l) cs += from[l] <= sp && sp <= std::min(tl[l], K - 1);
+      if (cs && S->cls[sp].fetch_add(cs) + cs == nx)
         for (int k = 0; k < NLIST; ++k) seal(sp, k, false);  // the step's partial chunks
     }
-    int nfin = 0;
-    for (int l = 0; l < m; ++l) nfin += tl[l] >= K;
-    if (nfin && S->fin.fetch_add(nfin) + nfin == nx) S->done.store(1);
+    return cnt;
   };
   bool deal = true;
   const auto t_start = std::chrono::steady_clock::now();
   while (true) {
-    std::vector<int> envs, from;
+    int c;
+    bool first = false;
     if (deal) {
       const int j = S->init.fetch_add(1);
       if (j >= Cx) { deal = false; continue; }
-      for (int l = 0; l < 64; ++l) {
-        const int i = (x + P * j) * 64 + l;
-        if (i < N) { envs.push_back(i); from.push_back(0); }
-      }
+      c = x + P * j;
+      first = true;
     } else {
       const int h = S->qhead.fetch_add(1);
       unsigned item = EMPTY;
@@ -124,10 +133,8 @@ void wave(int x, int seed, int runpct) {
         if (h < qcap) item = S->q[h].load();
         if (item != EMPTY || S->done.load()) break;
         if (h == S->qtail.load() && ++polls % 64 == 0) {  // first in line, idle: seal
-          int t_lo = 0;
-          while (t_lo < K && S->cls[t_lo].load() >= nx) ++t_lo;
-          int best = 0, bt = -1, bk = -1;
-          for (int tc = t_lo; tc < std::min(K, t_lo + 4); ++tc)
+          int best = 0, bt = -1, bk = -1;  // the lowest step's fullest partial chunk
+          for (int tc = 0; tc < K && bt < 0; ++tc)
             for (int kc = 0; kc < NLIST; ++kc) {
               const int v = S->ltail[tc * NLIST + kc].load();
               if ((v & 63) > best && (v >> 6) < seal_below) { best = v & 63; bt = tc; bk = kc; }
@@ -141,20 +148,30 @@ void wave(int x, int seed, int runpct) {
       }
       if (item == EMPTY) break;
       const int t = (int)(item >> 28), k = (int)((item >> 24) & 15u), j = (int)(item & 0x3FFFFu);
-      const int lidx = t * NLIST + k;
-      const int m = (int)((item >> 18) & 63u) + 1;
-      const int fv = S->fill[(size_t)lidx * jcap + j].load();
-      if ((fv & 0xFF) != 64 || ((fv >> 8) ? (fv >> 8) : 64) != m) { errors++; fprintf(stderr, "fill mismatch\n"); }
-      for (int l = 0; l < m; ++l) envs.push_back(S->list[(size_t)lidx * lcap + 64 * j + l].load());
-      if (rng() % 4 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 200));
-      for (int i : envs) {
-        if (i < 0 || i >= N || (i >> 6) % P != x) { errors++; fprintf(stderr, "bad entry\n"); return; }
-        if (rcount[(size_t)i * K + t].fetch_add(1) != 0) { errors++; fprintf(stderr, "dup run\n"); }
-        if (opt_of(i, t, runpct) != k) { errors++; fprintf(stderr, "wrong list\n"); }
-        from.push_back(t + 1);
+      if (k == QCLS) {
+        c = j;
+      } else {
+        const int lidx = t * NLIST + k;
+        const int m = (int)((item >> 18) & 63u) + 1;
+        const int fv = S->fill[(size_t)lidx * jcap + j].load();
+        if ((fv & 0xFF) != 64 || ((fv >> 8) ? (fv >> 8) : 64) != m) { errors++; fprintf(stderr, "fill mismatch\n"); }
+        std::vector<int> envs;
+        for (int l = 0; l < m; ++l) envs.push_back(S->list[(size_t)lidx * lcap + 64 * j + l].load());
+        if (rng() % 4 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 200));
+        std::vector<int> ready;
+        for (int i : envs) {
+          if (i < 0 || i >= N || (i >> 6) % P != x) { errors++; fprintf(stderr, "bad entry\n"); return; }
+          if (rcount[(size_t)i * K + t].fetch_add(1) != 0) { errors++; fprintf(stderr, "dup run\n"); }
+          if (opt_of(i, t, runpct) != k) { errors++; fprintf(stderr, "wrong list\n"); }
+          cstep[i].store(t + 1);
+          if (outst[i >> 6].fetch_sub(1) == 1) ready.push_back(i >> 6);
+        }
+        if (ready.empty()) continue;
+        c = ready[0];
+        for (size_t r = 1; r < ready.size(); ++r) push(0, QCLS, ready[r], 1);
       }
     }
-    ahead(envs, from);
+    if (round(c, first) == 0 && S->fin.fetch_add(1) + 1 == Cx) S->done.store(1);
   }
 }
 
@@ -166,9 +183,11 @@ int main(int argc, char** argv) {
   const int runpct = argc > 5 ? atoi(argv[5]) : 21;  // env-steps that run an option (%)
   C = (N + 63) / 64;
   const int cxm = (C + P - 1) / P;
-  seal_below = cxm; lcap = 2 * cxm * 64; jcap = 2 * cxm + 1; qcap = KMAX * NLIST * jcap;  // flow_init
+  seal_below = 3 * cxm; lcap = 4 * cxm * 64; jcap = 4 * cxm + 1; qcap = KMAX * (NLIST * jcap + cxm);  // flow_init
   ccount = std::vector<std::atomic<int>>((size_t)N * K);
   rcount = std::vector<std::atomic<int>>((size_t)N * K);
+  outst = std::vector<std::atomic<int>>(C);
+  cstep = std::vector<std::atomic<int>>(N);
   for (int x = 0; x < P; ++x) {
     Sub* s = new Sub();
     for (auto& a : s->cls) a = 0;
