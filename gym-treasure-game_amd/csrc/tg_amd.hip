@@ -1917,7 +1917,7 @@ int regen_all(tg_batch* h, hipStream_t st) {
 // ---- TG_MODE_FLOW (tg_flow.h) ----------------------------------------------------------------
 void flow_free(tg_batch* h) {
   auto& F = h->fl;
-  void* bufs[] = {F.ctl[0], F.ctl[1], F.q[0], F.q[1], F.fill[0], F.fill[1], F.list, F.outst, F.cstep};
+  void* bufs[] = {F.ctl[0], F.ctl[1], F.q[0], F.q[1], F.fill[0], F.fill[1], F.list, F.outst};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   F = {};
@@ -1945,19 +1945,12 @@ int flow_init(tg_batch* h) {
     if ((mask >> id) & 1u) F.xmap = (F.xmap & ~(0xFu << (4 * id))) | ((uint32_t)F.P++ << (4 * id));
   if (F.P == 0) return fail(TG_E_HIP, "flow census: no XCC id in 0..7");
   if (h->flow_debug) fprintf(stderr, "[flow] census mask %08x P %d\n", mask, F.P);
-  // 64-env chunks, sub-problem x holding chunks x, x + P, ... (at most cxm): per step and
-  // sub-problem at most cxm * 64 entries per list; idle seals (tg_flow.h) skip the rest of a
-  // chunk only below list chunk cxm, so a list's places stay below 2 cxm * 64 and its chunks
-  // below 2 cxm + 1
   const int64_t C = (h->n + 63) / 64, cxm = (C + F.P - 1) / F.P;
-  if (C > FLOW_MAX_JCAP || 4 * cxm + 1 > FLOW_MAX_JCAP)
-    return fail(TG_E_INVAL, "flow mode: at most %d envs per XCD sub-problem", (FLOW_MAX_JCAP / 4 - 1) * 64);
+  if (C > 0xFFFFFF) return fail(TG_E_INVAL, "flow mode: at most 2^24 chunks of 64 envs");
   F.C = (int32_t)C;
-  F.seal_below = (int32_t)(3 * cxm);
-  F.lcap = 4 * cxm * 64;
-  F.jcap = 4 * cxm + 1;
-  // run items (every list chunk of every step) + chunks readied for a round (one per step at most)
-  F.qcap = (int64_t)FLOW_MAX_K * (NLIST * F.jcap + cxm);
+  F.lcap = cxm * 64;
+  F.jcap = cxm + 1;
+  F.qcap = (int64_t)FLOW_MAX_K * (2 * cxm + NLIST);  // run items + chunks to classify, per step
   const size_t nctl = (size_t)F.P * CTL_WORDS, nq = (size_t)F.P * F.qcap,
                nfill = (size_t)F.P * FLOW_MAX_K * NLIST * F.jcap,
                nlist = (size_t)F.P * FLOW_MAX_K * NLIST * F.lcap;
@@ -1970,8 +1963,7 @@ int flow_init(tg_batch* h) {
          hipMemset(F.q[k], 0xFF, sizeof(uint32_t) * nq) == hipSuccess &&
          hipMemset(F.fill[k], 0, sizeof(int32_t) * nfill) == hipSuccess;
   ok = ok && hipMalloc((void**)&F.list, sizeof(int32_t) * nlist) == hipSuccess &&
-       hipMalloc((void**)&F.outst, sizeof(int32_t) * (size_t)C) == hipSuccess &&
-       hipMalloc((void**)&F.cstep, sizeof(int32_t) * (size_t)h->n) == hipSuccess;
+       hipMalloc((void**)&F.outst, sizeof(int32_t) * (size_t)C) == hipSuccess;
   if (!ok) {
     flow_free(h);
     return fail(TG_E_NOMEM, "flow work structures (%zu MB of lists)", nlist * 4 >> 20);
@@ -2008,9 +2000,9 @@ int launch_flow(tg_batch* h, int k, const FlowIO& io, bool ar, int pol, hipStrea
   }
   const int p = F.parity;
   F.parity ^= 1;
-  Flow f{F.ctl[p], F.q[p], F.fill[p], F.list, F.outst, F.cstep, F.ctl[p ^ 1], F.q[p ^ 1], F.fill[p ^ 1],
+  Flow f{F.ctl[p], F.q[p], F.fill[p], F.list, F.outst, F.ctl[p ^ 1], F.q[p ^ 1], F.fill[p ^ 1],
          c.refill, c.regen_ctr + (c.regen_parity * RCTR_N + RCTR_LIST) * CTR_STRIDE, c.rcap,
-         F.qcap, F.jcap, F.lcap, F.seal_below, F.C, F.P, k, F.xmap, h->flow_skip, nullptr, nullptr, nullptr};
+         F.qcap, F.jcap, F.lcap, F.C, F.P, k, F.xmap, h->flow_skip, nullptr, nullptr, nullptr};
 #ifdef TG_FLOW_DBG
   if (const int rc = flow_diag_setup(h, f)) return rc;
 #endif

@@ -128,13 +128,11 @@ struct tg_batch {
     uint32_t xmap = 0;        // XCC id -> sub-problem (nibbles)
     int32_t C = 0;            // 64-env chunks
     int64_t qcap = 0, jcap = 0, lcap = 0;
-    int32_t seal_below = 0;
     int32_t* ctl[2] = {nullptr, nullptr};  // two parities: a launch zeroes the other's
     uint32_t* q[2] = {nullptr, nullptr};
     int32_t* fill[2] = {nullptr, nullptr};
     int32_t* list = nullptr;
     int32_t* outst = nullptr;
-    int32_t* cstep = nullptr;
     int parity = 0;
     int bpc[2][2] = {{0, 0}, {0, 0}};  // k_flow<AR, POL> workgroups per CU (occupancy API)
     int64_t launches = 0;

@@ -1,33 +1,30 @@
-// tg_flow.h — k_flow: tg_rollout's K steps in ONE launch, each env advancing to its next step
-// as soon as its own option is done (TG_MODE_FLOW, §8f row 3).  Included by tg_amd.hip inside
-// its anonymous namespace, after the per-step kernels whose pieces it reuses (RngCodesT,
-// finish_step, record_episodes, wave_stats).
+// tg_flow.h — k_flow: tg_rollout's K steps in ONE launch, each 64-env chunk advancing to its
+// next step as soon as its own envs have finished the current one (TG_MODE_FLOW, §8f row 3).
+// Included by tg_amd.hip inside its anonymous namespace, after the per-step kernels whose
+// pieces it reuses (RngCodesT, finish_step, store_obs_wave, record_episodes, wave_stats).
 //
 // Why: the reference's step is per env (TG/:91-96 -> OP/:20-36): env i's step
 // t + 1 depends on env i's step t only.  The per-step kernels put a batch-wide barrier after
 // every step, so a step costs one maximal option chain (k_run ends with its slowest option
-// waves, ~50 us at the uniform policy, while only ~3.4 waves per SIMD carry work).  Round 5's
-// form handed steps on per 64-env chunk: a chunk was classified for t + 1 when all its envs
-// were done with t, so each chunk still waited, every step, for the slowest option among its
-// envs (chunks of 128 and 256 envs measured slower still, profiles/r06/r06c_*).  Here the hand-
-// off is per env: the lane that finishes env i's option at step t keeps the env in registers
-// and classifies it itself for t + 1, t + 2, ... ("run-ahead"), finishing in place every step
-// whose option cannot run (~79 % at the uniform policy: reward None, state and MT stream
-// untouched, OP/:22-23), until an option can run; only then is the env listed.
+// waves, ~50 us at the uniform policy, while only ~3.4 waves per SIMD carry work).  Here a chunk
+// whose envs are all done with step t is classified for step t + 1 at once, by the wave that
+// finished its last env, so chains of different steps overlap and the SIMDs stay busy.
 //
-// Work, per sub-problem (one per XCD, below; the envs of 64-env chunks x, x + P, ...):
-//   deal: chunk x + P j, dealt out by a counter: one lane per env (coalesced loads), each lane
-//     runs its env ahead from step 0.
+// Work, per sub-problem (one per XCD, below):
+//   classify (c, t): chunk c (envs 64c .. 64c + 63) at step t, one lane per env, as k_classify:
+//     the policy's action, can_run, the rows of the envs whose option cannot run (coalesced,
+//     through LDS), the stale-MT-half listing for k_regen; the rest are appended to the list
+//     (t, k) of their option k (L_RESET: entering done with auto-reset on), and the chunk's
+//     `outst` counter is set to their number.
 //   run (t, k, j): 64-entry chunk j of list (t, k), one lane per entry, as k_run: the option
-//     loop, the rows of step t; then each lane runs its env ahead from t + 1.
-//   run-ahead ends with the env listed at (t', k') — its entry appended to the list, its state
-//     stored for its run item — or with the env done with step K - 1.
-//   A list chunk is pushed on the sub-problem's run queue by the writer whose entry completes it
-//   (64 entries, counted per chunk in `fill`); the partial last chunk of every list of step t
-//   by the wave that completes step t's count of classified envs (FC_CLS + t: every env listed
-//   at t or finished t in place).  Waves take run items by ticket (one atomic on the queue head)
-//   and wait on their ticket's slot; the deal goes first.  A sub-problem is done when all its
-//   envs have finished step K - 1; waves holding tickets past the last item then leave.
+//     loop, the rows, the state; each lane then decrements its env's chunk's `outst`, and the
+//     lane that takes it to 0 hands the chunk to its wave, which classifies it for t + 1.
+//   A list chunk is pushed on the sub-problem's run queue by the writer whose entries complete
+//   it (64 entries, counted per chunk in `fill`); the partial last chunk of every list of step t
+//   by the wave that classifies step t's last chunk.  Waves take run items by ticket (one
+//   atomic on the queue head) and wait on their ticket's slot; the chunks' step-0 classification
+//   is dealt out first by a counter.  A sub-problem is done when all its chunks have finished
+//   step K - 1; waves holding tickets past the last item then leave.
 //
 // Coherence (MI355X_MICROARCH.md, inter-workgroup visibility): each XCD has its own L2, not
 // coherent with the others, and a CU's L1 is not refreshed by other CUs' stores.  So the batch
@@ -51,6 +48,7 @@
 constexpr int FLOW_MAX_K = REGEN_STEPS;  // steps per launch (the MT slack: k_regen every 16)
 constexpr int FLOW_MAX_PARTS = 8;        // sub-problems: one per XCD
 constexpr uint32_t Q_EMPTY = 0xFFFFFFFFu;
+constexpr int Q_CLASSIFY = 15;  // the list field of a queue item that is a chunk to classify
 constexpr unsigned long long FLOW_DEADLINE = 400000000ull;  // 4 s of s_memrealtime
 constexpr uint32_t E_FLOW = 1u << 30;    // TG_ERR_FLOW: a k_flow wait ran past FLOW_DEADLINE (a bug)
 // a sub-problem's control words, each on a 128-B line of its own
@@ -58,9 +56,9 @@ enum : int {
   FC_INIT = 0,  // step-0 classification: next chunk to deal out
   FC_QHEAD,     // run queue: tickets taken
   FC_QTAIL,     //   slots pushed
-  FC_FIN,       // chunks done with the launch (every env past step K - 1)
+  FC_FIN,       // chunks done with step K - 1
   FC_DONE,      // set when FC_FIN reaches the sub-problem's chunks (or on a deadline)
-  FC_CLS,       // + t: envs classified for step t (listed at t, or finished t in place)
+  FC_CLS,       // + t: chunks classified for step t
   FC_LTAIL = FC_CLS + FLOW_MAX_K,  // + t * NLIST + k: entries reserved in list (t, k)
   FC_N = FC_LTAIL + FLOW_MAX_K * NLIST
 };
@@ -69,25 +67,15 @@ constexpr int CTL_WORDS = FC_N * FC_STRIDE;
 // per-wave LDS: the option loop's code window, or the classification's obs-row staging
 constexpr int FLOW_WAVE_BYTES = (WIN_WAVE_BYTES > 64 * 9 * 8 ? WIN_WAVE_BYTES : 64 * 9 * 8);
 static_assert(FLOW_WAVE_BYTES % 16 == 0, "16-B aligned windows for the LDS-DMA");
-// queue item: step (4 bits), list (4 bits), entries - 1 (6 bits), list chunk (18 bits); or
-// (0, Q_CLASSIFY, 0, chunk): a chunk made ready for its next round
-constexpr int Q_CLASSIFY = 15;
+// queue item: step (4 bits), list (4 bits), list chunk (24 bits); or step, Q_CLASSIFY, chunk
 static_assert(FLOW_MAX_K <= 16 && NLIST < Q_CLASSIFY, "item fields");
-constexpr int FLOW_MAX_JCAP = 1 << 18;
-// the first-in-line wave seals a partial list chunk after waiting this long with nothing to run
-// (s_memrealtime ticks: 10 ns)
-#ifndef TG_FLOW_SEAL_AFTER
-#define TG_FLOW_SEAL_AFTER 200
-#endif
-constexpr unsigned long long FLOW_SEAL_AFTER = TG_FLOW_SEAL_AFTER;
 
 struct Flow {
   int32_t* ctl;      // [P][CTL_WORDS] this launch's control words (zero at launch)
   uint32_t* q;       // [P][qcap] run items (Q_EMPTY until pushed)
   int32_t* fill;     // [P][FLOW_MAX_K][NLIST][jcap] entries written per list chunk (zero)
   int32_t* list;     // [P][FLOW_MAX_K][NLIST][lcap] env indices
-  int32_t* outst;    // [C] envs of chunk c listed in its current round whose option has not run
-  int32_t* cstep;    // [N] the env's next step (written by its run item, or K by its round)
+  int32_t* outst;    // [C] envs of chunk c whose option is still running this step
   // the other parity's control words, run queue and fill counters: the previous launch's,
   // zeroed here for the next one (grid-stride, at the start)
   int32_t* ctl_next;
@@ -96,7 +84,6 @@ struct Flow {
   uint32_t* refill;  // k_regen's lists (list c % SHARDS, as k_classify's shards)
   int32_t* rcnt;
   int64_t rcap, qcap, jcap, lcap;
-  int32_t seal_below;  // idle seals only below this list chunk (cxm: later entries still fit)
   int32_t C, P, K;   // chunks, sub-problems, steps
   uint32_t xmap;     // nibble x: the sub-problem of XCC id x (0xF: none)
   int32_t skip;      // test hook (TG_FLOW_SKIP_PART): this sub-problem's waves leave at once, as
@@ -119,17 +106,6 @@ struct FlowIO {
 };
 
 __device__ __forceinline__ int32_t* fcw(int32_t* ctl, int w) { return ctl + w * FC_STRIDE; }
-// the envs of sub-problem x: those of its 64-env chunks x, x + P, ... below C (the last chunk of
-// the batch may be partial)
-__host__ __device__ __forceinline__ int32_t flow_envs(int32_t C, int P, int64_t n, int x) {
-  const int32_t Cx = (C - x + P - 1) / P;
-  return Cx <= 0 ? 0 : Cx * 64 - ((C - 1) % P == x ? (int32_t)((int64_t)C * 64 - n) : 0);
-}
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return v;
-}
 __device__ __forceinline__ int32_t ld_sc1(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -202,7 +178,6 @@ __device__ __forceinline__ uint32_t xcc_id() {
 #define FLOW_DIAG_TAKE(item, h) (void)0
 #define FLOW_DIAG_PATH(p) (void)0
 #define FLOW_DIAG_CLASSIFY(c, t) (void)0
-#define FLOW_DIAG_TAIL(v) (void)0
 #endif
 
 #ifndef TG_FLOW_TU  // (launched by tg_amd.hip's host code: the main unit only)
@@ -211,7 +186,7 @@ __global__ void k_census(uint32_t* mask) {
   if (threadIdx.x == 0) atomicOr(mask, 1u << (xcc_id() & 31u));
 }
 // after every k_flow launch, on its stream (one wave): a sub-problem whose chunks did not all
-// finish the launch sets TG_ERR_FLOW (no wave ran on its XCD; see "Coherence" above)
+// finish step K - 1 sets TG_ERR_FLOW (no wave ran on its XCD; see "Coherence" above)
 __global__ void k_flow_check(const int32_t* __restrict__ ctl, int P, int32_t C,
                              uint32_t* __restrict__ err_or) {
   const int x = (int)threadIdx.x;
@@ -222,8 +197,9 @@ __global__ void k_flow_check(const int32_t* __restrict__ ctl, int P, int32_t C,
 }
 #endif
 
-// 4 waves per SIMD (<= 128 VGPRs; built without MachineLICM, tg_flow.hip) — r05j A/B (round 5's
-// chunk form): uniform 0.1111 vs 0.1163 ms per step at 3 waves, masked 0.3309 vs 0.3491
+// 4 waves per SIMD (<= 128 VGPRs; built without MachineLICM, tg_flow.hip: 123-131 VGPRs
+// unconstrained) — r05j A/B: uniform 0.1111 vs 0.1163 ms per step at 3 waves, masked 0.3309 vs
+// 0.3491
 template <bool AR, int POL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_flow(Soa S, int64_t n, Level L,
                                                 const uint32_t* __restrict__ grid, FlowIO io,
@@ -264,43 +240,22 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     kst_end(ks, kt0);
     return;
   }
-  const int32_t nx = flow_envs(f.C, P, n, x);  // the sub-problem's envs
   int32_t* const ctl = f.ctl + (int64_t)x * CTL_WORDS;
   uint32_t* const q = f.q + (int64_t)x * f.qcap;
   int32_t* const fill = f.fill + (int64_t)x * FLOW_MAX_K * NLIST * f.jcap;
   int32_t* const list = f.list + (int64_t)x * FLOW_MAX_K * NLIST * f.lcap;
   const int64_t slot = (int64_t)blockIdx.x % nstat;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
   FLOW_DIAG_WAVE_STATE;
   if (lane == 0) FLOW_EV(10, x, 0, 0, 0);
 
-  // a run item on the queue (by the lane that calls it): chunk j of list (t, k), cnt entries
-  auto push = [&](int t, int k, int j, int cnt) {
+  // a run item on the queue (by the lane that calls it)
+  auto push = [&](int t, int k, int j, int src) {
     FLOW_DIAG_PUSH(t, k, j);
     const int at = atomicAdd(fcw(ctl, FC_QTAIL), 1);
-    const uint32_t item = ((uint32_t)t << 28) | ((uint32_t)k << 24) | ((uint32_t)(cnt - 1) << 18) | (uint32_t)j;
-    FLOW_EV(4, item, at, 0, x);
-    if ((int64_t)at < f.qcap) st_sc1(q + at, item);
+    FLOW_EV(4, ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j, at, src, x);
+    if ((int64_t)at < f.qcap) st_sc1(q + at, ((uint32_t)t << 28) | ((uint32_t)k << 24) | (uint32_t)j);
     else atomicOr(err_or, E_FLOW);  // (capacity is the bound of the pushes: unreachable)
-  };
-  // add to list chunk j's fill word; the adder that completes it pushes it.  The low byte counts
-  // entries written (a sealed chunk's missing places are added by its sealer), bits 8+ hold a
-  // sealed chunk's entry count (0: a full chunk of 64)
-  auto fill_add = [&](int t, int k, int j, int add) {
-    const int nv = atomicAdd(&fill[(int64_t)(t * NLIST + k) * f.jcap + j], add) + add;
-    if ((nv & 0xFF) == 64) push(t, k, j, (nv >> 8) ? (nv >> 8) : 64);
-  };
-  // seal the partial chunk at list (t, k)'s tail: its tail moves to the next chunk (one CAS,
-  // so no reservation lands in the sealed places), and the chunk is pushed with the entries it
-  // holds once they are written.  `reserve`: only below the first cxm chunks (every later entry
-  // then still fits lcap); the flush of a finished step seals unconditionally
-  auto seal = [&](int t, int k, bool reserve) -> bool {
-    int32_t* const lt = fcw(ctl, FC_LTAIL + t * NLIST + k);
-    const int v = ld_sc1(lt);
-    if (!(v & 63) || (reserve && (v >> 6) >= f.seal_below)) return false;
-    if (atomicCAS(lt, v, (v | 63) + 1) != v) return false;
-    const int r = v & 63;
-    fill_add(t, k, v >> 6, (64 - r) + (r << 8));
-    return true;
   };
   auto step_io = [&](int t) {
     return StepIO{nullptr, io.obs + (int64_t)t * io.obs_stride, io.reward + (int64_t)t * n,
@@ -308,223 +263,207 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                   io.t0 + t, io.tb + (uint32_t)t};
   };
 
-  // one run item: chunk j of list (t, k), cnt entries, one lane per entry, as k_run: the option
-  // loops of step t, the rows and the state; each lane then records its env's next step
-  // (cstep) and decrements its env's chunk's `outst`; returns the lanes whose env's chunk became
-  // ready (its chunk in cl)
-  auto run = [&](uint32_t item, int& cl) -> unsigned long long {
-    const int t = (int)(item >> 28), k = (int)((item >> 24) & 15u), j = (int)(item & 0x3FFFFu);
-    // a cheap guard: an item or entry out of range is a protocol bug; it sets
-    // TG_ERR_FLOW and runs nothing instead of addressing memory with it
-    const bool item_ok = t < K && k < NLIST && (int64_t)j < f.jcap;
-    const int lidx = item_ok ? t * NLIST + k : 0;
-    FLOW_DIAG_TAIL(tail);
-    const int mcnt = item_ok ? (int)((item >> 18) & 63u) + 1 : 0;
-    bool live = lane < mcnt;
-    int64_t i = 0;
-    if (live) i = ld_sc1(list + (int64_t)lidx * f.lcap + 64 * j + lane);
-    const bool bad = live && (i < 0 || i >= n || (int)((i >> 6) % P) != x);
-    if (lane == 0 && (!item_ok || __ballot(bad))) atomicOr(err_or, E_FLOW);
-    live = live && !bad;
-    FLOW_DIAG_RUN(item, i, live, mcnt, tail, lidx, j);
-    const StepIO st = step_io(t);
-    StepResult r{0, 0, 0, 0};
-    Env e;
-    e.mti = 0u;
-    int2 ep = make_int2(0, 0);
-    uint32_t draws = 0;
-    int lregen = 0;
-    if (live) {
-      unpack(ld16_sc1(S.st4, (uint32_t)i * 16u), ld_ang_sc1(S.ang, i), e);
-      ep = ld_ep_sc1(S.ep, i);
-      RngCodesT<true> rng(S.mt + i * MT_STORE, S.mc + i * MT_CODES, e.mti, (lds_u8*)warea);
-      rng.prime();
-      if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
-      if (k != L_RESET) run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform
-      r.done = is_done(e);
-      finish_step<AR, false, false>(level_div(L), e, rng, i, r, ep, st);  // valid: at listing
-      e.mti = rng.finish();
-      draws = rng.draws;
-      lregen = (int)rng.regens;
-      if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
-    }
-    if (AR) record_episodes(live && r.done, g0 + i, ep, st.tstep, eq, stats, slot);
-    if (live) {
-      st16_sc1(S.st4, (uint32_t)i * 16u, pack(e));
-      st16_sc1(S.ang, (uint32_t)i * 16u, d2u4(make_double2(e.ang0, e.ang1)));
-      st_ep_sc1(S.ep, i, ep);
-      st_sc1(f.cstep + i, t + 1);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    wave_stats(stats, 0, 0, r.ticks, (int)draws, AR ? (live && r.done) : 0,
-               __ballot(lregen != 0) ? wave_sum(lregen) : 0, true, slot);
-    // this wave's stores first, then the chunks' counters: the lane that takes its env's chunk
-    // to 0 hands the chunk to the wave (its next round below, in lane order)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int old = 0;
-    if (live) old = atomicSub(&f.outst[i >> 6], 1);
-    const unsigned long long ready = __ballot(live && old == 1);
-    if (lane == 0) FLOW_EV(7, item, (uint32_t)__popcll(ready), (uint32_t)mcnt, x);
-    cl = (int)(i >> 6);
-    return ready;
-  };
-
-  // One round of chunk c: every env of the chunk not yet done with step K - 1, one lane per env
-  // (coalesced loads), at its own next step (0 in the first round, the deal; later the step
-  // after the one its last option ran at, cstep).  Run-ahead (TG/:91-96 -> OP/:20-36: env i's
-  // step t + 1 depends on env i's step t alone): each lane classifies its env for its step t,
-  // t + 1, ... as k_classify would — the policy's action, can_run — and finishes every step
-  // whose option cannot run in place (reward None, state and MT stream untouched, OP/:22-23),
-  // until an option can run (the env is listed at (t', k)) or the launch's last step is past.
-  // The lanes advance in lockstep, so the rows of one step's lanes are adjacent.  The state is
-  // the same at every step of a run-ahead, so what depends on it alone is evaluated once: the 9
-  // options' can_run (available_mask, TG/:83-89), the obs row (get_state, TG/:94), done, and
-  // the policy's hash keyed by the env alone (policy_action's inner two rounds).  An env
-  // entering done with auto-reset on and no option to run goes on L_RESET (first round only: a
-  // run with auto-reset resets the env it finishes).  Returns the envs listed (0: the chunk is
-  // done with the launch).
-  auto round = [&](int c, bool first) -> int {
+  // classify chunk c for step t (k_classify's per-env work); returns the envs it listed
+  auto classify = [&](int c, int t) -> int {
     const int64_t i = (int64_t)c * 64 + lane;
-    bool live = i < n;
-    int t = 0;
-    if (live && !first) t = ld_sc1(f.cstep + i);
-    live = live && t < K;
-    Env e;
-    e.mti = 0u;
-    e.ang0 = e.ang1 = 0.0;
+    const bool live = i < n;
+    const StepIO st = step_io(t);
+    uint4 s4 = make_uint4(0, 0, 0, 0);
+    double2 a2 = make_double2(0.0, 0.0);
     int2 ep = make_int2(0, 0);
     if (live) {
-      unpack(ld16_sc1(S.st4, (uint32_t)i * 16u), ld_ang_sc1(S.ang, i), e);
+      s4 = ld16_sc1(S.st4, (uint32_t)i * 16u);
+      a2 = ld_ang_sc1(S.ang, i);
       ep = ld_ep_sc1(S.ep, i);
     }
-    const uint32_t f0 = e.f, mt0 = e.mti;
-    // a stale MT half not listed yet goes on k_regen's list c % SHARDS (MT_LISTED), as k_classify
+    Env e;
+    e.mti = 0u;
+    int k = -1;
+    bool runs = false;
+    if (live) {
+      unpack_st4(s4, e);
+      FLOW_EV_WAVE(11, c, t);  // (timing log: the state loads returned)
+      const int act = policy_action(L, m, e, POL, io.a0, g0 + i, io.t0 + t);
+      if (io.actions) io.actions[(int64_t)t * n + i] = act;
+      k = option_index(act);
+      runs = k >= 0 && can_run(L, m, e, k);
+      if (k < 0) e.f |= E_ACTION;
+    }
+    const bool rst = AR && live && !runs && is_done(e);  // entering done: reset (L_RESET)
+    const int bk = runs ? k : rst ? L_RESET : -1;
+    // The atomics that reserve this chunk's places go out first, their round trips overlapping
+    // the rows below (each one on the chain cost a classification ~1 us, the r05h event log):
+    // stale MT halves not listed yet go on k_regen's list c % SHARDS ...
     const bool stale = live && (e.mti & (MT_STALE | MT_LISTED)) == MT_STALE;
     const unsigned long long sb = __ballot(stale);
     int sbase = 0;
     if (sb && lane == 0) sbase = atomicAdd(&f.rcnt[(c % SHARDS) * CTR_STRIDE], __popcll(sb));
     if (stale) e.mti |= MT_LISTED;
-    const int tf = t;  // the lane's first classified step
-    int kl = -1, nvalid = 0;
-    if (live) {
-      const uint32_t avail = available_mask(L, m, e);
-      const bool done0 = is_done(e);
-      double orow[9];
-      observe(L, e, orow);
-      const uint64_t hb = sm64(io.a0 ^ sm64((uint64_t)(g0 + i)));
-      const int nav = __popc(avail);
-      while (t < K) {
-        const uint64_t hh = sm64(hb ^ (uint64_t)(io.t0 + t));
-        int act = (int)(hh % 9ull);  // policy_action, from the hoisted mask and hash
-        if (POL == TG_POLICY_MASKED && nav) {
-          uint32_t kk = (uint32_t)(hh % (uint64_t)nav), mm = avail;
-          while (kk--) mm &= mm - 1u;
-          act = __ffs(mm) - 1;
-        }
-        if (io.actions) io.actions[(int64_t)t * n + i] = act;
-        const int k = option_index(act);
-        const bool runs = k >= 0 && ((avail >> k) & 1u);
-        if (k < 0) e.f |= E_ACTION;
-        const StepIO st = step_io(t);
-        st.valid[i] = (uint8_t)runs;
-        if (runs) {
-          kl = k;
-          nvalid = 1;
-          break;
-        }
-        if (AR && done0) {
-          kl = L_RESET;
-          break;
-        }
-        st.reward[i] = 0;  // reward None (finish_step of a step whose option did not run)
-        st.done[i] = (uint8_t)done0;
-        store_obs(st.obs, i, orow);
-        ++t;
+    // ... and the listed lanes, grouped by list (rank in the group, its first lane and size),
+    // reserve their entries
+    const unsigned long long lb = __ballot(bk >= 0);
+    const int cnt = __popcll(lb);
+    int rank = 0, lead = 0, nb = 0;
+    unsigned long long pend = lb;
+    while (pend) {
+      const int first = __ffsll((long long)pend) - 1;
+      const int b0 = __builtin_amdgcn_readlane(bk, first);
+      const unsigned long long b = __ballot(bk == b0);
+      if (bk == b0) {
+        rank = __popcll(b & lt_mask);
+        lead = first;
+        nb = __popcll(b);
       }
-      if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+      pend &= ~b;
     }
-    FLOW_EV_WAVE(14, c, 0);  // (timing log: the run-ahead done)
-    const int tl = t;  // the listing step, or K
-    const bool listed = live && tl < K;
-    // the entries: lanes grouped by list (tl, k), one reservation per group (one atomic
-    // instruction of the groups' leads)
-    const int key = listed ? tl * NLIST + kl : -1;
-    int rank = 0, lead = 0, nb = 0, base = 0;
-    {
-      unsigned long long pend = __ballot(listed);
-      while (pend) {
-        const int first_l = __ffsll((long long)pend) - 1;
-        const int k0 = __builtin_amdgcn_readlane(key, first_l);
-        const unsigned long long b = __ballot(key == k0);
-        if (key == k0) {
-          rank = __popcll(b & ((1ull << lane) - 1ull));
-          lead = first_l;
-          nb = __popcll(b);
-        }
-        pend &= ~b;
-      }
+    const int lidx = t * NLIST + (bk >= 0 ? bk : 0);
+    int base = 0;
+    if (bk >= 0 && lane == lead) base = atomicAdd(fcw(ctl, FC_LTAIL + lidx), nb);
+    // every env's valid row, coalesced (as k_classify); the rows of the envs whose option cannot
+    // run: reward None, state unchanged (TG/:91-96, OP/:22-23)
+    if (live) st.valid[i] = (uint8_t)runs;
+    const bool fin = live && !runs && !rst;
+    double orow[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (fin) {
+      e.ang0 = a2.x;
+      e.ang1 = a2.y;
+      Rng rng(S.mt + i * MT_STORE, e.mti, S.mc + i * MT_CODES);  // no draws without a reset
+      StepResult r{0, 0, (int)is_done(e), 0};
+      finish_step<false, false, false>(L, e, rng, i, r, ep, st, orow);
     }
-    if (listed && lane == lead) base = atomicAdd(fcw(ctl, FC_LTAIL + key), nb);
-    const int cnt = __popcll(__ballot(listed));
-    // the handed-off bytes: refill entries, the state (when classification changed its flags:
-    // the env's run item loads it), the finished envs' next step (K), the list entries, the
-    // chunk's count; then publish: this wave's stores first; then the fill counts (the writer
-    // whose entries complete a list chunk pushes it), the steps classified (the wave that
-    // completes a step's count flushes its partial list chunks), a finished chunk
+    if (fin && (e.f & E_MASK)) atomicOr(err_or, e.f & E_MASK);
+    store_obs_wave(st.obs, (int64_t)c * 64, __ballot(fin), orow, reinterpret_cast<double*>(warea));
+    FLOW_EV_WAVE(12, c, t);  // (timing log: the rows issued)
+    // the handed-off bytes: refill entries, list entries, the state, the chunk's count
     sbase = __builtin_amdgcn_readlane(sbase, 0);
     if (stale)
-      f.refill[(c % SHARDS) * f.rcap + sbase + __popcll(sb & ((1ull << lane) - 1ull))] =
+      f.refill[(c % SHARDS) * f.rcap + sbase + __popcll(sb & lt_mask)] =
           (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
-    if (live && (e.f != f0 || e.mti != mt0)) st16_sc1(S.st4, (uint32_t)i * 16u, pack(e));
-    if (live && !listed) st_sc1(f.cstep + i, K);
-    const int gbase = __shfl(base, lead, 64);
-    if (listed) st_sc1(list + (int64_t)key * f.lcap + gbase + rank, (int32_t)i);
+    base = __shfl(base, lead, 64);
+    if (bk >= 0) st_sc1(list + (int64_t)lidx * f.lcap + base + rank, (int32_t)i);
+    if (live) {
+      const uint4 s4n = pack(e);
+      if (s4n.x != s4.x || s4n.y != s4.y || s4n.z != s4.z || s4n.w != s4.w)
+        st16_sc1(S.st4, (uint32_t)i * 16u, s4n);
+    }
     if (cnt && lane == 0) st_sc1(f.outst + c, cnt);
+    // publish: this wave's stores first (with no listed env, the chain goes on with the chunk's
+    // next step in this wave: its stores land first too); then the fill counts and the step's
+    // classified-chunk count together (the flush reads only the list tails, reserved above)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (listed && lane == lead) {
-      const int j0 = base >> 6, in0 = min(nb, 64 - (base & 63));
-      fill_add(tl, kl, j0, in0);
-      if (nb > in0) fill_add(tl, kl, j0 + 1, nb - in0);
+    FLOW_EV_WAVE(13, c, t);  // (timing log: the stores complete)
+    int32_t* const fl = fill + (int64_t)lidx * f.jcap;
+    const int j0 = base >> 6, in0 = min(nb, 64 - (base & 63));
+    int f0 = 0, f1 = 0, last = 0;
+    if (bk >= 0 && lane == lead) {
+      f0 = atomicAdd(&fl[j0], in0) + in0;
+      if (nb > in0) f1 = atomicAdd(&fl[j0 + 1], nb - in0) + (nb - in0);
     }
-    // steps classified: tf .. min(tl, K - 1) (the listing step's entry is written)
-    const int thi = live ? min(tl, K - 1) : -1;
-    const int s0 = __builtin_amdgcn_readfirstlane(wave_min_i(live && tf <= thi ? tf : K));
-    const int s1 = __builtin_amdgcn_readfirstlane(wave_max(thi));
-    for (int sp = s0; sp <= s1; ++sp) {
-      const int cs = __popcll(__ballot(live && tf <= sp && sp <= thi));
-      int last = 0;
-      if (cs && lane == 0) last = atomicAdd(fcw(ctl, FC_CLS + sp), cs) + cs == nx;
-      if (__builtin_amdgcn_readlane(last, 0) && lane < NLIST) seal(sp, lane, false);  // step sp's partial chunks
+    if (lane == 0) last = atomicAdd(fcw(ctl, FC_CLS + t), 1) + 1 == Cx;
+    if (bk >= 0 && lane == lead) {
+      if (f0 == 64) push(t, bk, j0, 0);
+      if (f1 == 64) push(t, bk, j0 + 1, 1);
     }
-    wave_stats(stats, live ? thi - tf + 1 : 0, nvalid, 0, 0, 0, 0, false, slot);
-    FLOW_EV_WAVE(15, c, cnt);  // (timing log: published)
+    wave_stats(stats, live ? 1 : 0, runs ? 1 : 0, 0, 0, 0, 0, false, slot);
+    // the last chunk classified for step t flushes step t's partial list chunks
+    if (lane == 0) FLOW_EV(2, c, t, cnt, x);
+    if (__builtin_amdgcn_readlane(last, 0) && lane < NLIST) {
+      const int tail = ld_sc1(fcw(ctl, FC_LTAIL + t * NLIST + lane));
+      if (tail & 63) push(t, lane, tail >> 6, 2 | (tail << 8));
+    }
     return cnt;
   };
+  // one run item: the option loops of a 64-entry list chunk (k_run's per-env work); returns the
+  // lanes whose env's chunk became ready (its chunk in cl)
+  auto run = [&](uint32_t item, int& cl) -> unsigned long long {
+      const int t = (int)(item >> 28), k = (int)((item >> 24) & 15u), j = (int)(item & 0xFFFFFFu);
+      // a cheap guard: an item or entry out of range is a protocol bug; it sets
+      // TG_ERR_FLOW and runs nothing instead of addressing memory with it
+      const bool item_ok = t < K && k < NLIST && (int64_t)j < f.jcap;
+      const int lidx = item_ok ? t * NLIST + k : 0;
+      int tail = 0;
+      if (lane == 0 && item_ok) tail = ld_sc1(fcw(ctl, FC_LTAIL + lidx));
+      tail = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(tail, 0));
+      const int mcnt = item_ok ? min(64, tail - 64 * j) : 0;
+      bool live = lane < mcnt;
+      int64_t i = 0;
+      if (live) i = ld_sc1(list + (int64_t)lidx * f.lcap + 64 * j + lane);
+      const bool bad = live && (i < 0 || i >= n || (int)((i >> 6) % P) != x);
+      if (lane == 0 && (!item_ok || __ballot(bad))) atomicOr(err_or, E_FLOW);
+      live = live && !bad;
+      FLOW_DIAG_RUN(item, i, live, mcnt, tail, lidx, j);
+      const StepIO st = step_io(t);
+      StepResult r{0, 0, 0, 0};
+      Env e;
+      e.mti = 0u;
+      int2 ep = make_int2(0, 0);
+      uint32_t draws = 0;
+      int lregen = 0;
+      if (live) {
+        unpack(ld16_sc1(S.st4, (uint32_t)i * 16u), ld_ang_sc1(S.ang, i), e);
+        ep = ld_ep_sc1(S.ep, i);
+        RngCodesT<true> rng(S.mt + i * MT_STORE, S.mc + i * MT_CODES, e.mti, (lds_u8*)warea);
+        rng.prime();
+        if (k != O_GO_LEFT && k != O_GO_RIGHT && k != O_INTERACT) __builtin_amdgcn_s_setprio(PRIO_SLOW);
+          if (k != L_RESET) run_option(L, trig, m, e, k, rng, r);  // k is wave-uniform
+        r.done = is_done(e);
+        finish_step<AR, false, false>(level_div(L), e, rng, i, r, ep, st);
+        e.mti = rng.finish();
+        draws = rng.draws;
+        lregen = (int)rng.regens;
+        if (e.f & E_MASK) atomicOr(err_or, e.f & E_MASK);
+      }
+      if (AR) record_episodes(live && r.done, g0 + i, ep, st.tstep, eq, stats, slot);
+      if (live) {
+        st16_sc1(S.st4, (uint32_t)i * 16u, pack(e));
+        st16_sc1(S.ang, (uint32_t)i * 16u, d2u4(make_double2(e.ang0, e.ang1)));
+        st_ep_sc1(S.ep, i, ep);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      wave_stats(stats, 0, 0, r.ticks, (int)draws, AR ? (live && r.done) : 0,
+                 __ballot(lregen != 0) ? wave_sum(lregen) : 0, true, slot);
+      // this wave's stores first, then the chunks' counters: the lane that takes its env's chunk
+      // to 0 hands the chunk to the wave (classified for t + 1 below, in lane order)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int old = 0;
+      if (live) old = atomicSub(&f.outst[i >> 6], 1);
+      if (live) FLOW_EV_LANE(3, item, (uint32_t)i, (uint32_t)old, (uint32_t)lane | ((uint32_t)mcnt << 8) | ((uint32_t)x << 16));
+      unsigned long long ready = __ballot(live && old == 1);
+      if (lane == 0) FLOW_EV(7, item, (uint32_t)__popcll(ready), (uint32_t)mcnt, x);
+      cl = (int)(i >> 6);
+      return ready;
+  };
 
-  // The wave's work loop: one unit per iteration, chosen by wave-uniform values only (each read
-  // back with readfirstlane, so the loop's branches stay scalar: with the work in nested loops
-  // whose exits the compiler did not prove uniform, round 5's bring-up saw a divergent loop
-  // nest).  In order: the first rounds of the chunks, dealt out by a counter; then the queue:
-  // run items, and the chunks other waves' run items made ready (a run item's envs come from up
-  // to 64 chunks; the first it readies runs its next round in this wave, the others go on the
-  // queue for any wave).  A chunk whose round lists no env is done with the launch.
-  bool deal = true;
-  int cl = 0;  // (per lane) the chunk of the lane's env in the last run item
+  // The wave's work loop: one unit of work per iteration, chosen by wave-uniform values only
+  // (each read back with readfirstlane, so the loop's branches stay scalar: with the work in
+  // nested loops whose exits the compiler did not prove uniform, it built a divergent loop
+  // nest whose lanes could sit in different iterations, and a wave re-classified chunk 0
+  // forever).  In order: a chunk carried to its next step (none of its envs ran an option, or
+  // the first chunk the wave's last run item completed), the step-0 chunks dealt out by a
+  // counter, then the queue: run items and the chunks other waves' run items completed (a run
+  // item's envs come from up to 64 chunks, and late in a step many of them complete together:
+  // classified by their one wave in turn they left the others waiting on the queue, 58 % of
+  // the waves' time in the r05g event log)
+  bool phase0 = true;
+  int cl = 0;                    // (per lane) the chunk of the lane's env in the last run item
+  int cc = -1, ct = 0;           // the carried chunk and its step
   while (true) {
-    int c;
-    bool first = false;
-    if (deal) {
+    int c, t;
+    FLOW_DIAG_PATH(cc >= 0 ? 1 : phase0 ? 3 : 2);
+    if (cc >= 0) {
+      c = cc;
+      t = ct;
+      cc = -1;
+    } else if (phase0) {
       int j = 0;
       if (lane == 0) j = atomicAdd(fcw(ctl, FC_INIT), 1);
       j = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(j, 0));
       if (j >= Cx) {
-        deal = false;
+        phase0 = false;
         continue;
       }
-      FLOW_DIAG_PATH(3);
-      FLOW_EV_WAVE(16, j, 0);  // (timing log: a deal chunk)
       c = x + P * j;
-      first = true;
+      t = 0;
     } else {
       // an item by ticket: wait for its slot (lane 0 polls, the wave reads its answer)
       int h = 0;
@@ -534,45 +473,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       if (lane == 0) FLOW_EV(8, h, x, 0, 0);
       uint32_t item = Q_EMPTY;
       int stop = 0;
-      unsigned long long t_wait = realtime();
       while (!stop) {
         uint32_t it = Q_EMPTY;
-        int dn = 0, head = 0;
+        int dn = 0;
         if (lane == 0) {
           if ((int64_t)h < f.qcap) it = ld_sc1(q + h);
-          if (it == Q_EMPTY) {
-            dn = ld_sc1(fcw(ctl, FC_DONE));
-            head = h == ld_sc1(fcw(ctl, FC_QTAIL));
-          }
+          if (it == Q_EMPTY) dn = ld_sc1(fcw(ctl, FC_DONE));
         }
         item = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(it, 0));
         dn = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(dn, 0));
-        head = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(head, 0));
         if (item != Q_EMPTY || dn) {
           stop = 1;
-        } else if (head && realtime() - t_wait > FLOW_SEAL_AFTER) {
-          // first in line and nothing to run: seal the partial list chunk of the lowest step
-          // (the fullest of that step's lists).  Besides latency this is what keeps a launch
-          // live: an env listed at a far step waits for that step's flush, which waits for a
-          // chunk-mate's next round, which waits for the far env's run (tests/native/flow_sim)
-          int best = -1, bt = K, bk = 0;
-          for (int t0 = 0; t0 < K && best < 0; t0 += 64 / NLIST) {
-            const int tc = t0 + lane / NLIST, kc = lane % NLIST;
-            int r = -1;
-            if (lane < (64 / NLIST) * NLIST && tc < K) {
-              const int v = ld_sc1(fcw(ctl, FC_LTAIL + tc * NLIST + kc));
-              if ((v & 63) && (v >> 6) < f.seal_below) r = ((K - tc) << 6) | (v & 63);
-            }
-            best = wave_max(r);
-            if (best >= 0) {
-              const unsigned long long bl = __ballot(r == best);
-              const int bl0 = __ffsll((long long)bl) - 1;
-              bt = __builtin_amdgcn_readlane(tc, bl0);
-              bk = __builtin_amdgcn_readlane(kc, bl0);
-            }
-          }
-          if (best >= 0 && lane == 0) seal(bt, bk, true);
-          t_wait = realtime();
         } else if (realtime() - t_start > FLOW_DEADLINE) {
           if (lane == 0) {
             atomicOr(err_or, E_FLOW);
@@ -587,10 +498,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       FLOW_DBG(3, h, item, x);
       if (lane == 0) FLOW_EV(5, h, item, x, 0);
       FLOW_DIAG_TAKE(item, h);
-      FLOW_DIAG_PATH(2);
-      if (((item >> 24) & 15u) == Q_CLASSIFY) {  // a chunk another wave's run item made ready
-        c = (int)(item & 0x3FFFFu);
-        if (c >= f.C || c % P != x) {  // (the run item's guard, for these items)
+      t = (int)(item >> 28);
+      if (((item >> 24) & 15u) == Q_CLASSIFY) {  // a chunk another wave's run item completed
+        c = (int)(item & 0xFFFFFFu);
+        if (t >= K || c >= f.C || c % P != x) {  // (the guard above, for classification items)
           if (lane == 0) atomicOr(err_or, E_FLOW);
           continue;
         }
@@ -601,17 +512,37 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         const unsigned long long ready =
             ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(rd >> 32)) << 32) |
             (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rd);
+        FLOW_DBG(4, h, item, (uint32_t)__popcll(ready));
         if (!ready) continue;
-        // the first readied chunk's next round runs here, the others by whichever waves take them
+        ++t;
+        if (t >= K) {  // chunks done with the last step
+          if (lane == 0) {
+            const int nr = __popcll(ready);
+            if (atomicAdd(fcw(ctl, FC_FIN), nr) + nr == Cx)
+              __hip_atomic_store(fcw(ctl, FC_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          continue;
+        }
+        // the first completed chunk is classified here, the others by whichever waves take them
         const int l0 = __ffsll((long long)ready) - 1;
         c = __builtin_amdgcn_readlane(cl, l0);
-        if (((ready >> lane) & 1ull) && lane != l0) push(0, Q_CLASSIFY, cl, 1);
+        if (((ready >> lane) & 1ull) && lane != l0) push(t, Q_CLASSIFY, cl, 3);
       }
     }
-    FLOW_DIAG_CLASSIFY(c, 0);
-    if (__builtin_amdgcn_readfirstlane(round(c, first)) == 0 && lane == 0 &&
-        atomicAdd(fcw(ctl, FC_FIN), 1) + 1 == Cx)  // the chunk is done with the launch
-      __hip_atomic_store(fcw(ctl, FC_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // chunk c at step t: classified, or, past the last step, finished
+    if (t >= K) {
+      if (lane == 0 && atomicAdd(fcw(ctl, FC_FIN), 1) + 1 == Cx)
+        __hip_atomic_store(fcw(ctl, FC_DONE), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    FLOW_DBG(10 + t, c, x, 0);
+    FLOW_DIAG_CLASSIFY(c, t);
+    const int cnt = __builtin_amdgcn_readfirstlane(classify(c, t));
+    FLOW_DBG(30 + t, c, x, cnt);
+    if (cnt == 0) {  // no env of the chunk runs an option: its next step at once
+      cc = c;
+      ct = t + 1;
+    }
   }
   FLOW_DBG(9, 0, 0, 0);
   if (lane == 0) FLOW_EV(9, x, 0, 0, 0);

@@ -96,8 +96,7 @@ constexpr uint32_t FLOW_EVW = 1024;
       }                                                                                          \
       if (lane == 0) {                                                                           \
         const int fl_ = ld_sc1(fill + (int64_t)(lidx) * f.jcap + (j));                           \
-        if (((fl_ & 0xFF) != 64 || ((fl_ >> 8) ? (fl_ >> 8) : 64) != (mcnt)) &&                   \
-            atomicCAS(f.dbg + 4091 * 4, 0u, 95u) == 0u) {                                         \
+        if (fl_ != (mcnt) && atomicCAS(f.dbg + 4091 * 4, 0u, 95u) == 0u) {                       \
           f.dbg[4091 * 4 + 1] = (item);                                                          \
           f.dbg[4091 * 4 + 2] = (uint32_t)fl_ | ((uint32_t)x << 24);                              \
           f.dbg[4091 * 4 + 3] = (uint32_t)(tail);                                                \
@@ -112,7 +111,7 @@ constexpr uint32_t FLOW_EVW = 1024;
     item_ = (item);                                                                              \
     if (lane == 0 && f.dbgc && (((item) >> 24) & 15u) != Q_CLASSIFY) {                           \
       const int it_l_ = (int)(((item) >> 28) * NLIST + (((item) >> 24) & 15u));                  \
-      const uint32_t o_ = atomicAdd(&f.dbgc[(int64_t)f.C * 16 + ((int64_t)x * FLOW_MAX_K * NLIST + it_l_) * f.jcap + ((item) & 0x3FFFFu)], 1u); \
+      const uint32_t o_ = atomicAdd(&f.dbgc[(int64_t)f.C * 16 + ((int64_t)x * FLOW_MAX_K * NLIST + it_l_) * f.jcap + ((item) & 0xFFFFFFu)], 1u); \
       if (o_ && atomicCAS(f.dbg + 4094 * 4, 0u, 98u) == 0u) {                                    \
         f.dbg[4094 * 4 + 1] = (item);                                                            \
         f.dbg[4094 * 4 + 2] = (uint32_t)(h);                                                     \
@@ -122,7 +121,6 @@ constexpr uint32_t FLOW_EVW = 1024;
   } while (0)
 
 #define FLOW_DIAG_PATH(p) (path_ = (p))
-#define FLOW_DIAG_TAIL(v) const int v = 0  // (FLOW_DIAG_RUN's tail word: unused by the run-ahead form)
 
 // a chunk classified twice for one step (slot 4095)
 #define FLOW_DIAG_CLASSIFY(c, t)                                                                  \

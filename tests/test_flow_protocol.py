@@ -1,7 +1,7 @@
 """CPU: a thread model of k_flow's work protocol (tests/native/flow_sim.cpp, restating
-csrc/tg_flow.h's deal / run-ahead / lists / queue / flush rules with host atomics) classifies
-every env-step exactly once, runs every env-step whose option runs exactly once and terminates,
-at ragged sizes, one and several sub-problems, and run rates from rare to every env.  The GPU suite (tests/test_gpu_flow.py) checks the kernel
+csrc/tg_flow.h's deal / lists / queue / readiness / flush rules with host atomics) runs every
+chunk-step exactly once and terminates, at ragged sizes, one and several sub-problems, and run
+rates from rare to every env.  The GPU suite (tests/test_gpu_flow.py) checks the kernel
 itself against the per-step API and the oracle."""
 import os
 import subprocess
