@@ -804,7 +804,14 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
 // specialised to that option's primitive actions.  (Round 3 also tried worklists per (option,
 // predicted length class), which raised lane efficiency from 0.53 to 0.84 but ran 2-5 % slower:
 // DESIGN.md §3.1.)
-constexpr int SHARDS = 8;
+constexpr int SHARDS = 8;  // the stale-MT-half refill lists: one per XCD (k_regen's waves of XCD x drain list x)
+// the worklists' shards (k_classify's workgroup b appends to shard b % WSHARDS): each
+// (option, shard) counter takes one returning atomic per workgroup that lists an env of that
+// option, so more shards spread a launch's ~4k x 10 atomics over more words
+#ifndef TG_WSHARDS
+#define TG_WSHARDS 8
+#endif
+constexpr int WSHARDS = TG_WSHARDS;
 // Worklists: one per option, and one (L_RESET) of the envs whose option cannot run but which
 // enter the step done with auto-reset on (stepped with auto-reset off until done, then on):
 // k_run resets them (reward None, no option), so k_classify carries no reset path (the gauss
@@ -823,12 +830,12 @@ constexpr RunPos make_runpos() {
   return r;
 }
 constexpr RunPos kRunPos = make_runpos();
-constexpr int NSEG = NLIST * SHARDS;  // segment = run position * SHARDS + shard
+constexpr int NSEG = NLIST * WSHARDS;  // segment = run position * WSHARDS + shard
 static_assert(NSEG <= 2 * RUN_BLOCK, "k_run's prefix: two segments per thread");
 constexpr int NCTR = NSEG;      // the worklist counters
 constexpr int CTR_STRIDE = 32;  // counters 128 B apart
 struct Work {
-  int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = run position * SHARDS + shard
+  int32_t* __restrict__ lists;   // [NSEG][shard_cap], segment = run position * WSHARDS + shard
   // the listed envs' state, in worklist order (written by k_classify, which has loaded it
   // anyway): k_run reads its chunk's 64 records coalesced, in one round trip with the list
   // entries, instead of a dependent gather of 16 + 16 + 8 scattered bytes per lane
@@ -852,11 +859,11 @@ struct Work {
 __constant__ int kOrder[NLIST] = {O_JUMP_LEFT, O_JUMP_RIGHT, O_GO_LEFT,     O_GO_RIGHT,
                                   O_DOWN_LEFT, O_DOWN_RIGHT, O_UP_LADDER,   O_DOWN_LADDER,
                                   O_INTERACT,  L_RESET};
-__constant__ int kSegBase[NLIST] = {kRunPos.of[0] * SHARDS, kRunPos.of[1] * SHARDS,
-                                      kRunPos.of[2] * SHARDS, kRunPos.of[3] * SHARDS,
-                                      kRunPos.of[4] * SHARDS, kRunPos.of[5] * SHARDS,
-                                      kRunPos.of[6] * SHARDS, kRunPos.of[7] * SHARDS,
-                                      kRunPos.of[8] * SHARDS, kRunPos.of[9] * SHARDS};
+__constant__ int kSegBase[NLIST] = {kRunPos.of[0] * WSHARDS, kRunPos.of[1] * WSHARDS,
+                                      kRunPos.of[2] * WSHARDS, kRunPos.of[3] * WSHARDS,
+                                      kRunPos.of[4] * WSHARDS, kRunPos.of[5] * WSHARDS,
+                                      kRunPos.of[6] * WSHARDS, kRunPos.of[7] * WSHARDS,
+                                      kRunPos.of[8] * WSHARDS, kRunPos.of[9] * WSHARDS};
 
 // 8 waves per SIMD: its 98-106 SGPRs (the level, the step's pointers) held it to 7; forced, 32-55
 // of them spill to VGPR lanes (no VGPR spills, 60 VGPRs).  A/B r04r: uniform 0.1246 vs 0.1258 ms
@@ -952,11 +959,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
   __syncthreads();
   // the workgroup's worklist ranges: issue the global atomics now, use them after the
   // reward-None envs are finished (their latency overlaps that work)
-  const int shard = blockIdx.x % SHARDS;
+  const int shard = blockIdx.x % SHARDS, wshard = blockIdx.x % WSHARDS;
   int my_base = 0;
   if (threadIdx.x < NLIST) {
     const int c = bcnt[threadIdx.x];
-    my_base = c ? atomicAdd(&w.ctr[(kSegBase[threadIdx.x] + shard) * CTR_STRIDE], c) : 0;
+    my_base = c ? atomicAdd(&w.ctr[(kSegBase[threadIdx.x] + wshard) * CTR_STRIDE], c) : 0;
   } else if (threadIdx.x == 64) {  // (another wave than the worklists' atomics)
     int c = 0;
 #pragma unroll
@@ -996,7 +1003,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     w.refill[shard * w.rcap + at] = (uint32_t)i | (mt_half(e.mti & MT_POS_MASK) ? 0x80000000u : 0u);
   }
   if (bk >= 0) {
-    const int64_t at = (int64_t)(kSegBase[bk] + shard) * w.shard_cap + bbase[bk] + slot;
+    const int64_t at = (int64_t)(kSegBase[bk] + wshard) * w.shard_cap + bbase[bk] + slot;
     w.lists[at] = (int32_t)i;
     w.wst4[at] = s4w;
     w.wang[at] = a2;
@@ -1060,7 +1067,7 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   if (threadIdx.x == 0) {
     int acc = 0;
     for (int j = 0; j < NLIST; ++j) {
-      const int sb = j * SHARDS, se = sb + SHARDS;
+      const int sb = j * WSHARDS, se = sb + WSHARDS;
       ostart[j] = acc;
       oraw[j] = pre[sb];
       acc += (pre[se] - pre[sb] + 63) & ~63;
@@ -1078,9 +1085,9 @@ __global__ __launch_bounds__(RUN_BLOCK) void k_run(Soa S, int64_t n, Level L,
   // this lane's place in option k's lists (the raw prefix's coordinates), and its segment
   const int qraw = oraw[oj] + base + (threadIdx.x & 63) - ostart[oj];
   const bool live = base < total && qraw < oraw[oj + 1];
-  int seg = oj * SHARDS;
+  int seg = oj * WSHARDS;
   if (live) {
-    int hi = seg + SHARDS;  // pre[seg] <= qraw < pre[hi]
+    int hi = seg + WSHARDS;  // pre[seg] <= qraw < pre[hi]
     while (hi - seg > 1) {
       const int mid = (seg + hi) >> 1;
       if (pre[mid] <= qraw) seg = mid; else hi = mid;
@@ -1627,15 +1634,16 @@ int alloc_ctx(StepCtx& c, int64_t off, int64_t n) {
   if (hipMalloc((void**)&(ptr), (bytes)) != hipSuccess)                \
     return fail(TG_E_NOMEM, "hipMalloc %zu B for " #ptr, (size_t)(bytes));
   ALLOC_C(c.stats, sizeof(unsigned long long) * ST_COUNT * (size_t)stat_slots(n));
-  // a shard holds the envs of every SHARDS-th workgroup
-  c.shard_cap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK;
+  // a worklist shard holds the envs of every WSHARDS-th workgroup; a refill list those of every
+  // SHARDS-th, REGEN_STEPS steps of them
+  c.shard_cap = (int64_t)((grid_for(n) + WSHARDS - 1) / WSHARDS) * BLOCK;
   ALLOC_C(c.wl, sizeof(int32_t) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wst4, sizeof(uint4) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wang, sizeof(double2) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wep, sizeof(int2) * NSEG * (size_t)c.shard_cap);
   ALLOC_C(c.wctr, sizeof(int32_t) * 2 * NCTR * CTR_STRIDE);
   // a shard's list holds at most its workgroups' envs per pending step
-  c.rcap = c.shard_cap * REGEN_STEPS;
+  c.rcap = (int64_t)((grid_for(n) + SHARDS - 1) / SHARDS) * BLOCK * REGEN_STEPS;
   ALLOC_C(c.refill, sizeof(uint32_t) * SHARDS * (size_t)c.rcap);
   ALLOC_C(c.regen_ctr, sizeof(int32_t) * 2 * RCTR_N * CTR_STRIDE);
 #undef ALLOC_C
