@@ -16,6 +16,7 @@
 
 #include <cstdarg>
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <unistd.h>
 #include <cstdio>
@@ -735,18 +736,15 @@ constexpr int POL_IMMEDIATE = -2;  // k_step's action is io.a0 (tg_step1), not a
 // POL: -1 actions given; POL_IMMEDIATE one action for all (tg_step1); else the TG_POLICY_*
 // evaluated here (tg_rollout).  A template
 // parameter, so the per-step kernels carry none of the policy's code or registers.
-template <bool AUTORESET, bool FINAL, int POL = -1>
-__global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
-                                                 const uint32_t* __restrict__ grid, StepIO io,
-                                                 EpQueue q, int64_t g0,
-                                                 unsigned long long* __restrict__ stats,
-                                                 uint32_t* __restrict__ err_or,
-                                                 unsigned long long* __restrict__ ks) {
-  const unsigned long long kt0 = kst_begin(ks);
-  __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
-  LEVEL_IN_LDS();
-  lds_u8* const wscr = (lds_u8*)win + (threadIdx.x >> 6) * WIN_WAVE_BYTES;
-  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+// One step of env i (lane i's; live iff i < n) with the level in LDS (trig, m) and the wave's
+// code window wscr: k_step's body, also k_serve1's private-stream step.  Every lane of the wave
+// must reach it.
+template <bool AUTORESET, bool FINAL, int POL>
+__device__ __forceinline__ void step_env(const Soa& S, int64_t n, const Level& L,
+                                         const uint32_t* trig, const Map& m, lds_u8* wscr,
+                                         int64_t i, const StepIO& io, const EpQueue& q,
+                                         int64_t g0, unsigned long long* __restrict__ stats,
+                                         uint32_t* __restrict__ err_or) {
   const bool live = i < n;
   StepResult r{0, 0, 0, 0};
   uint32_t draws = 0;
@@ -789,6 +787,21 @@ __global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
   }
   wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
               __popcll(need) + wave_sum(lregen), true);
+}
+
+template <bool AUTORESET, bool FINAL, int POL = -1>
+__global__ __launch_bounds__(BLOCK) void k_step(Soa S, int64_t n, Level L,
+                                                 const uint32_t* __restrict__ grid, StepIO io,
+                                                 EpQueue q, int64_t g0,
+                                                 unsigned long long* __restrict__ stats,
+                                                 uint32_t* __restrict__ err_or,
+                                                 unsigned long long* __restrict__ ks) {
+  const unsigned long long kt0 = kst_begin(ks);
+  __shared__ __attribute__((aligned(16))) uint8_t win[(BLOCK / 64) * WIN_WAVE_BYTES];
+  LEVEL_IN_LDS();
+  lds_u8* const wscr = (lds_u8*)win + (threadIdx.x >> 6) * WIN_WAVE_BYTES;
+  step_env<AUTORESET, FINAL, POL>(S, n, L, trig, m, wscr, (int64_t)blockIdx.x * BLOCK + threadIdx.x,
+                                  io, q, g0, stats, err_or);
   kst_end(ks, kt0);
 }
 
@@ -1401,17 +1414,19 @@ __global__ __launch_bounds__(BLOCK) void k_gather_mt(Soa S, int64_t first, int64
 // read by absolute position across generations), and gauss_next carried in and out.
 constexpr int PY_GENS = 3;  // generations held in LDS; a 4th+ is twisted in place by lane 0
 struct PyRng {
-  uint32_t* w;     // LDS: PY_GENS slots of MT_N words, generation g in slot g % PY_GENS
+  uint32_t* w;     // LDS: PY_GENS slots of MT_N words, generation g in slot (g + off) % PY_GENS
   uint32_t q;      // absolute word position (generation g holds positions [g*624, g*624 + 624))
   uint32_t lo;     // oldest generation held
   uint32_t draws;
+  uint32_t off;    // the ring's rotation (k_serve1 keeps the ring in LDS across calls)
+  __device__ __forceinline__ uint32_t* slot(uint32_t g) const { return w + ((g + off) % PY_GENS) * MT_N; }
   __device__ __forceinline__ uint32_t word(uint32_t pos) {
     const uint32_t g = pos / MT_N;
     while (g >= lo + PY_GENS) {  // > 2 generations in one call (long levels): twist in place
-      twist_gen(w + ((lo + PY_GENS - 1) % PY_GENS) * MT_N, w + (lo % PY_GENS) * MT_N);
+      twist_gen(slot(lo + PY_GENS - 1), slot(lo));
       ++lo;
     }
-    return w[(g % PY_GENS) * MT_N + (pos - g * MT_N)];
+    return slot(g)[pos - g * MT_N];
   }
   __device__ __forceinline__ double random() {
     const uint32_t a = word(q), b = word(q + 1);
@@ -1442,42 +1457,26 @@ __device__ __forceinline__ void lds_twist64(const uint32_t* src, uint32_t* dst) 
     __syncthreads();
   }
 }
-// The Python stream's generation and its two successors, kept on the device between calls
-// (tg_batch::pyc): cache_in is it when the caller's state is the one the last call returned
-// (the host compares them), else null and the generation is read from the caller's state (py,
-// pinned host memory) and its successors twisted here.  q0 / gauss: the caller's index and
-// gauss_next, as kernel arguments (no host-memory reads in the common case).  On return py
-// holds the state after the call: its index and gauss_next, and the generation's words when
-// the generation changed (otherwise py's words already are the generation's), and cache_out
-// holds the new generation and its two successors.
+// lane 0 runs the call (a step of `action`, or RESET) over the ring W, where generation j of the
+// caller's stream (j = 0: the one tg_pystate holds; q0 its index) sits in slot (j + off) % 3.
+// On return py holds the state after the call: its index and gauss_next, and the generation's
+// words when the generation changed (otherwise py's words already are the generation's); the
+// ring holds the new generation and its two successors, off updated to match.  Returns the new
+// generation's number (0: unchanged).  Every lane of the (one-wave) workgroup must reach it.
 template <bool RESET>
-__global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __restrict__ grid,
-                                            int action, tg_pystate* py, const uint32_t* cache_in,
-                                            uint32_t* cache_out, uint32_t q0, int has_gauss,
+__device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const LdsLevel& lv,
+                                            uint32_t* W, uint32_t& off, int action,
+                                            tg_pystate* py, uint32_t q0, int has_gauss,
                                             double gauss_next, TgOne* out, uint32_t tstep,
                                             unsigned long long* __restrict__ stats,
                                             uint32_t* __restrict__ err_or) {
-  __shared__ uint32_t W[PY_GENS * MT_N];
-  __shared__ LdsLevel lv;
   __shared__ uint32_t out_g, out_lo, out_idx;
   const int lane = threadIdx.x;
-  const int nwords = ((L.W + 2 * PAD) * (L.H + 2 * PAD) + 3) / 4;
-  for (int i = lane; i < nwords; i += 64) lv.grid[i] = grid[i];
-  if (lane < 12) lv.trig[lane] = L.trig[lane >> 1][lane & 1];
-  if (cache_in) {
-    for (int i = lane; i < PY_GENS * MT_N; i += 64) W[i] = cache_in[i];
-    __syncthreads();
-  } else {
-    for (int i = lane; i < MT_N; i += 64) W[i] = py->mt[i];
-    __syncthreads();
-    lds_twist64(W, W + MT_N);
-    lds_twist64(W + MT_N, W + 2 * MT_N);
-  }
   StepResult r{0, 0, 0, 0};
   uint32_t draws = 0;
   if (lane == 0) {
     const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
-    PyRng rng{W, q0, 0u, 0u};
+    PyRng rng{W, q0, 0u, 0u, off};
     Env e;
     unpack(S.st4[0], S.ang[0], e);
     int2 ep = S.ep[0];
@@ -1512,19 +1511,152 @@ __global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __re
   __syncthreads();
   const uint32_t g = out_g;
   if (g != 0u) {  // the caller's generation changed
-    const uint32_t* src = W + (g % PY_GENS) * MT_N;
+    const uint32_t* src = W + ((g + off) % PY_GENS) * MT_N;
     for (int i = lane; i < MT_N; i += 64) py->mt[i] = src[i];
+    // the ring: generations g, g + 1, g + 2 (it holds out_lo .. out_lo + 2, g among them; the
+    // missing successors are twisted over generations older than g)
+    for (uint32_t hi = out_lo + PY_GENS - 1; hi < g + PY_GENS - 1; ++hi)
+      lds_twist64(W + ((hi + off) % PY_GENS) * MT_N, W + ((hi + 1 + off) % PY_GENS) * MT_N);
+    off = (off + g) % PY_GENS;
   }
   if (lane == 0) py->index = out_idx;
-  if (g != 0u || !cache_in) {
-    // the cache: generations g, g + 1, g + 2 (the ring holds out_lo .. out_lo + 2, g among
-    // them; the missing successors are twisted over generations older than g)
-    for (uint32_t hi = out_lo + PY_GENS - 1; hi < g + PY_GENS - 1; ++hi)
-      lds_twist64(W + (hi % PY_GENS) * MT_N, W + ((hi + 1) % PY_GENS) * MT_N);
-    for (int j = 0; j < PY_GENS; ++j)
-      for (int i = lane; i < MT_N; i += 64) cache_out[j * MT_N + i] = W[((g + j) % PY_GENS) * MT_N + i];
-  }
   wave_stats(stats, lane == 0 && !RESET ? 1 : 0, r.ran, r.ticks, (int)draws, 0);
+  return g;
+}
+// the ring from the caller's state (py, pinned host memory): its generation and two successors
+__device__ __forceinline__ void py_ring_cold(uint32_t* W, const tg_pystate* py) {
+  for (int i = threadIdx.x; i < MT_N; i += 64) W[i] = py->mt[i];
+  __syncthreads();
+  lds_twist64(W, W + MT_N);
+  lds_twist64(W + MT_N, W + 2 * MT_N);
+}
+__device__ __forceinline__ void py_level(LdsLevel& lv, const Level& L, const uint32_t* __restrict__ grid) {
+  const int nwords = ((L.W + 2 * PAD) * (L.H + 2 * PAD) + 3) / 4;
+  for (int i = threadIdx.x; i < nwords; i += 64) lv.grid[i] = grid[i];
+  if (threadIdx.x < 12) lv.trig[threadIdx.x] = L.trig[threadIdx.x >> 1][threadIdx.x & 1];
+}
+// The Python stream's generation and its two successors, kept on the device between calls
+// (tg_batch::pyc, generation j in slot j): cache_in is it when the caller's state is the one the
+// last call returned (the host compares them), else null and the ring is built from the
+// caller's state.  q0 / gauss: the caller's index and gauss_next, as kernel arguments (no
+// host-memory reads in the common case).  On return py holds the state after the call and
+// cache_out the new generation and its two successors.
+template <bool RESET>
+__global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __restrict__ grid,
+                                            int action, tg_pystate* py, const uint32_t* cache_in,
+                                            uint32_t* cache_out, uint32_t q0, int has_gauss,
+                                            double gauss_next, TgOne* out, uint32_t tstep,
+                                            unsigned long long* __restrict__ stats,
+                                            uint32_t* __restrict__ err_or) {
+  __shared__ uint32_t W[PY_GENS * MT_N];
+  __shared__ LdsLevel lv;
+  const int lane = threadIdx.x;
+  py_level(lv, L, grid);
+  if (cache_in) {
+    for (int i = lane; i < PY_GENS * MT_N; i += 64) W[i] = cache_in[i];
+    __syncthreads();
+  } else {
+    py_ring_cold(W, py);
+  }
+  uint32_t off = 0;
+  const uint32_t g = py_call<RESET>(S, L, lv, W, off, action, py, q0, has_gauss, gauss_next, out,
+                                    tstep, stats, err_or);
+  if (g != 0u || !cache_in)
+    for (int j = 0; j < PY_GENS; ++j)
+      for (int i = lane; i < MT_N; i += 64) cache_out[j * MT_N + i] = W[((j + off) % PY_GENS) * MT_N + i];
+}
+
+// ---- the N = 1 server (tg_batch::serve) ------------------------------------------------------
+// One wave, resident for a 1-env handle's tg_step1 / tg_step1_py / tg_reset1_py: it polls the
+// mailbox's seq (a system-scope load of pinned host memory), serves a new command with the same
+// device code as k_step<POL_IMMEDIATE> / k_py1 (step_env, py_call), writes the result row and
+// the stream state into pinned host memory, releases them at system scope and then stores
+// done = seq, which the host spins on.  The level, the code window and the Python stream's ring
+// (rotated by off) stay in LDS between commands.  Every lane leaves together, on SRV_QUIT or
+// after `idle` ticks of s_memrealtime (100 MHz) without a command; a leaving server writes the
+// ring to pyc (generation j in slot j), where the next server or k_py1 finds it.
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+__global__ __launch_bounds__(64) void k_serve1(Soa S, Level L, const uint32_t* __restrict__ grid,
+                                               SrvBox* box, tg_pystate* py, uint32_t* pyc,
+                                               TgOne* out, EpQueue q, int64_t g0, uint32_t idle,
+                                               int trace, unsigned long long* __restrict__ stats,
+                                               uint32_t* __restrict__ err_or) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[WIN_WAVE_BYTES];
+  __shared__ uint32_t W[PY_GENS * MT_N];
+  __shared__ LdsLevel lv;
+  const int lane = threadIdx.x;
+  py_level(lv, L, grid);
+  __syncthreads();
+  const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
+  bool ring = false;  // W holds the Python stream's ring
+  uint32_t off = 0;
+  uint32_t served = sys_load(&box->done);
+  unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+  while (true) {
+    const uint32_t s = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+    if (s == served) {
+      if (__builtin_amdgcn_s_memrealtime() - t_last > idle) break;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
+    const int32_t kind = (int32_t)sys_load((const uint32_t*)&box->kind);
+    if (kind == SRV_QUIT) {
+      served = s;
+      break;
+    }
+    const int action = (int)sys_load((const uint32_t*)&box->action);
+    const uint32_t tstep = sys_load(&box->tstep);
+    if (kind == SRV_STEP) {
+      const StepIO io{nullptr, out->obs, &out->reward, &out->valid, &out->done, nullptr,
+                      POL_IMMEDIATE, (uint64_t)(int64_t)action, 0, tstep};
+      step_env<false, false, POL_IMMEDIATE>(S, 1, L, lv.trig, m, (lds_u8*)win, lane, io, q, g0,
+                                            stats, err_or);
+    } else {
+      const uint32_t q0 = sys_load(&box->q0);
+      const int has_gauss = (int)sys_load((const uint32_t*)&box->has_gauss);
+      const bool warm = sys_load((const uint32_t*)&box->warm) != 0u;
+      const uint64_t gb = (uint64_t)sys_load((const uint32_t*)&box->gauss_bits) |
+                          (uint64_t)sys_load((const uint32_t*)&box->gauss_bits + 1) << 32;
+      const double gauss_next = __builtin_bit_cast(double, gb);
+      if (!ring || !warm) {  // a new server, or draws on the stream since the last call
+        if (warm) {
+          for (int i = lane; i < PY_GENS * MT_N; i += 64) W[i] = pyc[i];
+          __syncthreads();
+        } else {
+          py_ring_cold(W, py);
+        }
+        off = 0;
+        ring = true;
+      }
+      if (kind == SRV_RESET_PY)
+        py_call<true>(S, L, lv, W, off, 0, py, q0, has_gauss, gauss_next, out, tstep, stats, err_or);
+      else
+        py_call<false>(S, L, lv, W, off, action, py, q0, has_gauss, gauss_next, out, tstep, stats,
+                       err_or);
+    }
+    // the row and the state (host memory; the env's state and MT ring in HBM for the next
+    // command) before the answer
+    if (trace && lane == 0) {
+      box->t_seen = t_seen;
+      box->t_end = __builtin_amdgcn_s_memrealtime();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    if (lane == 0) __hip_atomic_store(&box->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    served = s;
+    t_last = __builtin_amdgcn_s_memrealtime();
+  }
+  if (ring)
+    for (int j = 0; j < PY_GENS; ++j)
+      for (int i = lane; i < MT_N; i += 64) pyc[j * MT_N + i] = W[((j + off) % PY_GENS) * MT_N + i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (lane == 0) __hip_atomic_store(&box->done, served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // tg_probe_dispatch: nothing (a dependent kernel boundary's cost alone)
@@ -1709,6 +1841,12 @@ int tg_create(tg_batch** out, int64_t n, uint64_t seed_base, int64_t global_offs
   h->domain = dom;
   h->flow_debug = getenv("TG_FLOW_DEBUG") != nullptr;
   if (const char* sp = getenv("TG_FLOW_SKIP_PART")) h->flow_skip = atoi(sp);
+  if (const char* sv = getenv("TG_SERVE")) h->serve = atoi(sv) != 0;
+  h->srv_trace = getenv("TG_SERVE_TRACE") != nullptr;
+  // the server's idle limit: 500 us by default (a stream it shares a hardware queue with waits
+  // at most this long behind it)
+  const char* si = getenv("TG_SERVE_IDLE_US");
+  h->srv_idle = 100u * (uint32_t)std::min(std::max(si ? atoi(si) : 500, 1), 1000000);
   // completed-episode queue: drained by tg_episodes; records beyond it are counted as dropped
   const int64_t cap = 4 * n > (1 << 16) ? 4 * n : (1 << 16);
   h->eps_cap = (int32_t)(cap < (1 << 28) ? cap : (1 << 28));
@@ -1772,6 +1910,16 @@ void tg_destroy(tg_batch* h) {
   if (!h) return;
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
+  if (h->srv_live) (void)srv_stop(h);
+  if (h->srv_trace && h->srv_calls)
+    fprintf(stderr, "[serve] calls %lld launches %lld: mean per call %.2f us to post, %.2f us post -> "
+            "answer, of which %.2f us between the server's pickup and its answer\n",
+            (long long)h->srv_calls, (long long)h->srv_launches, h->srv_post_ns / h->srv_calls / 1e3,
+            h->srv_rt_ns / h->srv_calls / 1e3, h->srv_gpu_ns / h->srv_calls / 1e3);
+  if (h->srv_ev) (void)hipEventDestroy(h->srv_ev);
+  if (h->srv_dep) (void)hipEventDestroy(h->srv_dep);
+  if (h->srv_st) (void)hipStreamDestroy(h->srv_st);
+  if (h->box) (void)hipHostFree(h->box);
   render_free(h->rs);
   flow_free(h);
   void* bufs[] = {h->grid, h->genrand, h->gotab, h->masks, h->obs_q, h->S.st4, h->S.ang, h->S.ep,
@@ -2076,25 +2224,151 @@ int tg_step(tg_batch* h, const int32_t* actions, double* obs, int32_t* reward, u
                      h->tstep++);
 }
 
+}  // extern "C"
+
+namespace {
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// the N = 1 calls' result row: pinned, coherent host memory the kernel (or server) writes
+int one_row(tg_batch* h) {
+  if (h->one) return TG_OK;
+  if (hipHostMalloc((void**)&h->one, sizeof(TgOne), hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipSuccess)
+    return fail(TG_E_NOMEM, "tg_step1: pinned result buffer");
+  HIP_TRY(hipHostGetDevicePointer((void**)&h->one_dev, h->one, 0));
+  return TG_OK;
+}
+
+// launch k_serve1 on the server's stream, after the work queued on the caller's stream
+int srv_start(tg_batch* h, hipStream_t caller) {
+  if (!h->box) {
+    if (hipHostMalloc((void**)&h->box, sizeof(SrvBox), hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess)
+      return fail(TG_E_NOMEM, "tg_step1: pinned server mailbox");
+    memset(h->box, 0, sizeof(SrvBox));
+    HIP_TRY(hipHostGetDevicePointer((void**)&h->box_dev, h->box, 0));
+    HIP_TRY(hipStreamCreateWithFlags(&h->srv_st, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&h->srv_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&h->srv_dep, hipEventDisableTiming));
+    h->srv_seq = 0;
+  }
+  if (!h->py) {  // (the server's kernel argument; only SRV_*_PY commands touch it)
+    if (hipHostMalloc((void**)&h->py, sizeof(tg_pystate), hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess)
+      return fail(TG_E_NOMEM, "tg_step1: pinned stream state");
+    HIP_TRY(hipHostGetDevicePointer((void**)&h->py_dev, h->py, 0));
+  }
+  if (!h->pyc) {
+    if (hipMalloc((void**)&h->pyc, sizeof(uint32_t) * PY_GENS * MT_N) != hipSuccess)
+      return fail(TG_E_NOMEM, "tg_step1: stream cache");
+    h->py_warm = false;
+  }
+  HIP_TRY(hipEventRecord(h->srv_dep, caller));
+  HIP_TRY(hipStreamWaitEvent(h->srv_st, h->srv_dep, 0));
+  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
+  hipLaunchKernelGGL(k_serve1, dim3(1), dim3(64), 0, h->srv_st, h->S, h->L, h->grid, h->box_dev,
+                     h->py_dev, h->pyc, h->one_dev, q, h->g0, h->srv_idle, (int)h->srv_trace,
+                     h->main.stats, h->err);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(h->srv_ev, h->srv_st));
+  h->srv_live = true;
+  h->srv_t_last = now_ns();
+  ++h->srv_launches;
+  return TG_OK;
+}
+
+// post a command and spin on its answer; a server that left (idle) before it saw the command is
+// relaunched, and the new one serves it (it starts from the mailbox's done)
+int srv_call(tg_batch* h, const SrvBox& c, hipStream_t caller) {
+  // a server idle for more than half its limit (host clock, which starts after the server's)
+  // may have left: ask its event before posting
+  const int64_t t0 = now_ns();
+  if (!h->srv_live ||
+      (t0 - h->srv_t_last > (int64_t)h->srv_idle * 5 && hipEventQuery(h->srv_ev) == hipSuccess)) {
+    if (const int rc = srv_start(h, caller)) return rc;
+  }
+  SrvBox* const b = h->box;
+  const uint32_t seq = ++h->srv_seq;
+  b->kind = c.kind;
+  b->action = c.action;
+  b->tstep = c.tstep;
+  b->q0 = c.q0;
+  b->has_gauss = c.has_gauss;
+  b->warm = c.warm;
+  b->gauss_bits = c.gauss_bits;
+  const int64_t tp = h->srv_trace ? now_ns() : 0;
+  __atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
+  ++h->srv_calls;
+  for (uint64_t it = 1;; ++it) {
+    if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) {
+      h->srv_t_last = now_ns();
+      if (h->srv_trace) {
+        h->srv_post_ns += (double)(tp - t0);
+        h->srv_rt_ns += (double)(h->srv_t_last - tp);
+        h->srv_gpu_ns += 10.0 * (double)(b->t_end - b->t_seen);
+      }
+      return TG_OK;
+    }
+    __builtin_ia32_pause();
+    if ((it & 4095) == 0) {
+      const hipError_t e = hipEventQuery(h->srv_ev);
+      if (e == hipSuccess) {  // the server left: a new one serves the command
+        if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) continue;
+        if (const int rc = srv_start(h, caller)) return rc;
+      } else if (e != hipErrorNotReady) {
+        h->srv_live = false;
+        return fail(TG_E_HIP, "tg_step1 server: %s", hipGetErrorString(e));
+      } else if (now_ns() - t0 > 20000000000ll) {
+        return fail(TG_E_HIP, "tg_step1 server: no answer to command %u in 20 s", seq);
+      }
+    }
+  }
+}
+}  // namespace
+
+namespace tg {
+int srv_stop(tg_batch* h) {
+  if (!h->srv_live) return TG_OK;
+  h->srv_live = false;
+  if (hipEventQuery(h->srv_ev) != hipSuccess) {
+    SrvBox* const b = h->box;
+    b->kind = SRV_QUIT;
+    __atomic_store_n(&b->seq, ++h->srv_seq, __ATOMIC_RELEASE);
+  }
+  HIP_TRY(hipEventSynchronize(h->srv_ev));
+  // gone: a QUIT it left (idle) without reading is void, not a command for the next server
+  h->box->done = h->box->seq;
+  return TG_OK;
+}
+}  // namespace tg
+
+extern "C" {
+
 int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t* valid,
              uint8_t* done, void* stream) {
-  BIND(h);
+  BIND_SERVE(h);
   if (h->n != 1 || !obs || !reward || !valid || !done)
     return fail(TG_E_INVAL, "tg_step1: a 1-env handle and host obs/reward/valid/done");
-  if (!h->one) {  // the step's row, written by the kernel straight into pinned host memory
-    if (hipHostMalloc((void**)&h->one, sizeof(TgOne), hipHostMallocMapped) != hipSuccess)
-      return fail(TG_E_NOMEM, "tg_step1: pinned result buffer");
-    HIP_TRY(hipHostGetDevicePointer((void**)&h->one_dev, h->one, 0));
-  }
+  if (const int rc = one_row(h)) return rc;
   hipStream_t st = (hipStream_t)stream;
-  TgOne* const d = h->one_dev;
-  const StepIO io{nullptr, d->obs, &d->reward, &d->valid, &d->done, nullptr, POL_IMMEDIATE,
-                  (uint64_t)(int64_t)action, 0, h->tstep++};
-  const EpQueue q{h->eps, h->eps_count, h->eps_cap};
-  hipLaunchKernelGGL((k_step<false, false, POL_IMMEDIATE>), dim3(1), dim3(BLOCK), 0, st, h->S,
-                     h->n, h->L, h->grid, io, q, h->g0, h->main.stats, h->err, nullptr);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(st));
+  if (h->serve) {
+    SrvBox c{};
+    c.kind = SRV_STEP;
+    c.action = action;
+    c.tstep = h->tstep++;
+    if (const int rc = srv_call(h, c, st)) return rc;
+  } else {
+    TgOne* const d = h->one_dev;
+    const StepIO io{nullptr, d->obs, &d->reward, &d->valid, &d->done, nullptr, POL_IMMEDIATE,
+                    (uint64_t)(int64_t)action, 0, h->tstep++};
+    const EpQueue q{h->eps, h->eps_count, h->eps_cap};
+    hipLaunchKernelGGL((k_step<false, false, POL_IMMEDIATE>), dim3(1), dim3(BLOCK), 0, st, h->S,
+                       h->n, h->L, h->grid, io, q, h->g0, h->main.stats, h->err, nullptr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+  }
   memcpy(obs, h->one->obs, sizeof h->one->obs);
   *reward = h->one->reward;
   *valid = h->one->valid;
@@ -2102,22 +2376,26 @@ int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t*
   return TG_OK;
 }
 
+int tg_set_serve(tg_batch* h, int on) {
+  BIND(h);  // (stops a running server)
+  h->serve = on != 0;
+  return TG_OK;
+}
+
 }  // extern "C"
 
 namespace {
-// one k_py1 launch: the caller's stream state in, the result row and the advanced state out
+// one k_py1 launch (or server command): the caller's stream state in, the result row and the
+// advanced state out
 template <bool RESET>
 int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) {
   if (h->n != 1 || !st) return fail(TG_E_INVAL, "tg_*1_py: a 1-env handle and a stream state");
   if (st->index > (uint32_t)MT_N)
     return fail(TG_E_INVAL, "tg_*1_py: index %u outside [0, 624]", st->index);
-  if (!h->one) {
-    if (hipHostMalloc((void**)&h->one, sizeof(TgOne), hipHostMallocMapped) != hipSuccess)
-      return fail(TG_E_NOMEM, "tg_*1_py: pinned result buffer");
-    HIP_TRY(hipHostGetDevicePointer((void**)&h->one_dev, h->one, 0));
-  }
+  if (const int rc = one_row(h)) return rc;
   if (!h->py) {
-    if (hipHostMalloc((void**)&h->py, sizeof(tg_pystate), hipHostMallocMapped) != hipSuccess)
+    if (hipHostMalloc((void**)&h->py, sizeof(tg_pystate), hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess)
       return fail(TG_E_NOMEM, "tg_*1_py: pinned stream state");
     HIP_TRY(hipHostGetDevicePointer((void**)&h->py_dev, h->py, 0));
   }
@@ -2133,11 +2411,23 @@ int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) 
   // a step's tstep is its index; a reset's, the next step's (the new episode's start)
   const uint32_t tstep = RESET ? h->tstep : h->tstep++;
   h->py_warm = false;  // until the call has returned
-  hipLaunchKernelGGL(k_py1<RESET>, dim3(1), dim3(64), 0, stream, h->S, h->L, h->grid, (int)action,
-                     h->py_dev, warm ? h->pyc : nullptr, h->pyc, st->index, (int)st->has_gauss,
-                     st->gauss_next, h->one_dev, tstep, h->main.stats, h->err);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(stream));
+  if (h->serve) {
+    SrvBox c{};
+    c.kind = RESET ? SRV_RESET_PY : SRV_STEP_PY;
+    c.action = action;
+    c.tstep = tstep;
+    c.q0 = st->index;
+    c.has_gauss = (int32_t)st->has_gauss;
+    c.warm = warm ? 1 : 0;
+    memcpy(&c.gauss_bits, &st->gauss_next, sizeof c.gauss_bits);
+    if (const int rc = srv_call(h, c, stream)) return rc;
+  } else {
+    hipLaunchKernelGGL(k_py1<RESET>, dim3(1), dim3(64), 0, stream, h->S, h->L, h->grid, (int)action,
+                       h->py_dev, warm ? h->pyc : nullptr, h->pyc, st->index, (int)st->has_gauss,
+                       st->gauss_next, h->one_dev, tstep, h->main.stats, h->err);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
   memcpy(st, h->py, sizeof(tg_pystate));
   h->py_last = *st;
   h->py_warm = true;
@@ -2149,7 +2439,7 @@ extern "C" {
 
 int tg_step1_py(tg_batch* h, int32_t action, tg_pystate* st, double* obs, int32_t* reward,
                 uint8_t* valid, uint8_t* done, void* stream) {
-  BIND(h);
+  BIND_SERVE(h);
   if (!obs || !reward || !valid || !done) return fail(TG_E_INVAL, "tg_step1_py: null output");
   const int rc = launch_py1<false>(h, action, st, (hipStream_t)stream);
   if (rc) return rc;
@@ -2161,7 +2451,7 @@ int tg_step1_py(tg_batch* h, int32_t action, tg_pystate* st, double* obs, int32_
 }
 
 int tg_reset1_py(tg_batch* h, tg_pystate* st, double* obs, void* stream) {
-  BIND(h);
+  BIND_SERVE(h);
   const int rc = launch_py1<true>(h, 0, st, (hipStream_t)stream);
   if (rc) return rc;
   if (obs) memcpy(obs, h->one->obs, sizeof h->one->obs);

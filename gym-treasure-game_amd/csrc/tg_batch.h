@@ -45,6 +45,29 @@ struct TgOne {
   uint8_t valid, done;
 };
 
+// The N = 1 server's mailbox (k_serve1, tg_amd.hip): pinned, coherent host memory.  Line 0 is
+// the host's (a command's fields, then seq), line 1 the server's (done: the last command it
+// served; a server that starts reads it, so a command posted while none ran is served by the
+// next one).
+enum : int32_t { SRV_STEP = 1, SRV_STEP_PY = 2, SRV_RESET_PY = 3, SRV_QUIT = 4 };
+struct SrvBox {
+  uint32_t seq;         // the last command posted
+  int32_t kind;         // SRV_*
+  int32_t action;
+  uint32_t tstep;       // the step's index (h->tstep)
+  uint32_t q0;          // SRV_*_PY: the caller's index and gauss_next, and whether the device's
+  int32_t has_gauss;    //   generations are the caller's (tg_batch::py_warm)
+  int32_t warm;
+  int32_t pad0;
+  uint64_t gauss_bits;
+  uint8_t pad1[64 - 40];
+  uint32_t done;
+  uint32_t pad2[3];
+  uint64_t t_seen, t_end;  // TG_SERVE_TRACE: the server's clock at the command's pickup / answer
+  uint32_t pad3[8];
+};
+static_assert(sizeof(SrvBox) == 128, "SrvBox: two 64-B lines");
+
 struct RenderState;  // tg_render.hip
 void render_free(RenderState* rs);
 
@@ -119,6 +142,22 @@ struct tg_batch {
   uint32_t* pyc = nullptr;  // the Python stream's generation + 2 successors, on the device
   tg_pystate py_last{};     // the state the last tg_*1_py call returned
   bool py_warm = false;     // pyc matches py_last
+  // the N = 1 calls' resident server (k_serve1): tg_step1 / tg_step1_py / tg_reset1_py post a
+  // command to its mailbox and spin on the answer instead of a launch and a synchronisation
+  // each; every other entry point stops it first (BIND)
+  bool serve = true;               // tg_set_serve / TG_SERVE (read at tg_create)
+  uint32_t srv_idle = 0;           // the server leaves after this many 10-ns ticks without a command
+  tg::SrvBox* box = nullptr;       // the mailbox (pinned, coherent) and its device address
+  tg::SrvBox* box_dev = nullptr;
+  hipStream_t srv_st = nullptr;    // the server's stream: after the caller's stream (srv_dep)
+  hipEvent_t srv_ev = nullptr;     //   recorded after each server launch: complete = it left
+  hipEvent_t srv_dep = nullptr;
+  bool srv_live = false;           // a server was launched and not stopped
+  uint32_t srv_seq = 0;
+  int64_t srv_t_last = 0;          // host clock (ns) at the last answer
+  int64_t srv_launches = 0, srv_calls = 0;
+  bool srv_trace = false;          // TG_SERVE_TRACE: sums printed at tg_destroy (diagnostic)
+  double srv_rt_ns = 0.0, srv_gpu_ns = 0.0, srv_post_ns = 0.0;
   tg::RenderState* rs = nullptr;   // tg_render_init
   std::vector<int> kst_k;          // steps each in-use step record covers (a k_flow launch: K)
   // TG_MODE_FLOW's work structures (tg_flow.h Flow; allocated at the first flow rollout)
@@ -151,7 +190,18 @@ inline int bind(const tg_batch* h) {
   if (cur != h->device) HIP_TRY(hipSetDevice(h->device));
   return TG_OK;
 }
+int srv_stop(tg_batch* h);  // tg_amd.hip: stop the N = 1 server (if one runs) and wait for it
+// every entry point: the handle's device current, and the N = 1 server stopped (it steps the
+// env on a stream of its own: nothing else may touch the handle's state while it runs)
 #define BIND(h)                       \
+  do {                                \
+    if (!(h)) return fail(TG_E_INVAL, "null handle"); \
+    int rc_ = bind(h);                \
+    if (!rc_ && (h)->srv_live) rc_ = srv_stop(h); \
+    if (rc_) return rc_;              \
+  } while (0)
+// the N = 1 calls the server serves
+#define BIND_SERVE(h)                 \
   do {                                \
     if (!(h)) return fail(TG_E_INVAL, "null handle"); \
     int rc_ = bind(h);                \

@@ -307,6 +307,12 @@ class TreasureGameVec:
         check(self._L.tg_errors(self.handle, ctypes.byref(v), self._stream()), "tg_errors")
         return int(v.value)
 
+    def set_serve(self, on=True):
+        """A 1-env handle's N = 1 calls (TreasureGame.step / reset) through the resident server
+        kernel (the default; tg_set_serve) or one launch + synchronisation each: identical
+        results, the server without the launch and the synchronisation."""
+        check(self._L.tg_set_serve(self.handle, 1 if on else 0), "tg_set_serve")
+
     def set_mode(self, mode="compact", run_blocks=0):
         """Step implementation: "compact" (two-pass, default), "direct" (one lane per env
         runs in place) or "flow" (as compact per step; rollout() runs up to 16 steps per launch,

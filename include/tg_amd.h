@@ -138,19 +138,28 @@ int tg_reset(tg_batch *h, const uint8_t *mask, double *obs, void *stream);
 int tg_step(tg_batch *h, const int32_t *actions, double *obs, int32_t *reward, uint8_t *valid,
             uint8_t *done, double *final_obs, uint32_t flags, void *stream);
 
-/* step(action) of a 1-env handle, for the N=1 drop-in (TreasureGame.step, TG/:91-96): the
- * action travels as a kernel argument and the kernel writes the result row straight into
- * pinned host memory, so one launch and one stream synchronisation make the whole call (no
- * auto-reset, as the reference).  Outputs are HOST pointers: obs f64 [9], reward, valid,
- * done.  Synchronises `stream`. */
+/* step(action) of a 1-env handle, for the N=1 drop-in (TreasureGame.step, TG/:91-96), no
+ * auto-reset (as the reference).  Outputs are HOST pointers: obs f64 [9], reward, valid, done.
+ * By default (tg_set_serve) the call is served by a one-wave kernel resident on the device
+ * (k_serve1) that polls a mailbox in pinned host memory: the call posts the action, spins on
+ * the answer and returns the row the kernel wrote into pinned host memory -- no launch and no
+ * synchronisation per call.  The server is launched by the first such call (after the work
+ * queued on `stream`), stopped by any other call on the handle, and leaves by itself after
+ * TG_SERVE_IDLE_US (default 500) microseconds without a command.  With serving off: one launch
+ * on `stream` and one synchronisation of it. */
 int tg_step1(tg_batch *h, int32_t action, double *obs, int32_t *reward, uint8_t *valid,
              uint8_t *done, void *stream);
+
+/* The N = 1 calls (tg_step1, tg_step1_py, tg_reset1_py) through the resident server (on != 0,
+ * the default unless TG_SERVE=0 at tg_create) or one launch + synchronisation each (0).  Stops
+ * a running server.  Results are identical either way. */
+int tg_set_serve(tg_batch *h, int on);
 
 /* The N=1 drop-in drawing from a caller-held Python random stream instead of the env's own
  * (TreasureGame with the reference's module-global random, IM/:2, OB/:9): `st` (host memory)
  * is read at the call and written back with the stream advanced by exactly the draws the
- * reference's call makes, any index (odd ones too) and gauss_next included.  One launch and one
- * stream synchronisation per call.
+ * reference's call makes, any index (odd ones too) and gauss_next included.  Served as tg_step1
+ * (the resident server, or one launch and one synchronisation per call).
  *   tg_step1_py:  step(action) (TG/:91-96); outputs as tg_step1.
  *   tg_reset1_py: reset() (TG/:78-81, IM/:55-73: 2 uniform + 2 gauss), also the constructor's
  *                 build (IM/:31-53); obs f64 [9] host, may be NULL. */

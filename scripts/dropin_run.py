@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""The N = 1 drop-in's call latency alone (bench.dropin_latency), for a profiler to wrap:
+
+    rocprofv3 --kernel-trace --stats -d DIR -- python3 scripts/dropin_run.py [STEPS]
+
+Also prints the floor of one launch + one synchronisation on this box: a one-element torch
+add_ and hipStreamSynchronize, timed the same way.  Diagnostic, not the product."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import gym_treasure_game_amd as tg  # noqa: E402
+
+
+def launch_sync_floor(n=2000):
+    x = torch.zeros(1, device="cuda")
+    for _ in range(50):
+        x.add_(1)
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        x.add_(1)
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e6
+
+
+def main():
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+    out = bench.dropin_latency(tg, steps=steps)
+    out["launch_sync_floor_us"] = launch_sync_floor()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

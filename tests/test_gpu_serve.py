@@ -1,0 +1,98 @@
+"""The N = 1 drop-in's resident server (k_serve1, tg_set_serve): every call of TreasureGame
+through it equals the launch-per-call path and the reference restatements, including the server's
+leaving and relaunching (TG_SERVE_IDLE_US), the races around it (a 1 us idle limit: nearly every
+call finds the server gone or leaving), sleeps longer than the limit between calls (the next
+server reloads the Python stream's generations from the device cache), the user's own draws on
+the shared stream (the ring rebuilt from the caller's state) and other calls on the handle in
+between (which stop the server)."""
+import random
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _shared_run(tg, seed, serve, sleeps):
+    import pyref  # test infrastructure (oracle/), on sys.path via conftest
+    saved = random.getstate()
+    try:
+        random.seed(seed)
+        env = tg.TreasureGame()
+        env._vec.set_serve(serve)
+        ref = pyref.Env(seed)
+        assert env.reset() == ref.reset()
+        u = random.Random(seed + 1)
+        out = []
+        for t in range(160):
+            a = u.randrange(9)
+            if t % 9 == 4:
+                assert random.random() == ref.rng.random()
+            if t % 13 == 6:
+                assert random.gauss(0, 1) == ref.rng.gauss(0, 1)
+            if sleeps and t % 17 == 5:
+                time.sleep(0.003)
+            st, r, d, _ = env.step(a)
+            rs, rr, rd, _ = ref.step(a)
+            assert (st, r, d) == (list(rs), rr, rd), (serve, t)
+            out.append((st, r, d))
+            if d or t % 50 == 11:
+                assert env.reset() == ref.reset()
+            if t % 31 == 30:  # another call on the handle: stops the server
+                assert env.available_mask.tolist() == list(ref.available_mask())
+            assert random.getstate() == ref.rng.getstate(), (serve, t)
+        assert env._vec.errors() == 0
+        env.close()
+        return out
+    finally:
+        random.setstate(saved)
+
+
+@pytest.mark.parametrize("idle_us", [None, "1"])
+def test_serve_shared_stream_matches_launch_path(tg, monkeypatch, idle_us):
+    if idle_us:
+        monkeypatch.setenv("TG_SERVE_IDLE_US", idle_us)
+    on = _shared_run(tg, 31, True, sleeps=True)
+    off = _shared_run(tg, 31, False, sleeps=False)
+    assert on == off
+
+
+@pytest.mark.parametrize("idle_us", [None, "1"])
+def test_serve_private_stream_matches_oracle(tg, oracle, monkeypatch, idle_us):
+    if idle_us:
+        monkeypatch.setenv("TG_SERVE_IDLE_US", idle_us)
+    for serve in (True, False):
+        env = tg.TreasureGame(seed=8)
+        env._vec.set_serve(serve)
+        ref = oracle.OracleEnv(8)
+        assert np.array_equal(np.array(env.reset()).view(np.uint64), ref.obs.view(np.uint64))
+        for t in range(200):
+            a = oracle.pick_action(0xA5, 8, t, True, ref.mask())
+            if serve and t % 23 == 7:
+                time.sleep(0.002)
+            st, r, d, _ = env.step(a)
+            rs, rr, rd, _ = ref.step(a)
+            assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)), (serve, t)
+            assert (r, d) == (rr, rd), (serve, t)
+            if d:
+                s0 = env.reset()
+                ref.reset()
+                assert np.array_equal(np.array(s0).view(np.uint64), ref.obs.view(np.uint64))
+        assert env._vec.errors() == 0
+        env.close()
+
+
+def test_serve_toggle_mid_episode(tg, oracle):
+    """tg_set_serve stops a running server; the env continues on either path"""
+    env = tg.TreasureGame(seed=3)
+    ref = oracle.OracleEnv(3)
+    env.reset()
+    for t in range(120):
+        if t % 10 == 0:
+            env._vec.set_serve(t % 20 == 0)
+        a = t % 9
+        st, r, d, _ = env.step(a)
+        rs, rr, rd, _ = ref.step(a)
+        assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)) and (r, d) == (rr, rd), t
+    env.close()
