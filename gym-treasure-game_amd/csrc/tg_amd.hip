@@ -740,7 +740,7 @@ constexpr int POL_IMMEDIATE = -2;  // k_step's action is io.a0 (tg_step1), not a
 // code window wscr: k_step's body, also k_serve1's private-stream step.  Every lane of the wave
 // must reach it.
 template <bool AUTORESET, bool FINAL, int POL>
-__device__ __forceinline__ void step_env(const Soa& S, int64_t n, const Level& L,
+__device__ __forceinline__ StepResult step_env(const Soa& S, int64_t n, const Level& L,
                                          const uint32_t* trig, const Map& m, lds_u8* wscr,
                                          int64_t i, const StepIO& io, const EpQueue& q,
                                          int64_t g0, unsigned long long* __restrict__ stats,
@@ -787,6 +787,7 @@ __device__ __forceinline__ void step_env(const Soa& S, int64_t n, const Level& L
   }
   wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
               __popcll(need) + wave_sum(lregen), true);
+  return r;
 }
 
 template <bool AUTORESET, bool FINAL, int POL = -1>
@@ -1469,7 +1470,7 @@ __device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const 
                                             tg_pystate* py, uint32_t q0, int has_gauss,
                                             double gauss_next, TgOne* out, uint32_t tstep,
                                             unsigned long long* __restrict__ stats,
-                                            uint32_t* __restrict__ err_or) {
+                                            uint32_t* __restrict__ err_or, int* ticks = nullptr) {
   __shared__ uint32_t out_g, out_lo, out_idx;
   const int lane = threadIdx.x;
   StepResult r{0, 0, 0, 0};
@@ -1521,6 +1522,7 @@ __device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const 
   }
   if (lane == 0) py->index = out_idx;
   wave_stats(stats, lane == 0 && !RESET ? 1 : 0, r.ran, r.ticks, (int)draws, 0);
+  if (ticks) *ticks = r.ticks;
   return g;
 }
 // the ring from the caller's state (py, pinned host memory): its generation and two successors
@@ -1595,14 +1597,15 @@ __global__ __launch_bounds__(64) void k_serve1(Soa S, Level L, const uint32_t* _
   uint32_t served = sys_load(&box->done);
   unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
   while (true) {
-    const uint32_t s = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+    const uint32_t s = sys_load(&box->seq);
     if (s == served) {
       if (__builtin_amdgcn_s_memrealtime() - t_last > idle) break;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the command's fields after its seq
     const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
+    int ticks = 0;
     const int32_t kind = (int32_t)sys_load((const uint32_t*)&box->kind);
     if (kind == SRV_QUIT) {
       served = s;
@@ -1613,8 +1616,8 @@ __global__ __launch_bounds__(64) void k_serve1(Soa S, Level L, const uint32_t* _
     if (kind == SRV_STEP) {
       const StepIO io{nullptr, out->obs, &out->reward, &out->valid, &out->done, nullptr,
                       POL_IMMEDIATE, (uint64_t)(int64_t)action, 0, tstep};
-      step_env<false, false, POL_IMMEDIATE>(S, 1, L, lv.trig, m, (lds_u8*)win, lane, io, q, g0,
-                                            stats, err_or);
+      ticks = step_env<false, false, POL_IMMEDIATE>(S, 1, L, lv.trig, m, (lds_u8*)win, lane, io, q,
+                                                    g0, stats, err_or).ticks;
     } else {
       const uint32_t q0 = sys_load(&box->q0);
       const int has_gauss = (int)sys_load((const uint32_t*)&box->has_gauss);
@@ -1633,16 +1636,18 @@ __global__ __launch_bounds__(64) void k_serve1(Soa S, Level L, const uint32_t* _
         ring = true;
       }
       if (kind == SRV_RESET_PY)
-        py_call<true>(S, L, lv, W, off, 0, py, q0, has_gauss, gauss_next, out, tstep, stats, err_or);
+        py_call<true>(S, L, lv, W, off, 0, py, q0, has_gauss, gauss_next, out, tstep, stats, err_or,
+                      &ticks);
       else
         py_call<false>(S, L, lv, W, off, action, py, q0, has_gauss, gauss_next, out, tstep, stats,
-                       err_or);
+                       err_or, &ticks);
     }
     // the row and the state (host memory; the env's state and MT ring in HBM for the next
     // command) before the answer
     if (trace && lane == 0) {
       box->t_seen = t_seen;
       box->t_end = __builtin_amdgcn_s_memrealtime();
+      box->ticks = (uint32_t)ticks;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __syncthreads();
@@ -1916,6 +1921,13 @@ void tg_destroy(tg_batch* h) {
             "answer, of which %.2f us between the server's pickup and its answer\n",
             (long long)h->srv_calls, (long long)h->srv_launches, h->srv_post_ns / h->srv_calls / 1e3,
             h->srv_rt_ns / h->srv_calls / 1e3, h->srv_gpu_ns / h->srv_calls / 1e3);
+  if (h->srv_trace && h->srv_calls > 2) {  // server time = a + b * ticks (least squares)
+    const double n = (double)h->srv_calls, sk = h->srv_fit[0], skk = h->srv_fit[1];
+    const double sg = h->srv_gpu_ns, sgk = h->srv_fit[2];
+    const double b = (n * sgk - sk * sg) / (n * skk - sk * sk), a = (sg - b * sk) / n;
+    fprintf(stderr, "[serve] ticks per command %.2f; server time = %.2f us + %.3f us x ticks\n",
+            sk / n, a / 1e3, b / 1e3);
+  }
   if (h->srv_ev) (void)hipEventDestroy(h->srv_ev);
   if (h->srv_dep) (void)hipEventDestroy(h->srv_dep);
   if (h->srv_st) (void)hipStreamDestroy(h->srv_st);
@@ -2305,9 +2317,13 @@ int srv_call(tg_batch* h, const SrvBox& c, hipStream_t caller) {
     if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) {
       h->srv_t_last = now_ns();
       if (h->srv_trace) {
+        const double g = 10.0 * (double)(b->t_end - b->t_seen), k = (double)b->ticks;
         h->srv_post_ns += (double)(tp - t0);
         h->srv_rt_ns += (double)(h->srv_t_last - tp);
-        h->srv_gpu_ns += 10.0 * (double)(b->t_end - b->t_seen);
+        h->srv_gpu_ns += g;
+        h->srv_fit[0] += k;
+        h->srv_fit[1] += k * k;
+        h->srv_fit[2] += g * k;
       }
       return TG_OK;
     }
@@ -2386,12 +2402,15 @@ int tg_set_serve(tg_batch* h, int on) {
 
 namespace {
 // one k_py1 launch (or server command): the caller's stream state in, the result row and the
-// advanced state out
+// advanced state out.  The state is the 624 words, the index and (may be null: a step draws no
+// gauss) has_gauss / gauss_next, wherever the caller keeps them: a tg_pystate, or the words and
+// index of a CPython random.Random object (tg_step1_pywords).
 template <bool RESET>
-int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) {
-  if (h->n != 1 || !st) return fail(TG_E_INVAL, "tg_*1_py: a 1-env handle and a stream state");
-  if (st->index > (uint32_t)MT_N)
-    return fail(TG_E_INVAL, "tg_*1_py: index %u outside [0, 624]", st->index);
+int launch_py1(tg_batch* h, int32_t action, uint32_t* words, uint32_t* index, uint32_t* has_gauss,
+               double* gauss_next, hipStream_t stream) {
+  if (h->n != 1 || !words || !index) return fail(TG_E_INVAL, "tg_*1_py: a 1-env handle and a stream state");
+  if (*index > (uint32_t)MT_N)
+    return fail(TG_E_INVAL, "tg_*1_py: index %u outside [0, 624]", *index);
   if (const int rc = one_row(h)) return rc;
   if (!h->py) {
     if (hipHostMalloc((void**)&h->py, sizeof(tg_pystate), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -2406,8 +2425,21 @@ int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) 
   }
   // the device's cached generations serve the call iff the caller's state is the one the last
   // call returned (no other draws on the stream since: the user's own, another env's)
-  const bool warm = h->py_warm && memcmp(st, &h->py_last, sizeof(tg_pystate)) == 0;
-  if (!warm) memcpy(h->py, st, sizeof(tg_pystate));
+  const bool warm = h->py_warm && *index == h->py_last.index &&
+                    (!has_gauss || (*has_gauss == h->py_last.has_gauss &&
+                                    memcmp(gauss_next, &h->py_last.gauss_next, sizeof(double)) == 0)) &&
+                    memcmp(words, h->py_last.mt, sizeof h->py_last.mt) == 0;
+  if (!warm) {
+    memcpy(h->py->mt, words, sizeof h->py->mt);
+    h->py->index = *index;
+  }
+  if (has_gauss) {
+    h->py->has_gauss = *has_gauss;
+    h->py->gauss_next = *gauss_next;
+  }
+  const uint32_t q0 = *index;
+  const int hg = has_gauss ? (int)*has_gauss : 0;
+  const double gn = has_gauss ? *gauss_next : 0.0;
   // a step's tstep is its index; a reset's, the next step's (the new episode's start)
   const uint32_t tstep = RESET ? h->tstep : h->tstep++;
   h->py_warm = false;  // until the call has returned
@@ -2416,21 +2448,36 @@ int launch_py1(tg_batch* h, int32_t action, tg_pystate* st, hipStream_t stream) 
     c.kind = RESET ? SRV_RESET_PY : SRV_STEP_PY;
     c.action = action;
     c.tstep = tstep;
-    c.q0 = st->index;
-    c.has_gauss = (int32_t)st->has_gauss;
+    c.q0 = q0;
+    c.has_gauss = hg;
     c.warm = warm ? 1 : 0;
-    memcpy(&c.gauss_bits, &st->gauss_next, sizeof c.gauss_bits);
+    memcpy(&c.gauss_bits, &gn, sizeof c.gauss_bits);
     if (const int rc = srv_call(h, c, stream)) return rc;
   } else {
     hipLaunchKernelGGL(k_py1<RESET>, dim3(1), dim3(64), 0, stream, h->S, h->L, h->grid, (int)action,
-                       h->py_dev, warm ? h->pyc : nullptr, h->pyc, st->index, (int)st->has_gauss,
-                       st->gauss_next, h->one_dev, tstep, h->main.stats, h->err);
+                       h->py_dev, warm ? h->pyc : nullptr, h->pyc, q0, hg, gn, h->one_dev, tstep,
+                       h->main.stats, h->err);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(stream));
   }
-  memcpy(st, h->py, sizeof(tg_pystate));
-  h->py_last = *st;
+  memcpy(words, h->py->mt, sizeof h->py->mt);
+  *index = h->py->index;
+  memcpy(h->py_last.mt, words, sizeof h->py_last.mt);
+  h->py_last.index = *index;
+  if (has_gauss) {
+    *has_gauss = h->py->has_gauss;
+    *gauss_next = h->py->gauss_next;
+    h->py_last.has_gauss = *has_gauss;
+    h->py_last.gauss_next = *gauss_next;
+  }
   h->py_warm = true;
+  return TG_OK;
+}
+int row_out(const tg_batch* h, double* obs, int32_t* reward, uint8_t* valid, uint8_t* done) {
+  memcpy(obs, h->one->obs, sizeof h->one->obs);
+  *reward = h->one->reward;
+  *valid = h->one->valid;
+  *done = h->one->done;
   return TG_OK;
 }
 }  // namespace
@@ -2440,19 +2487,28 @@ extern "C" {
 int tg_step1_py(tg_batch* h, int32_t action, tg_pystate* st, double* obs, int32_t* reward,
                 uint8_t* valid, uint8_t* done, void* stream) {
   BIND_SERVE(h);
-  if (!obs || !reward || !valid || !done) return fail(TG_E_INVAL, "tg_step1_py: null output");
-  const int rc = launch_py1<false>(h, action, st, (hipStream_t)stream);
-  if (rc) return rc;
-  memcpy(obs, h->one->obs, sizeof h->one->obs);
-  *reward = h->one->reward;
-  *valid = h->one->valid;
-  *done = h->one->done;
-  return TG_OK;
+  if (!obs || !reward || !valid || !done || !st) return fail(TG_E_INVAL, "tg_step1_py: null output");
+  const int rc = launch_py1<false>(h, action, st->mt, &st->index, &st->has_gauss, &st->gauss_next,
+                                   (hipStream_t)stream);
+  return rc ? rc : row_out(h, obs, reward, valid, done);
+}
+
+int tg_step1_pywords(tg_batch* h, int32_t action, uint32_t* words, int32_t* index, double* obs,
+                     int32_t* reward, uint8_t* valid, uint8_t* done, void* stream) {
+  BIND_SERVE(h);
+  if (!obs || !reward || !valid || !done || !words || !index)
+    return fail(TG_E_INVAL, "tg_step1_pywords: null argument");
+  if (*index < 0) return fail(TG_E_INVAL, "tg_step1_pywords: index %d < 0", *index);
+  const int rc = launch_py1<false>(h, action, words, reinterpret_cast<uint32_t*>(index), nullptr,
+                                   nullptr, (hipStream_t)stream);
+  return rc ? rc : row_out(h, obs, reward, valid, done);
 }
 
 int tg_reset1_py(tg_batch* h, tg_pystate* st, double* obs, void* stream) {
   BIND_SERVE(h);
-  const int rc = launch_py1<true>(h, 0, st, (hipStream_t)stream);
+  if (!st) return fail(TG_E_INVAL, "tg_reset1_py: null stream state");
+  const int rc = launch_py1<true>(h, 0, st->mt, &st->index, &st->has_gauss, &st->gauss_next,
+                                  (hipStream_t)stream);
   if (rc) return rc;
   if (obs) memcpy(obs, h->one->obs, sizeof h->one->obs);
   return TG_OK;

@@ -64,7 +64,8 @@ struct SrvBox {
   uint32_t done;
   uint32_t pad2[3];
   uint64_t t_seen, t_end;  // TG_SERVE_TRACE: the server's clock at the command's pickup / answer
-  uint32_t pad3[8];
+  uint32_t ticks;          //   and the command's ticks
+  uint32_t pad3[7];
 };
 static_assert(sizeof(SrvBox) == 128, "SrvBox: two 64-B lines");
 
@@ -157,7 +158,7 @@ struct tg_batch {
   int64_t srv_t_last = 0;          // host clock (ns) at the last answer
   int64_t srv_launches = 0, srv_calls = 0;
   bool srv_trace = false;          // TG_SERVE_TRACE: sums printed at tg_destroy (diagnostic)
-  double srv_rt_ns = 0.0, srv_gpu_ns = 0.0, srv_post_ns = 0.0;
+  double srv_rt_ns = 0.0, srv_gpu_ns = 0.0, srv_post_ns = 0.0, srv_fit[3] = {0.0, 0.0, 0.0};
   tg::RenderState* rs = nullptr;   // tg_render_init
   std::vector<int> kst_k;          // steps each in-use step record covers (a k_flow launch: K)
   // TG_MODE_FLOW's work structures (tg_flow.h Flow; allocated at the first flow rollout)

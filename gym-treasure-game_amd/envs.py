@@ -585,6 +585,17 @@ class TreasureGame:
         self.viewer = None
         self._h_obs = np.zeros(_lib.OBS_DIM, np.float64)  # tg_step1's host outputs
         self._h_rew, self._h_valid, self._h_done = ctypes.c_int32(), ctypes.c_uint8(), ctypes.c_uint8()
+        # the step call's arguments, made once: a step is one C call and nothing else.  Its
+        # stream is the null stream: every TreasureGame call returns host data, so none of this
+        # env's device work is pending when a step starts.
+        self._step_args = (self._h_obs.ctypes.data, ctypes.byref(self._h_rew),
+                           ctypes.byref(self._h_valid), ctypes.byref(self._h_done), None)
+        # the shared stream's step works in place on the global random.Random's own words and
+        # index (tg_step1_pywords; _GlobalMT checked the layout): no getstate / setstate
+        self._pywords = None
+        if share_global_random and _GLOBAL_MT.ok:
+            base = id(_GLOBAL_MT._inst)
+            self._pywords = (base + _GLOBAL_MT._state, base + _GLOBAL_MT._index)
         if self._shared:
             self._py = _lib.PyState()
             # _TreasureGameImpl.__init__'s build draws from the global stream (IM/:31-53)
@@ -653,16 +664,19 @@ class TreasureGame:
         tg_step1_py over the global stream), one launch whose kernel writes the row into
         pinned host memory, one synchronisation"""
         v = self._vec
-        if self._shared:
+        if self._pywords is not None and random._inst is _GLOBAL_MT._inst:
+            rc = v._L.tg_step1_pywords(v.handle, a, *self._pywords, *self._step_args)
+            if rc:
+                check(rc, "tg_step1_pywords")
+        elif self._shared:
             self._load_global()
-            check(v._L.tg_step1_py(v.handle, int(a), ctypes.byref(self._py), self._h_obs.ctypes.data,
-                                   ctypes.byref(self._h_rew), ctypes.byref(self._h_valid),
-                                   ctypes.byref(self._h_done), v._stream()), "tg_step1_py")
+            check(v._L.tg_step1_py(v.handle, a, ctypes.byref(self._py), *self._step_args),
+                  "tg_step1_py")
             self._store_global()
         else:
-            check(v._L.tg_step1(v.handle, int(a), self._h_obs.ctypes.data,
-                                ctypes.byref(self._h_rew), ctypes.byref(self._h_valid),
-                                ctypes.byref(self._h_done), v._stream()), "tg_step1")
+            rc = v._L.tg_step1(v.handle, a, *self._step_args)
+            if rc:
+                check(rc, "tg_step1")
         r = int(self._h_rew.value) if self._h_valid.value else None
         return self._h_obs.tolist(), r, bool(self._h_done.value)
 

@@ -167,6 +167,15 @@ int tg_step1_py(tg_batch *h, int32_t action, tg_pystate *st, double *obs, int32_
                 uint8_t *valid, uint8_t *done, void *stream);
 int tg_reset1_py(tg_batch *h, tg_pystate *st, double *obs, void *stream);
 
+/* tg_step1_py over a stream state kept elsewhere: `words` (624 uint32) and `index` (int32,
+ * 0..624) are read at the call and written back advanced, in place -- for the N=1 drop-in,
+ * the words and index of CPython's global random.Random object itself (Modules/_randommodule.c
+ * keeps them as `int index; uint32_t state[624]`; the Python side checks the layout against
+ * random.getstate() first), so a step costs no getstate / setstate.  A step draws no gauss, so
+ * gauss_next is not an argument. */
+int tg_step1_pywords(tg_batch *h, int32_t action, uint32_t *words, int32_t *index, double *obs,
+                     int32_t *reward, uint8_t *valid, uint8_t *done, void *stream);
+
 /* K steps in one call with the on-device synthetic policy (TG_POLICY_*): step t0 + s takes
  * the actions tg_policy_actions(action_seed, t0 + s) would give, evaluated inside the step's
  * first kernel (no action launch, no host round trip).  Outputs are step-major: actions (may

@@ -14,13 +14,17 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _shared_run(tg, seed, serve, sleeps):
+def _shared_run(tg, seed, serve, sleeps, words=True):
     import pyref  # test infrastructure (oracle/), on sys.path via conftest
     saved = random.getstate()
     try:
         random.seed(seed)
         env = tg.TreasureGame()
         env._vec.set_serve(serve)
+        if words:  # steps in place on the global Random's words (tg_step1_pywords)
+            assert env._pywords is not None
+        else:  # steps through a tg_pystate (tg_step1_py), getstate / setstate around each
+            env._pywords = None
         ref = pyref.Env(seed)
         assert env.reset() == ref.reset()
         u = random.Random(seed + 1)
@@ -56,6 +60,8 @@ def test_serve_shared_stream_matches_launch_path(tg, monkeypatch, idle_us):
     on = _shared_run(tg, 31, True, sleeps=True)
     off = _shared_run(tg, 31, False, sleeps=False)
     assert on == off
+    assert _shared_run(tg, 31, True, sleeps=False, words=False) == on
+    assert _shared_run(tg, 31, False, sleeps=False, words=False) == on
 
 
 @pytest.mark.parametrize("idle_us", [None, "1"])
