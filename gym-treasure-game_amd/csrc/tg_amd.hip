@@ -1580,51 +1580,89 @@ __global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __re
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
-__global__ __launch_bounds__(64) void k_serve1(Soa S, Level L, const uint32_t* __restrict__ grid,
+// Resident for many commands, the server keeps in LDS what a step would otherwise fetch from
+// HBM each time, one dependent round trip apiece: the env's state (st4 / ang / ep: written back
+// to HBM when it leaves) and, when they fit (`stage`: 1 the GoTable, 2 get_state's quotient
+// table; dynamic LDS, sized at launch), the level's tables.
+constexpr uint32_t SRV_STAGE_GOTAB = 1u, SRV_STAGE_OBSQ = 2u;
+__global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t* __restrict__ grid,
                                                SrvBox* box, tg_pystate* py, uint32_t* pyc,
                                                TgOne* out, EpQueue q, int64_t g0, uint32_t idle,
-                                               int trace, unsigned long long* __restrict__ stats,
+                                               int trace, uint32_t stage,
+                                               unsigned long long* __restrict__ stats,
                                                uint32_t* __restrict__ err_or) {
   __shared__ __attribute__((aligned(16))) uint8_t win[WIN_WAVE_BYTES];
   __shared__ uint32_t W[PY_GENS * MT_N];
   __shared__ LdsLevel lv;
+  __shared__ uint4 st4_l;
+  __shared__ double2 ang_l;
+  __shared__ int2 ep_l;
+  extern __shared__ __attribute__((aligned(16))) uint8_t srv_dyn[];
   const int lane = threadIdx.x;
-  py_level(lv, L, grid);
+  py_level(lv, Lg, grid);
+  Level L = Lg;
+  if (stage & SRV_STAGE_OBSQ) {
+    double* const qd = reinterpret_cast<double*>(srv_dyn);
+    const int nq = Lg.qx_n + Lg.qy_n;
+    for (int i = lane; i < nq; i += 64) qd[i] = Lg.obs_q[i];
+    L.obs_q = qd;
+  }
+  if (stage & SRV_STAGE_GOTAB) {
+    uint32_t* const gd = reinterpret_cast<uint32_t*>(
+        srv_dyn + ((stage & SRV_STAGE_OBSQ) ? sizeof(double) * (size_t)(Lg.qx_n + Lg.qy_n) : 0));
+    const int ng = Lg.W * Lg.H * 32;
+    for (int i = lane; i < ng; i += 64) gd[i] = Lg.gotab[i];
+    L.gotab = gd;
+  }
+  if (lane == 0) {
+    st4_l = Sg.st4[0];
+    ang_l = Sg.ang[0];
+    ep_l = Sg.ep[0];
+  }
   __syncthreads();
+  const Soa S{&st4_l, &ang_l, &ep_l, Sg.mt, Sg.mc};
   const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
   bool ring = false;  // W holds the Python stream's ring
   uint32_t off = 0;
   uint32_t served = sys_load(&box->done);
   unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+  __shared__ TgOne row_l;  // the command's result row, written to host memory in one burst
+  TgOne* const row = &row_l;
   while (true) {
-    const uint32_t s = sys_load(&box->seq);
+    // the command group in one load (volatile: system scope, no cache)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 cg = *reinterpret_cast<const volatile u32x4*>(box);
+    const uint32_t s = __builtin_amdgcn_readfirstlane(cg.w);
     if (s == served) {
       if (__builtin_amdgcn_s_memrealtime() - t_last > idle) break;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the command's fields after its seq
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // what the host wrote before seq
     const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
     int ticks = 0;
-    const int32_t kind = (int32_t)sys_load((const uint32_t*)&box->kind);
+    const uint32_t word = __builtin_amdgcn_readfirstlane(cg.x);
+    const uint32_t kind = word & 15u;
     if (kind == SRV_QUIT) {
       served = s;
       break;
     }
-    const int action = (int)sys_load((const uint32_t*)&box->action);
-    const uint32_t tstep = sys_load(&box->tstep);
+    const int action = (int)((word >> 4) & 31u) - 16;
+    const uint32_t tstep = __builtin_amdgcn_readfirstlane(cg.y);
     if (kind == SRV_STEP) {
-      const StepIO io{nullptr, out->obs, &out->reward, &out->valid, &out->done, nullptr,
+      const StepIO io{nullptr, row->obs, &row->reward, &row->valid, &row->done, nullptr,
                       POL_IMMEDIATE, (uint64_t)(int64_t)action, 0, tstep};
       ticks = step_env<false, false, POL_IMMEDIATE>(S, 1, L, lv.trig, m, (lds_u8*)win, lane, io, q,
                                                     g0, stats, err_or).ticks;
     } else {
-      const uint32_t q0 = sys_load(&box->q0);
-      const int has_gauss = (int)sys_load((const uint32_t*)&box->has_gauss);
-      const bool warm = sys_load((const uint32_t*)&box->warm) != 0u;
-      const uint64_t gb = (uint64_t)sys_load((const uint32_t*)&box->gauss_bits) |
-                          (uint64_t)sys_load((const uint32_t*)&box->gauss_bits + 1) << 32;
-      const double gauss_next = __builtin_bit_cast(double, gb);
+      const bool warm = (word >> 9) & 1u;
+      const int has_gauss = (int)((word >> 10) & 1u);
+      const uint32_t q0 = word >> 11;
+      double gauss_next = 0.0;
+      if (kind == SRV_RESET_PY) {
+        const uint32_t* gp = reinterpret_cast<const uint32_t*>(&box->gauss_bits);
+        gauss_next = __builtin_bit_cast(double, (uint64_t)sys_load(gp) | (uint64_t)sys_load(gp + 1) << 32);
+      }
       if (!ring || !warm) {  // a new server, or draws on the stream since the last call
         if (warm) {
           for (int i = lane; i < PY_GENS * MT_N; i += 64) W[i] = pyc[i];
@@ -1636,12 +1674,15 @@ __global__ __launch_bounds__(64) void k_serve1(Soa S, Level L, const uint32_t* _
         ring = true;
       }
       if (kind == SRV_RESET_PY)
-        py_call<true>(S, L, lv, W, off, 0, py, q0, has_gauss, gauss_next, out, tstep, stats, err_or,
+        py_call<true>(S, L, lv, W, off, 0, py, q0, has_gauss, gauss_next, row, tstep, stats, err_or,
                       &ticks);
       else
-        py_call<false>(S, L, lv, W, off, action, py, q0, has_gauss, gauss_next, out, tstep, stats,
+        py_call<false>(S, L, lv, W, off, action, py, q0, has_gauss, gauss_next, row, tstep, stats,
                        err_or, &ticks);
     }
+    __syncthreads();
+    if (lane < (int)(sizeof(TgOne) / 8))
+      reinterpret_cast<uint64_t*>(out)[lane] = reinterpret_cast<const uint64_t*>(row)[lane];
     // the row and the state (host memory; the env's state and MT ring in HBM for the next
     // command) before the answer
     if (trace && lane == 0) {
@@ -1649,8 +1690,7 @@ __global__ __launch_bounds__(64) void k_serve1(Soa S, Level L, const uint32_t* _
       box->t_end = __builtin_amdgcn_s_memrealtime();
       box->ticks = (uint32_t)ticks;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __syncthreads();
+    __syncthreads();  // (the release below covers the row the lanes wrote: one wave)
     if (lane == 0) __hip_atomic_store(&box->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     served = s;
@@ -1659,6 +1699,12 @@ __global__ __launch_bounds__(64) void k_serve1(Soa S, Level L, const uint32_t* _
   if (ring)
     for (int j = 0; j < PY_GENS; ++j)
       for (int i = lane; i < MT_N; i += 64) pyc[j * MT_N + i] = W[((j + off) % PY_GENS) * MT_N + i];
+  __syncthreads();
+  if (lane == 0) {
+    Sg.st4[0] = st4_l;
+    Sg.ang[0] = ang_l;
+    Sg.ep[0] = ep_l;
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
   if (lane == 0) __hip_atomic_store(&box->done, served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1925,8 +1971,8 @@ void tg_destroy(tg_batch* h) {
     const double n = (double)h->srv_calls, sk = h->srv_fit[0], skk = h->srv_fit[1];
     const double sg = h->srv_gpu_ns, sgk = h->srv_fit[2];
     const double b = (n * sgk - sk * sg) / (n * skk - sk * sk), a = (sg - b * sk) / n;
-    fprintf(stderr, "[serve] ticks per command %.2f; server time = %.2f us + %.3f us x ticks\n",
-            sk / n, a / 1e3, b / 1e3);
+    fprintf(stderr, "[serve] ticks per command %.2f; server time = %.2f us + %.3f us x ticks "
+            "(level tables in LDS: %d, %zu B)\n", sk / n, a / 1e3, b / 1e3, h->srv_stage, h->srv_dyn);
   }
   if (h->srv_ev) (void)hipEventDestroy(h->srv_ev);
   if (h->srv_dep) (void)hipEventDestroy(h->srv_dep);
@@ -2280,9 +2326,37 @@ int srv_start(tg_batch* h, hipStream_t caller) {
   HIP_TRY(hipEventRecord(h->srv_dep, caller));
   HIP_TRY(hipStreamWaitEvent(h->srv_st, h->srv_dep, 0));
   const EpQueue q{h->eps, h->eps_count, h->eps_cap};
-  hipLaunchKernelGGL(k_serve1, dim3(1), dim3(64), 0, h->srv_st, h->S, h->L, h->grid, h->box_dev,
-                     h->py_dev, h->pyc, h->one_dev, q, h->g0, h->srv_idle, (int)h->srv_trace,
-                     h->main.stats, h->err);
+  if (h->srv_stage < 0) {  // the level's tables into the server's LDS, those that fit
+    hipFuncAttributes fa{};
+    int dev_max = 0;
+    HIP_TRY(hipFuncGetAttributes(&fa, (const void*)k_serve1));
+    HIP_TRY(hipDeviceGetAttribute(&dev_max, hipDeviceAttributeMaxSharedMemoryPerBlock, h->device));
+    const size_t room = dev_max > (int)fa.sharedSizeBytes ? (size_t)dev_max - fa.sharedSizeBytes : 0;
+    const size_t qb = h->L.obs_q ? sizeof(double) * (size_t)(h->L.qx_n + h->L.qy_n) : 0;
+    const size_t gb = h->L.gotab ? sizeof(uint32_t) * (size_t)h->L.W * h->L.H * 32 : 0;
+    uint32_t stage = 0;
+    size_t dyn = 0;
+    if (qb && qb <= room) {
+      stage |= SRV_STAGE_OBSQ;
+      dyn += qb;
+    }
+    if (gb && dyn + gb <= room) {
+      stage |= SRV_STAGE_GOTAB;
+      dyn += gb;
+    }
+    if (dyn > 65536 &&
+        hipFuncSetAttribute((const void*)k_serve1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)dyn) != hipSuccess) {
+      (void)hipGetLastError();
+      stage = qb && qb <= 65536 ? SRV_STAGE_OBSQ : 0u;
+      dyn = stage ? qb : 0;
+    }
+    h->srv_stage = (int)stage;
+    h->srv_dyn = dyn;
+  }
+  hipLaunchKernelGGL(k_serve1, dim3(1), dim3(64), h->srv_dyn, h->srv_st, h->S, h->L, h->grid,
+                     h->box_dev, h->py_dev, h->pyc, h->one_dev, q, h->g0, h->srv_idle,
+                     (int)h->srv_trace, (uint32_t)h->srv_stage, h->main.stats, h->err);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(h->srv_ev, h->srv_st));
   h->srv_live = true;
@@ -2303,12 +2377,8 @@ int srv_call(tg_batch* h, const SrvBox& c, hipStream_t caller) {
   }
   SrvBox* const b = h->box;
   const uint32_t seq = ++h->srv_seq;
-  b->kind = c.kind;
-  b->action = c.action;
+  b->word = c.word;
   b->tstep = c.tstep;
-  b->q0 = c.q0;
-  b->has_gauss = c.has_gauss;
-  b->warm = c.warm;
   b->gauss_bits = c.gauss_bits;
   const int64_t tp = h->srv_trace ? now_ns() : 0;
   __atomic_store_n(&b->seq, seq, __ATOMIC_RELEASE);
@@ -2350,7 +2420,7 @@ int srv_stop(tg_batch* h) {
   h->srv_live = false;
   if (hipEventQuery(h->srv_ev) != hipSuccess) {
     SrvBox* const b = h->box;
-    b->kind = SRV_QUIT;
+    b->word = srv_word(SRV_QUIT, 0, false, false, 0);
     __atomic_store_n(&b->seq, ++h->srv_seq, __ATOMIC_RELEASE);
   }
   HIP_TRY(hipEventSynchronize(h->srv_ev));
@@ -2371,8 +2441,7 @@ int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t*
   hipStream_t st = (hipStream_t)stream;
   if (h->serve) {
     SrvBox c{};
-    c.kind = SRV_STEP;
-    c.action = action;
+    c.word = srv_word(SRV_STEP, action, false, false, 0);
     c.tstep = h->tstep++;
     if (const int rc = srv_call(h, c, st)) return rc;
   } else {
@@ -2445,12 +2514,8 @@ int launch_py1(tg_batch* h, int32_t action, uint32_t* words, uint32_t* index, ui
   h->py_warm = false;  // until the call has returned
   if (h->serve) {
     SrvBox c{};
-    c.kind = RESET ? SRV_RESET_PY : SRV_STEP_PY;
-    c.action = action;
+    c.word = srv_word(RESET ? SRV_RESET_PY : SRV_STEP_PY, action, warm, hg != 0, q0);
     c.tstep = tstep;
-    c.q0 = q0;
-    c.has_gauss = hg;
-    c.warm = warm ? 1 : 0;
     memcpy(&c.gauss_bits, &gn, sizeof c.gauss_bits);
     if (const int rc = srv_call(h, c, stream)) return rc;
   } else {

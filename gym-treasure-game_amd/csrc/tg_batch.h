@@ -44,23 +44,26 @@ struct TgOne {
   int32_t reward;
   uint8_t valid, done;
 };
+static_assert(sizeof(TgOne) == 80, "TgOne: ten 8-B words (k_serve1 copies it out by word)");
 
 // The N = 1 server's mailbox (k_serve1, tg_amd.hip): pinned, coherent host memory.  Line 0 is
-// the host's (a command's fields, then seq), line 1 the server's (done: the last command it
-// served; a server that starts reads it, so a command posted while none ran is served by the
-// next one).
-enum : int32_t { SRV_STEP = 1, SRV_STEP_PY = 2, SRV_RESET_PY = 3, SRV_QUIT = 4 };
+// the host's: a command is one 16-B group (seq last: the server reads the group with one load,
+// and a group whose seq is new carries the command's fields) and, for a reset, gauss_next
+// (read after the group).  Line 1 is the server's: done, the last command it served (a server
+// that starts reads it, so a command posted while none ran is served by the next one).
+enum : uint32_t { SRV_STEP = 1, SRV_STEP_PY = 2, SRV_RESET_PY = 3, SRV_QUIT = 4 };
+// the command word: kind | (action + 16) << 4 | warm << 9 | has_gauss << 10 | q0 << 11
+inline uint32_t srv_word(uint32_t kind, int32_t action, bool warm, bool has_gauss, uint32_t q0) {
+  return kind | (uint32_t)((action + 16) & 31) << 4 | (warm ? 1u : 0u) << 9 |
+         (has_gauss ? 1u : 0u) << 10 | (q0 & 1023u) << 11;
+}
 struct SrvBox {
-  uint32_t seq;         // the last command posted
-  int32_t kind;         // SRV_*
-  int32_t action;
+  uint32_t word;        // srv_word
   uint32_t tstep;       // the step's index (h->tstep)
-  uint32_t q0;          // SRV_*_PY: the caller's index and gauss_next, and whether the device's
-  int32_t has_gauss;    //   generations are the caller's (tg_batch::py_warm)
-  int32_t warm;
-  int32_t pad0;
-  uint64_t gauss_bits;
-  uint8_t pad1[64 - 40];
+  uint32_t pad0;
+  uint32_t seq;         // the last command posted (written last)
+  uint64_t gauss_bits;  // SRV_RESET_PY: the caller's gauss_next
+  uint8_t pad1[64 - 24];
   uint32_t done;
   uint32_t pad2[3];
   uint64_t t_seen, t_end;  // TG_SERVE_TRACE: the server's clock at the command's pickup / answer
@@ -157,6 +160,8 @@ struct tg_batch {
   uint32_t srv_seq = 0;
   int64_t srv_t_last = 0;          // host clock (ns) at the last answer
   int64_t srv_launches = 0, srv_calls = 0;
+  int srv_stage = -1;              // the level tables the server keeps in LDS (k_serve1 stage; -1:
+  size_t srv_dyn = 0;              //   not chosen yet) and their dynamic LDS bytes
   bool srv_trace = false;          // TG_SERVE_TRACE: sums printed at tg_destroy (diagnostic)
   double srv_rt_ns = 0.0, srv_gpu_ns = 0.0, srv_post_ns = 0.0, srv_fit[3] = {0.0, 0.0, 0.0};
   tg::RenderState* rs = nullptr;   // tg_render_init
