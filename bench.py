@@ -190,25 +190,30 @@ def dropin_latency(tg, steps=300, seed=0):
     """The N=1 drop-in's own hot call: TreasureGame.step(a) (TG/:91-96) from Python, one env on
     the GPU, uniform random actions from a host RNG, resetting when done; mean µs per call.
     Both construction modes: TreasureGame() draws from Python's global random as the reference
-    does (tg_step1_py: the stream state goes in and out with the launch), TreasureGame(seed=s)
-    from the env's own stream (tg_step1); each is one launch and one synchronisation."""
+    does (tg_step1_pywords: the global Random's words and index in place), TreasureGame(seed=s)
+    from the env's own stream (tg_step1).  Each call is served by the resident server kernel
+    (k_serve1, the default); the ``launch_per_call`` figures are the same calls with serving
+    off (one launch and one synchronisation each, tg_set_serve(0))."""
     import random
     out = {"steps": steps, "api": "TreasureGame.step, host RNG actions, synchronous"}
     saved = random.getstate()
     try:
-        for mode in ("shared_global_random", "private_stream"):
-            random.seed(seed)
-            env = tg.TreasureGame() if mode == "shared_global_random" else tg.TreasureGame(seed=seed)
-            env.reset()
-            r = random.Random(seed)
-            for _ in range(20):
-                env.step(r.randrange(9))
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                if env.step(r.randrange(9))[2]:
-                    env.reset()
-            out[mode + "_step_us"] = (time.perf_counter() - t0) / steps * 1e6
-            env.close()
+        for serve in (True, False):
+            for mode in ("shared_global_random", "private_stream"):
+                random.seed(seed)
+                env = tg.TreasureGame() if mode == "shared_global_random" else tg.TreasureGame(seed=seed)
+                env._vec.set_serve(serve)
+                env.reset()
+                r = random.Random(seed)
+                for _ in range(20):
+                    env.step(r.randrange(9))
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    if env.step(r.randrange(9))[2]:
+                        env.reset()
+                key = mode + "_step_us" if serve else "launch_per_call_" + mode + "_step_us"
+                out[key] = (time.perf_counter() - t0) / steps * 1e6
+                env.close()
     finally:
         random.setstate(saved)
     out["step_us"] = out["shared_global_random_step_us"]  # the default TreasureGame()
