@@ -531,10 +531,18 @@ class Runner:
         self.timing = True
         if self.world > 1:
             dist.barrier()
-        torch.cuda.synchronize(self.dev)
         # HIP events on the step's stream (torch's current stream, which the steps use) around
         # the whole timed region: two records, none between kernels
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if os.environ.get("TG_BENCH_PRESPIN", "1") != "0":
+            # the synchronisation before the region as a spin on an event: a blocking wait let
+            # the host thread sleep, and the region's first launch then ran on a cold core
+            # (~58 us from ev0 to the first kernel's GPU start)
+            evs = torch.cuda.Event()
+            evs.record()
+            while not evs.query():
+                pass
+        torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
         ev0.record()
         if self.K:

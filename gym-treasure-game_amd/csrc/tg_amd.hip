@@ -17,6 +17,7 @@
 #include <cstdarg>
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <cstdlib>
 #include <unistd.h>
 #include <cstdio>
@@ -36,6 +37,9 @@ thread_local std::string g_err;
 }
 #endif
 using namespace tg;
+namespace {
+void srv_register(tg_batch* h, bool live);  // the exit-time server registry (below)
+}
 
 namespace {
 
@@ -1962,6 +1966,7 @@ void tg_destroy(tg_batch* h) {
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != h->device) (void)hipSetDevice(h->device);
   if (h->srv_live) (void)srv_stop(h);
+  srv_register(h, false);
   if (h->srv_trace && h->srv_calls)
     fprintf(stderr, "[serve] calls %lld launches %lld: mean per call %.2f us to post, %.2f us post -> "
             "answer, of which %.2f us between the server's pickup and its answer\n",
@@ -2360,6 +2365,7 @@ int srv_start(tg_batch* h, hipStream_t caller) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(h->srv_ev, h->srv_st));
   h->srv_live = true;
+  srv_register(h, true);
   h->srv_t_last = now_ns();
   ++h->srv_launches;
   return TG_OK;
@@ -2414,15 +2420,45 @@ int srv_call(tg_batch* h, const SrvBox& c, hipStream_t caller) {
 }
 }  // namespace
 
+namespace {
+// Handles whose server may be running.  At exit (the library's static destructors run before
+// those of libamdhip64, which it depends on) every one still running is told to quit and waited
+// for, at most a second each: no server outlives the process's pinned mailbox.
+std::mutex g_srv_mu;
+std::vector<tg_batch*> g_srv_handles;
+void srv_register(tg_batch* h, bool live) {
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  auto it = std::find(g_srv_handles.begin(), g_srv_handles.end(), h);
+  if (live && it == g_srv_handles.end()) g_srv_handles.push_back(h);
+  if (!live && it != g_srv_handles.end()) g_srv_handles.erase(it);
+}
+void srv_post_quit(tg_batch* h) {
+  SrvBox* const b = h->box;
+  b->word = srv_word(SRV_QUIT, 0, false, false, 0);
+  __atomic_store_n(&b->seq, ++h->srv_seq, __ATOMIC_RELEASE);
+}
+struct SrvReaper {
+  ~SrvReaper() {
+    std::lock_guard<std::mutex> lk(g_srv_mu);
+    for (tg_batch* h : g_srv_handles) {
+      if (!h->srv_live || hipSetDevice(h->device) != hipSuccess) continue;
+      if (hipEventQuery(h->srv_ev) == hipErrorNotReady) srv_post_quit(h);
+      const int64_t t0 = now_ns();
+      while (hipEventQuery(h->srv_ev) == hipErrorNotReady && now_ns() - t0 < 1000000000ll) {
+      }
+      h->srv_live = false;
+    }
+    g_srv_handles.clear();
+  }
+} g_srv_reaper;
+}  // namespace
+
 namespace tg {
 int srv_stop(tg_batch* h) {
   if (!h->srv_live) return TG_OK;
   h->srv_live = false;
-  if (hipEventQuery(h->srv_ev) != hipSuccess) {
-    SrvBox* const b = h->box;
-    b->word = srv_word(SRV_QUIT, 0, false, false, 0);
-    __atomic_store_n(&b->seq, ++h->srv_seq, __ATOMIC_RELEASE);
-  }
+  srv_register(h, false);
+  if (hipEventQuery(h->srv_ev) != hipSuccess) srv_post_quit(h);
   HIP_TRY(hipEventSynchronize(h->srv_ev));
   // gone: a QUIT it left (idle) without reading is void, not a command for the next server
   h->box->done = h->box->seq;

@@ -102,3 +102,25 @@ def test_serve_toggle_mid_episode(tg, oracle):
         rs, rr, rd, _ = ref.step(a)
         assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)) and (r, d) == (rr, rd), t
     env.close()
+
+
+def test_process_exits_with_the_server_resident(tmp_path):
+    """A process that ends with a server still running (idle limit 1 s, no close(); the env is
+    kept alive past interpreter teardown) exits cleanly and promptly: the library stops live
+    servers at unload (tg_amd.hip SrvReaper)"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, builtins; sys.path.insert(0, %r); import gym_treasure_game_amd as tg\n"
+            "env = tg.TreasureGame(seed=1); env.reset()\n"
+            "for i in range(50): env.step(i %% 9)\n"
+            "builtins._tg_keep = env\n"
+            "print('stepped', flush=True)\n" % root)
+    env = dict(os.environ, TG_SERVE_IDLE_US="1000000")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "stepped" in r.stdout
+    assert time.time() - t0 < 100
