@@ -1227,6 +1227,12 @@ constexpr int REGEN_STEPS = 16;
 constexpr int RCTR_LIST = 8;
 constexpr int RCTR_N = 16;
 #ifndef TG_FLOW_TU  // (the other kernels: the main unit only; tg_flow.hip compiles k_flow alone)
+// k_regen's ring stores: non-temporal (its words and codes are read steps later, not by this
+// launch) with TG_REGEN_NT=1
+#ifndef TG_REGEN_NT
+#define TG_REGEN_NT 0
+#endif
+constexpr bool REGEN_NT = TG_REGEN_NT != 0;
 __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restrict__ refill,
                                                  int64_t rcap, int32_t* __restrict__ ctr,
                                                  int32_t* __restrict__ ctr_next,
@@ -1283,8 +1289,8 @@ __global__ __launch_bounds__(BLOCK) void k_regen(Soa S, const uint32_t* __restri
       const uint32_t dst = (uint32_t)MT_HALF - mt_half(s & MT_POS_MASK);
       TwistIn t;
       twist_load(src_of(env, s), t);
-      twist_chain(t, (glb_u32*)(S.mt + (int64_t)env * MT_STORE), S.mc + (int64_t)env * MT_CODES,
-                  (int)(dst / (uint32_t)MT_N), MT_HALF_GENS, true, scr);
+      twist_chain<REGEN_NT>(t, (glb_u32*)(S.mt + (int64_t)env * MT_STORE), S.mc + (int64_t)env * MT_CODES,
+                            (int)(dst / (uint32_t)MT_N), MT_HALF_GENS, true, scr);
       ++halves;
     }
   }

@@ -24,6 +24,13 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 
+// a ring store: plain, or non-temporal (NT: k_regen, whose words and codes are read steps later,
+// not by this launch)
+template <bool NT, class P, class T>
+__device__ __forceinline__ void ring_store(P* p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 __device__ __forceinline__ void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -34,6 +41,7 @@ __device__ __forceinline__ void wave_fence() {
 // A generation's 312 draw codes from its words in LDS: draw d = r * 64 + lane per round, its
 // two words one 8-B LDS read (consecutive lanes, consecutive 8 B: no bank conflict, where a
 // 4-B read of every other word conflicted 2-way), its code one byte of a coalesced 64-B store.
+template <bool NT = false>
 __device__ __forceinline__ void codes_from_lds(const lds_u32* w, uint8_t* dst_c) {
   const int lane = threadIdx.x & 63;
   const lds_u64* const wl = reinterpret_cast<const lds_u64*>(w) + lane;
@@ -43,8 +51,9 @@ __device__ __forceinline__ void codes_from_lds(const lds_u32* w, uint8_t* dst_c)
     if (r < MT_N / 2 / 64 || lane < MT_N / 2 - 64 * (MT_N / 2 / 64)) {
       const uint64_t p = wl[64 * r];  // words 128 r + 2 lane (low) and + 1
       const uint32_t w0 = (uint32_t)p, a = mt_temper(w0) >> 5;
-      cl[64 * r] = (uint8_t)(__builtin_expect(top27_slow(a), 0) ? draw_code(mt_double(w0, (uint32_t)(p >> 32)))
-                                                                  : top27_code(a));
+      ring_store<NT>(cl + 64 * r,
+                     (uint8_t)(__builtin_expect(top27_slow(a), 0) ? draw_code(mt_double(w0, (uint32_t)(p >> 32)))
+                                                                  : top27_code(a)));
     }
   }
 }
@@ -79,6 +88,7 @@ __device__ __forceinline__ void twist_load(const glb_u32* src, TwistIn& t) {
 constexpr int TWIST_GROUP = 3;
 // the generation after the one in t (registers), into scratch (LDS) and, unless null, dst
 // (HBM), then, unless dst_c is null, its codes (dst / dst_c wave-uniform)
+template <bool NT = false>
 __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint8_t* dst_c,
                                             lds_u32* scratch) {
   const int lane = threadIdx.x & 63;
@@ -92,7 +102,7 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
         const uint32_t cc = p < MT_N - MT_M ? t.c[r < 4 ? r : 0] : scratch[p - (MT_N - MT_M)];
         const uint32_t w = twist_word(t.a[r], bb, cc);
         scratch[p] = w;
-        if (dst) dst[p] = w;
+        if (dst) ring_store<NT>(dst + p, w);
       }
     }
     // the group visible to later groups, whose lanes read what other lanes wrote: a
@@ -101,7 +111,7 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
     // s_waitcnt lgkmcnt(0) after every round: 0.1322 vs 0.1340 ms)
     wave_fence();
   }
-  if (dst_c) codes_from_lds(scratch, dst_c);
+  if (dst_c) codes_from_lds<NT>(scratch, dst_c);
 }
 // The next generation in place in LDS (s: a generation -> its successor), stored to dst with
 // its codes.  Round r reads words p + 1 (old: round r + 1 writes it, for lane 63), p + 397
@@ -109,6 +119,7 @@ __device__ __forceinline__ void twist_store(const TwistIn& t, glb_u32* dst, uint
 // writes p.  A group's reads are all issued before its writes (the compiler barrier: one
 // wave's LDS operations execute in order), so round r + 1's write cannot overtake round r's
 // read of word 64 (r + 1).  dst / dst_c as twist_store.  Must be reached by all 64 lanes.
+template <bool NT = false>
 __device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst_c) {
   const int lane = threadIdx.x & 63;
   wave_fence();  // the previous codes pass's reads of s before this twist's writes
@@ -131,12 +142,12 @@ __device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst
       const int p = r * 64 + lane;
       if (p < MT_N) {
         s[p] = w[r - r0];
-        if (dst) dst[p] = w[r - r0];
+        if (dst) ring_store<NT>(dst + p, w[r - r0]);
       }
     }
     wave_fence();
   }
-  if (dst_c) codes_from_lds(s, dst_c);
+  if (dst_c) codes_from_lds<NT>(s, dst_c);
 }
 // `gens` generations in sequence after the one in t, ring generations g0, g0 + 1, ... of an env
 // whose stored words start at w and codes at c: each one's codes, and the words of the even
@@ -145,12 +156,13 @@ __device__ __forceinline__ void twist_lds(lds_u32* s, glb_u32* dst, uint8_t* dst
 // stored nor coded).  The first twist from registers, the rest chained in the wave's LDS
 // scratch, so a half's regeneration reads one generation from HBM.  w / c wave-uniform; must
 // be reached by all 64 lanes.
+template <bool NT = false>
 __device__ __forceinline__ void twist_chain(const TwistIn& t, glb_u32* w, uint8_t* c, int g0, int gens,
                                             bool lead, lds_u32* scratch) {
   auto wd = [&](int g) { return (g & 1) ? (glb_u32*)nullptr : w + mt_store_off((uint32_t)g); };
-  if (lead) twist_store(t, nullptr, nullptr, scratch);
-  else twist_store(t, wd(g0), c + g0 * (MT_N / 2), scratch);
-  for (int j = lead ? 0 : 1; j < gens; ++j) twist_lds(scratch, wd(g0 + j), c + (g0 + j) * (MT_N / 2));
+  if (lead) twist_store<NT>(t, nullptr, nullptr, scratch);
+  else twist_store<NT>(t, wd(g0), c + g0 * (MT_N / 2), scratch);
+  for (int j = lead ? 0 : 1; j < gens; ++j) twist_lds<NT>(scratch, wd(g0 + j), c + (g0 + j) * (MT_N / 2));
 }
 __device__ __forceinline__ void wave_twist_gens(const glb_u32* src, glb_u32* w, uint8_t* c, int g0,
                                                 int gens, bool lead, lds_u32* scratch) {
