@@ -1430,17 +1430,40 @@ struct PyRng {
   uint32_t lo;     // oldest generation held
   uint32_t draws;
   uint32_t off;    // the ring's rotation (k_serve1 keeps the ring in LDS across calls)
+  // the generation holding the next word, its slot and the word's index there (set up at the
+  // first draw; a draw crosses into the next generation only every 312 draws)
+  uint32_t gc = 0u, qi = 0u;
+  const uint32_t* cs = nullptr;
   __device__ __forceinline__ uint32_t* slot(uint32_t g) const { return w + ((g + off) % PY_GENS) * MT_N; }
-  __device__ __forceinline__ uint32_t word(uint32_t pos) {
-    const uint32_t g = pos / MT_N;
+  __device__ __forceinline__ const uint32_t* gen(uint32_t g) {
     while (g >= lo + PY_GENS) {  // > 2 generations in one call (long levels): twist in place
       twist_gen(slot(lo + PY_GENS - 1), slot(lo));
       ++lo;
     }
-    return slot(g)[pos - g * MT_N];
+    return slot(g);
+  }
+  __device__ __forceinline__ uint32_t next_word() {
+    if (qi == (uint32_t)MT_N) {
+      cs = gen(++gc);
+      qi = 0u;
+    }
+    return cs[qi++];
   }
   __device__ __forceinline__ double random() {
-    const uint32_t a = word(q), b = word(q + 1);
+    if (!cs) {
+      gc = q / MT_N;
+      qi = q - gc * MT_N;
+      cs = gen(gc);
+    }
+    uint32_t a, b;
+    if (qi + 2u <= (uint32_t)MT_N) {  // both words in the current generation
+      a = cs[qi];
+      b = cs[qi + 1u];
+      qi += 2u;
+    } else {
+      a = next_word();
+      b = next_word();
+    }
     q += 2;
     ++draws;
     return mt_double(a, b);
@@ -1480,13 +1503,14 @@ __device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const 
                                             tg_pystate* py, uint32_t q0, int has_gauss,
                                             double gauss_next, TgOne* out, uint32_t tstep,
                                             unsigned long long* __restrict__ stats,
-                                            uint32_t* __restrict__ err_or, int* ticks = nullptr) {
+                                            uint32_t* __restrict__ err_or, int* ticks = nullptr,
+                                            const uint32_t* mk = nullptr) {
   __shared__ uint32_t out_g, out_lo, out_idx;
   const int lane = threadIdx.x;
   StepResult r{0, 0, 0, 0};
   uint32_t draws = 0;
   if (lane == 0) {
-    const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
+    const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H, mk};
     PyRng rng{W, q0, 0u, 0u, off};
     Env e;
     unpack(S.st4[0], S.ang[0], e);
@@ -1607,9 +1631,13 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
   __shared__ uint4 st4_l;
   __shared__ double2 ang_l;
   __shared__ int2 ep_l;
+  __shared__ uint32_t mk_l[MK_MAX_WORDS];  // the level bitmasks (Map::mk), as k_run's
   extern __shared__ __attribute__((aligned(16))) uint8_t srv_dyn[];
   const int lane = threadIdx.x;
   py_level(lv, Lg, grid);
+  if (Lg.masks)
+    for (int i = lane; i < mk_words(Lg.W, Lg.H); i += 64) mk_l[i] = Lg.masks[i];
+  const uint32_t* const mk = Lg.masks ? mk_l : nullptr;
   Level L = Lg;
   if (stage & SRV_STAGE_OBSQ) {
     double* const qd = reinterpret_cast<double*>(srv_dyn);
@@ -1631,7 +1659,7 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
   }
   __syncthreads();
   const Soa S{&st4_l, &ang_l, &ep_l, Sg.mt, Sg.mc};
-  const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H};
+  const Map m{reinterpret_cast<const uint8_t*>(lv.grid), L.W, L.H, mk};
   bool ring = false;  // W holds the Python stream's ring
   uint32_t off = 0;
   uint32_t served = sys_load(&box->done);
@@ -1685,10 +1713,10 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
       }
       if (kind == SRV_RESET_PY)
         py_call<true>(S, L, lv, W, off, 0, py, q0, has_gauss, gauss_next, row, tstep, stats, err_or,
-                      &ticks);
+                      &ticks, mk);
       else
         py_call<false>(S, L, lv, W, off, action, py, q0, has_gauss, gauss_next, row, tstep, stats,
-                       err_or, &ticks);
+                       err_or, &ticks, mk);
     }
     __syncthreads();
     if (lane < (int)(sizeof(TgOne) / 8))
