@@ -677,6 +677,21 @@ __device__ __forceinline__ void wave_stats(unsigned long long* __restrict__ part
   }
 }
 
+// wave_stats for a wave whose only live lane is lane 0 (k_py1, k_serve1): lane 0's own values,
+// no cross-lane reductions (~0.5 us of a one-env call)
+__device__ __forceinline__ void lane0_stats(unsigned long long* __restrict__ part, int steps,
+                                            int valid, int ticks, int draws, int episodes,
+                                            int regens = 0, bool wave_ticks = false) {
+  if ((threadIdx.x & 63) != 0) return;
+  unsigned long long* const slot = part + (size_t)blockIdx.x * ST_COUNT;
+  const int v[5] = {steps, valid, ticks, draws, episodes};
+#pragma unroll
+  for (int c = 0; c < 5; ++c)
+    if (v[c]) atomicAdd(&slot[c], (unsigned long long)v[c]);
+  if (regens) atomicAdd(&slot[ST_REGENS], (unsigned long long)regens);
+  if (wave_ticks && ticks) atomicAdd(&slot[ST_WTICKS], (unsigned long long)ticks);
+}
+
 // finish one env-step: obs/reward/valid/done rows, episode counters, optional auto-reset.
 // keep != nullptr: the obs row is returned there instead of stored (the caller stores it).
 // The option waves' epilogue computes its obs rows by f64 division: the quotient table
@@ -743,7 +758,7 @@ constexpr int POL_IMMEDIATE = -2;  // k_step's action is io.a0 (tg_step1), not a
 // One step of env i (lane i's; live iff i < n) with the level in LDS (trig, m) and the wave's
 // code window wscr: k_step's body, also k_serve1's private-stream step.  Every lane of the wave
 // must reach it.
-template <bool AUTORESET, bool FINAL, int POL>
+template <bool AUTORESET, bool FINAL, int POL, bool ONE = false>  // ONE: only lane 0 live (k_serve1)
 __device__ __forceinline__ StepResult step_env(const Soa& S, int64_t n, const Level& L,
                                          const uint32_t* trig, const Map& m, lds_u8* wscr,
                                          int64_t i, const StepIO& io, const EpQueue& q,
@@ -789,8 +804,12 @@ __device__ __forceinline__ StepResult step_env(const Soa& S, int64_t n, const Le
     S.ang[i] = make_double2(e.ang0, e.ang1);
     if (ep.x != ep_in.x || ep.y != ep_in.y) S.ep[i] = ep;  // a reward-None step changes nothing
   }
-  wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
-              __popcll(need) + wave_sum(lregen), true);
+  if constexpr (ONE)
+    lane0_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
+                __popcll(need) + lregen, true);
+  else
+    wave_stats(stats, live ? 1 : 0, r.ran, r.ticks, (int)draws, AUTORESET ? (live && r.done) : 0,
+               __popcll(need) + wave_sum(lregen), true);
   return r;
 }
 
@@ -1504,7 +1523,8 @@ __device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const 
                                             double gauss_next, TgOne* out, uint32_t tstep,
                                             unsigned long long* __restrict__ stats,
                                             uint32_t* __restrict__ err_or, int* ticks = nullptr,
-                                            const uint32_t* mk = nullptr) {
+                                            const uint32_t* mk = nullptr,
+                                            unsigned long long* stamps = nullptr) {
   __shared__ uint32_t out_g, out_lo, out_idx;
   const int lane = threadIdx.x;
   StepResult r{0, 0, 0, 0};
@@ -1516,6 +1536,7 @@ __device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const 
     unpack(S.st4[0], S.ang[0], e);
     int2 ep = S.ep[0];
     double o[9];
+    if (stamps) stamps[0] = __builtin_amdgcn_s_memrealtime();
     if (RESET) {
       GaussNext g{has_gauss != 0, gauss_next};
       reset_env_gauss(L, e, rng, g);
@@ -1526,7 +1547,9 @@ __device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const 
       r = env_step(L, lv.trig, m, e, action, rng);
       ep.x += r.reward;  // (ep.y: the episode's start step)
     }
-    observe(L, e, o);
+    if (stamps) stamps[1] = __builtin_amdgcn_s_memrealtime();
+    observe(level_div(L), e, o);  // by f64 division, as k_run (the table's loads: 0.48 us)
+    if (stamps) stamps[2] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
     for (int k = 0; k < 9; ++k) out->obs[k] = o[k];
     out->reward = r.reward;
@@ -1544,6 +1567,7 @@ __device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const 
     draws = rng.draws;
   }
   __syncthreads();
+  if (stamps && lane == 0) stamps[3] = __builtin_amdgcn_s_memrealtime();
   const uint32_t g = out_g;
   if (g != 0u) {  // the caller's generation changed
     const uint32_t* src = W + ((g + off) % PY_GENS) * MT_N;
@@ -1555,8 +1579,9 @@ __device__ __forceinline__ uint32_t py_call(const Soa& S, const Level& L, const 
     off = (off + g) % PY_GENS;
   }
   if (lane == 0) py->index = out_idx;
-  wave_stats(stats, lane == 0 && !RESET ? 1 : 0, r.ran, r.ticks, (int)draws, 0);
+  lane0_stats(stats, !RESET ? 1 : 0, r.ran, r.ticks, (int)draws, 0);
   if (ticks) *ticks = r.ticks;
+  if (stamps && lane == 0) stamps[4] = __builtin_amdgcn_s_memrealtime();
   return g;
 }
 // the ring from the caller's state (py, pinned host memory): its generation and two successors
@@ -1665,6 +1690,7 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
   uint32_t served = sys_load(&box->done);
   unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
   __shared__ TgOne row_l;  // the command's result row, written to host memory in one burst
+  __shared__ unsigned long long phase_l[5];  // TG_SERVE_TRACE: py_call's phase stamps
   TgOne* const row = &row_l;
   while (true) {
     // the command group in one load (volatile: system scope, no cache)
@@ -1690,8 +1716,8 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
     if (kind == SRV_STEP) {
       const StepIO io{nullptr, row->obs, &row->reward, &row->valid, &row->done, nullptr,
                       POL_IMMEDIATE, (uint64_t)(int64_t)action, 0, tstep};
-      ticks = step_env<false, false, POL_IMMEDIATE>(S, 1, L, lv.trig, m, (lds_u8*)win, lane, io, q,
-                                                    g0, stats, err_or).ticks;
+      ticks = step_env<false, false, POL_IMMEDIATE, true>(S, 1, L, lv.trig, m, (lds_u8*)win, lane, io,
+                                                          q, g0, stats, err_or).ticks;
     } else {
       const bool warm = (word >> 9) & 1u;
       const int has_gauss = (int)((word >> 10) & 1u);
@@ -1716,7 +1742,7 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
                       &ticks, mk);
       else
         py_call<false>(S, L, lv, W, off, action, py, q0, has_gauss, gauss_next, row, tstep, stats,
-                       err_or, &ticks, mk);
+                       err_or, &ticks, mk, trace ? phase_l : nullptr);
     }
     __syncthreads();
     if (lane < (int)(sizeof(TgOne) / 8))
@@ -1727,6 +1753,7 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
       box->t_seen = t_seen;
       box->t_end = __builtin_amdgcn_s_memrealtime();
       box->ticks = (uint32_t)ticks;
+      for (int j = 0; j < 5; ++j) box->phase[j] = kind == SRV_STEP_PY ? phase_l[j] : 0ull;
     }
     __syncthreads();  // (the release below covers the row the lanes wrote: one wave)
     if (lane == 0) __hip_atomic_store(&box->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2012,6 +2039,13 @@ void tg_destroy(tg_batch* h) {
     const double b = (n * sgk - sk * sg) / (n * skk - sk * sk), a = (sg - b * sk) / n;
     fprintf(stderr, "[serve] ticks per command %.2f; server time = %.2f us + %.3f us x ticks "
             "(level tables in LDS: %d, %zu B)\n", sk / n, a / 1e3, b / 1e3, h->srv_stage, h->srv_dyn);
+    if (h->srv_phase_n)
+      fprintf(stderr, "[serve] py steps %lld, mean us: pickup -> option %.3f, option %.3f, observe "
+              "%.3f, -> barrier %.3f, -> py_call return %.3f, -> answer %.3f\n",
+              (long long)h->srv_phase_n, h->srv_phase[0] / h->srv_phase_n / 1e3,
+              h->srv_phase[1] / h->srv_phase_n / 1e3, h->srv_phase[2] / h->srv_phase_n / 1e3,
+              h->srv_phase[3] / h->srv_phase_n / 1e3, h->srv_phase[4] / h->srv_phase_n / 1e3,
+              h->srv_phase[5] / h->srv_phase_n / 1e3);
   }
   if (h->srv_ev) (void)hipEventDestroy(h->srv_ev);
   if (h->srv_dep) (void)hipEventDestroy(h->srv_dep);
@@ -2434,6 +2468,12 @@ int srv_call(tg_batch* h, const SrvBox& c, hipStream_t caller) {
         h->srv_fit[0] += k;
         h->srv_fit[1] += k * k;
         h->srv_fit[2] += g * k;
+        if (b->phase[0]) {  // py_call's phases: pickup -> option start -> end -> observe ->
+          const uint64_t t[7] = {b->t_seen, b->phase[0], b->phase[1], b->phase[2], b->phase[3],
+                                 b->phase[4], b->t_end};  // barrier -> its return -> answer
+          for (int j = 0; j < 6; ++j) h->srv_phase[j] += 10.0 * (double)(t[j + 1] - t[j]);
+          ++h->srv_phase_n;
+        }
       }
       return TG_OK;
     }

@@ -46,7 +46,8 @@ struct TgOne {
 };
 static_assert(sizeof(TgOne) == 80, "TgOne: ten 8-B words (k_serve1 copies it out by word)");
 
-// The N = 1 server's mailbox (k_serve1, tg_amd.hip): pinned, coherent host memory.  Line 0 is
+// The N = 1 server's mailbox (k_serve1, tg_amd.hip): pinned, coherent host memory (line 2:
+// TG_SERVE_TRACE's stamps).  Line 0 is
 // the host's: a command is one 16-B group (seq last: the server reads the group with one load,
 // and a group whose seq is new carries the command's fields) and, for a reset, gauss_next
 // (read after the group).  Line 1 is the server's: done, the last command it served (a server
@@ -69,8 +70,10 @@ struct SrvBox {
   uint64_t t_seen, t_end;  // TG_SERVE_TRACE: the server's clock at the command's pickup / answer
   uint32_t ticks;          //   and the command's ticks
   uint32_t pad3[7];
+  uint64_t phase[5];       // TG_SERVE_TRACE: py_call's phase stamps (SRV_STEP_PY)
+  uint64_t pad4[3];
 };
-static_assert(sizeof(SrvBox) == 128, "SrvBox: two 64-B lines");
+static_assert(sizeof(SrvBox) == 192, "SrvBox: three 64-B lines");
 
 struct RenderState;  // tg_render.hip
 void render_free(RenderState* rs);
@@ -164,6 +167,8 @@ struct tg_batch {
   size_t srv_dyn = 0;              //   not chosen yet) and their dynamic LDS bytes
   bool srv_trace = false;          // TG_SERVE_TRACE: sums printed at tg_destroy (diagnostic)
   double srv_rt_ns = 0.0, srv_gpu_ns = 0.0, srv_post_ns = 0.0, srv_fit[3] = {0.0, 0.0, 0.0};
+  double srv_phase[6] = {0, 0, 0, 0, 0, 0};
+  int64_t srv_phase_n = 0;
   tg::RenderState* rs = nullptr;   // tg_render_init
   std::vector<int> kst_k;          // steps each in-use step record covers (a k_flow launch: K)
   // TG_MODE_FLOW's work structures (tg_flow.h Flow; allocated at the first flow rollout)
