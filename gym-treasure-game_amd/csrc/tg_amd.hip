@@ -1640,10 +1640,10 @@ __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 // Resident for many commands, the server keeps in LDS what a step would otherwise fetch from
-// HBM each time, one dependent round trip apiece: the env's state (st4 / ang / ep: written back
-// to HBM when it leaves) and, when they fit (`stage`: 1 the GoTable, 2 get_state's quotient
-// table; dynamic LDS, sized at launch), the level's tables.
-constexpr uint32_t SRV_STAGE_GOTAB = 1u, SRV_STAGE_OBSQ = 2u;
+// HBM each time: the env's state (st4 / ang / ep: written back to HBM when it leaves), the level
+// bitmasks and, when it fits (`stage`: dynamic LDS, sized at launch), the GoTable.  (get_state
+// divides, as k_run: no quotient table.)
+constexpr uint32_t SRV_STAGE_GOTAB = 1u;
 __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t* __restrict__ grid,
                                                SrvBox* box, tg_pystate* py, uint32_t* pyc,
                                                TgOne* out, EpQueue q, int64_t g0, uint32_t idle,
@@ -1664,15 +1664,8 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
     for (int i = lane; i < mk_words(Lg.W, Lg.H); i += 64) mk_l[i] = Lg.masks[i];
   const uint32_t* const mk = Lg.masks ? mk_l : nullptr;
   Level L = Lg;
-  if (stage & SRV_STAGE_OBSQ) {
-    double* const qd = reinterpret_cast<double*>(srv_dyn);
-    const int nq = Lg.qx_n + Lg.qy_n;
-    for (int i = lane; i < nq; i += 64) qd[i] = Lg.obs_q[i];
-    L.obs_q = qd;
-  }
   if (stage & SRV_STAGE_GOTAB) {
-    uint32_t* const gd = reinterpret_cast<uint32_t*>(
-        srv_dyn + ((stage & SRV_STAGE_OBSQ) ? sizeof(double) * (size_t)(Lg.qx_n + Lg.qy_n) : 0));
+    uint32_t* const gd = reinterpret_cast<uint32_t*>(srv_dyn);
     const int ng = Lg.W * Lg.H * 32;
     for (int i = lane; i < ng; i += 64) gd[i] = Lg.gotab[i];
     L.gotab = gd;
@@ -2038,7 +2031,7 @@ void tg_destroy(tg_batch* h) {
     const double sg = h->srv_gpu_ns, sgk = h->srv_fit[2];
     const double b = (n * sgk - sk * sg) / (n * skk - sk * sk), a = (sg - b * sk) / n;
     fprintf(stderr, "[serve] ticks per command %.2f; server time = %.2f us + %.3f us x ticks "
-            "(level tables in LDS: %d, %zu B)\n", sk / n, a / 1e3, b / 1e3, h->srv_stage, h->srv_dyn);
+            "(GoTable in LDS: %d, %zu B)\n", sk / n, a / 1e3, b / 1e3, h->srv_stage, h->srv_dyn);
     if (h->srv_phase_n)
       fprintf(stderr, "[serve] py steps %lld, mean us: pickup -> option %.3f, option %.3f, observe "
               "%.3f, -> barrier %.3f, -> py_call return %.3f, -> answer %.3f\n",
@@ -2405,24 +2398,19 @@ int srv_start(tg_batch* h, hipStream_t caller) {
     HIP_TRY(hipFuncGetAttributes(&fa, (const void*)k_serve1));
     HIP_TRY(hipDeviceGetAttribute(&dev_max, hipDeviceAttributeMaxSharedMemoryPerBlock, h->device));
     const size_t room = dev_max > (int)fa.sharedSizeBytes ? (size_t)dev_max - fa.sharedSizeBytes : 0;
-    const size_t qb = h->L.obs_q ? sizeof(double) * (size_t)(h->L.qx_n + h->L.qy_n) : 0;
     const size_t gb = h->L.gotab ? sizeof(uint32_t) * (size_t)h->L.W * h->L.H * 32 : 0;
     uint32_t stage = 0;
     size_t dyn = 0;
-    if (qb && qb <= room) {
-      stage |= SRV_STAGE_OBSQ;
-      dyn += qb;
-    }
-    if (gb && dyn + gb <= room) {
-      stage |= SRV_STAGE_GOTAB;
-      dyn += gb;
+    if (gb && gb <= room) {
+      stage = SRV_STAGE_GOTAB;
+      dyn = gb;
     }
     if (dyn > 65536 &&
         hipFuncSetAttribute((const void*)k_serve1, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)dyn) != hipSuccess) {
       (void)hipGetLastError();
-      stage = qb && qb <= 65536 ? SRV_STAGE_OBSQ : 0u;
-      dyn = stage ? qb : 0;
+      stage = 0u;
+      dyn = 0;
     }
     h->srv_stage = (int)stage;
     h->srv_dyn = dyn;
