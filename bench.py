@@ -213,6 +213,15 @@ def dropin_latency(tg, steps=300, seed=0):
                         env.reset()
                 key = mode + "_step_us" if serve else "launch_per_call_" + mode + "_step_us"
                 out[key] = (time.perf_counter() - t0) / steps * 1e6
+                if mode == "shared_global_random":  # an agent reading the mask before each step
+                    t0 = time.perf_counter()
+                    for _ in range(steps):
+                        m = env.available_mask
+                        if env.step(r.randrange(9))[2]:
+                            env.reset()
+                    key = "mask_and_step_us" if serve else "launch_per_call_mask_and_step_us"
+                    out[key] = (time.perf_counter() - t0) / steps * 1e6
+                    del m
                 env.close()
     finally:
         random.setstate(saved)

@@ -1706,7 +1706,13 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
     }
     const int action = (int)((word >> 4) & 31u) - 16;
     const uint32_t tstep = __builtin_amdgcn_readfirstlane(cg.y);
-    if (kind == SRV_STEP) {
+    if (kind == SRV_MASK) {  // available_mask (TG/:83-89), as k_mask
+      if (lane == 0) {
+        Env e;
+        unpack(S.st4[0], S.ang[0], e);
+        box->mask = available_mask(L, m, e);
+      }
+    } else if (kind == SRV_STEP) {
       const StepIO io{nullptr, row->obs, &row->reward, &row->valid, &row->done, nullptr,
                       POL_IMMEDIATE, (uint64_t)(int64_t)action, 0, tstep};
       ticks = step_env<false, false, POL_IMMEDIATE, true>(S, 1, L, lv.trig, m, (lds_u8*)win, lane, io,
@@ -1738,7 +1744,7 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
                        err_or, &ticks, mk, trace ? phase_l : nullptr);
     }
     __syncthreads();
-    if (lane < (int)(sizeof(TgOne) / 8))
+    if (kind != SRV_MASK && lane < (int)(sizeof(TgOne) / 8))
       reinterpret_cast<uint64_t*>(out)[lane] = reinterpret_cast<const uint64_t*>(row)[lane];
     // the row and the state (host memory; the env's state and MT ring in HBM for the next
     // command) before the answer
@@ -2055,6 +2061,7 @@ void tg_destroy(tg_batch* h) {
   if (h->fork) (void)hipEventDestroy(h->fork);
   if (h->one) (void)hipHostFree(h->one);
   if (h->py) (void)hipHostFree(h->py);
+  if (h->mask1) (void)hipHostFree(h->mask1);
   if (h->pyc) (void)hipFree(h->pyc);
   delete h;
 }
@@ -2367,6 +2374,9 @@ int one_row(tg_batch* h) {
 
 // launch k_serve1 on the server's stream, after the work queued on the caller's stream
 int srv_start(tg_batch* h, hipStream_t caller) {
+  // every buffer the server may write, whichever call launches it (a server first launched by
+  // tg_available_mask1 serves the steps after it too)
+  if (const int rc = one_row(h)) return rc;
   if (!h->box) {
     if (hipHostMalloc((void**)&h->box, sizeof(SrvBox), hipHostMallocMapped | hipHostMallocCoherent) !=
         hipSuccess)
@@ -2415,6 +2425,9 @@ int srv_start(tg_batch* h, hipStream_t caller) {
     h->srv_stage = (int)stage;
     h->srv_dyn = dyn;
   }
+  if (!h->box_dev || !h->py_dev || !h->pyc || !h->one_dev || !h->S.st4 || !h->S.ang || !h->S.ep ||
+      !h->S.mt || !h->S.mc || !h->grid || !h->main.stats || !h->err)
+    return fail(TG_E_HIP, "k_serve1: a buffer it writes is not allocated");
   hipLaunchKernelGGL(k_serve1, dim3(1), dim3(64), h->srv_dyn, h->srv_st, h->S, h->L, h->grid,
                      h->box_dev, h->py_dev, h->pyc, h->one_dev, q, h->g0, h->srv_idle,
                      (int)h->srv_trace, (uint32_t)h->srv_stage, h->main.stats, h->err);
@@ -2556,6 +2569,30 @@ int tg_step1(tg_batch* h, int32_t action, double* obs, int32_t* reward, uint8_t*
   *reward = h->one->reward;
   *valid = h->one->valid;
   *done = h->one->done;
+  return TG_OK;
+}
+
+int tg_available_mask1(tg_batch* h, uint16_t* mask, void* stream) {
+  BIND_SERVE(h);
+  if (h->n != 1 || !mask) return fail(TG_E_INVAL, "tg_available_mask1: a 1-env handle and a host output");
+  if (h->serve) {
+    SrvBox c{};
+    c.word = srv_word(SRV_MASK, 0, false, false, 0);
+    if (const int rc = srv_call(h, c, (hipStream_t)stream)) return rc;
+    *mask = (uint16_t)h->box->mask;
+    return TG_OK;
+  }
+  if (!h->mask1) {
+    if (hipHostMalloc((void**)&h->mask1, sizeof(uint16_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess)
+      return fail(TG_E_NOMEM, "tg_available_mask1: pinned result");
+    HIP_TRY(hipHostGetDevicePointer((void**)&h->mask1_dev, h->mask1, 0));
+  }
+  hipLaunchKernelGGL(k_mask, dim3(1), dim3(BLOCK), 0, (hipStream_t)stream, h->S, h->n, h->L, h->grid,
+                     h->mask1_dev);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  *mask = *h->mask1;
   return TG_OK;
 }
 

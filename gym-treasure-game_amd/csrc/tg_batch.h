@@ -52,7 +52,7 @@ static_assert(sizeof(TgOne) == 80, "TgOne: ten 8-B words (k_serve1 copies it out
 // and a group whose seq is new carries the command's fields) and, for a reset, gauss_next
 // (read after the group).  Line 1 is the server's: done, the last command it served (a server
 // that starts reads it, so a command posted while none ran is served by the next one).
-enum : uint32_t { SRV_STEP = 1, SRV_STEP_PY = 2, SRV_RESET_PY = 3, SRV_QUIT = 4 };
+enum : uint32_t { SRV_STEP = 1, SRV_STEP_PY = 2, SRV_RESET_PY = 3, SRV_QUIT = 4, SRV_MASK = 5 };
 // the command word: kind | (action + 16) << 4 | warm << 9 | has_gauss << 10 | q0 << 11
 inline uint32_t srv_word(uint32_t kind, int32_t action, bool warm, bool has_gauss, uint32_t q0) {
   return kind | (uint32_t)((action + 16) & 31) << 4 | (warm ? 1u : 0u) << 9 |
@@ -66,7 +66,8 @@ struct SrvBox {
   uint64_t gauss_bits;  // SRV_RESET_PY: the caller's gauss_next
   uint8_t pad1[64 - 24];
   uint32_t done;
-  uint32_t pad2[3];
+  uint32_t mask;           // SRV_MASK's answer: available_mask's bits
+  uint32_t pad2[2];
   uint64_t t_seen, t_end;  // TG_SERVE_TRACE: the server's clock at the command's pickup / answer
   uint32_t ticks;          //   and the command's ticks
   uint32_t pad3[7];
@@ -144,6 +145,8 @@ struct tg_batch {
   double* obs_scratch = nullptr;   // tg_rollout without an obs output
   tg::TgOne* one = nullptr;            // tg_step1's row: pinned host memory the kernel writes
   tg::TgOne* one_dev = nullptr;        //   (its device-side address)
+  uint16_t* mask1 = nullptr;           // tg_available_mask1's answer without the server (pinned)
+  uint16_t* mask1_dev = nullptr;
   tg_pystate* py = nullptr;            // tg_step1_py / tg_reset1_py's stream state (pinned)
   tg_pystate* py_dev = nullptr;
   uint32_t* pyc = nullptr;  // the Python stream's generation + 2 successors, on the device

@@ -588,6 +588,8 @@ class TreasureGame:
         # the step call's arguments, made once: a step is one C call and nothing else.  Its
         # stream is the null stream: every TreasureGame call returns host data, so none of this
         # env's device work is pending when a step starts.
+        self._h_mask = ctypes.c_uint16()
+        self._p_mask = ctypes.byref(self._h_mask)
         self._step_args = (self._h_obs.ctypes.data, ctypes.byref(self._h_rew),
                            ctypes.byref(self._h_valid), ctypes.byref(self._h_done), None)
         # the shared stream's step works in place on the global random.Random's own words and
@@ -652,7 +654,13 @@ class TreasureGame:
         return self._vec.reset().cpu().numpy()[0].tolist()
 
     def _mask_bits(self):
-        return int(self._vec.available_mask().cpu().item()) & 0x1FF
+        # tg_available_mask1: through the resident server (a mask read between steps does not
+        # stop it); the null stream, as the step
+        v = self._vec
+        rc = v._L.tg_available_mask1(v.handle, self._p_mask, None)
+        if rc:
+            check(rc, "tg_available_mask1")
+        return int(self._h_mask.value) & 0x1FF
 
     @property
     def available_mask(self):

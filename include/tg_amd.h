@@ -198,6 +198,11 @@ int tg_set_groups(tg_batch *h, int32_t groups, int32_t stagger);
 /* available_mask for every env: u16 [N], bit k == option k can run. */
 int tg_available_mask(tg_batch *h, uint16_t *mask, void *stream);
 
+/* available_mask of a 1-env handle (the N=1 drop-in's TreasureGame.available_mask, TG/:83-89)
+ * into a HOST u16: served by the resident server like tg_step1 (so a mask read between steps
+ * does not stop it), or one launch + synchronisation with serving off. */
+int tg_available_mask1(tg_batch *h, uint16_t *mask, void *stream);
+
 /* current observation of every env, f64 [N][9]. */
 int tg_observe(tg_batch *h, double *obs, void *stream);
 

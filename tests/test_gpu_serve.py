@@ -124,3 +124,22 @@ def test_process_exits_with_the_server_resident(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert "stepped" in r.stdout
     assert time.time() - t0 < 100
+
+
+def test_mask_first_then_steps(tg, oracle):
+    """A server first launched by available_mask (tg_available_mask1) serves the steps after it:
+    the call that starts a server must not matter (round 6: the row buffer was allocated only by
+    the step calls, and a mask-first server wrote its first step's row through a null pointer)"""
+    for serve in (True, False):
+        env = tg.TreasureGame(seed=12)
+        env._vec.set_serve(serve)
+        ref = oracle.OracleEnv(12)
+        env.reset()  # (tg_reset: no server yet, so the mask read below launches it)
+        assert env.available_mask.tolist() == [(ref.mask() >> k) & 1 for k in range(9)]
+        for t in range(40):
+            a = oracle.pick_action(0x5A, 12, t, True, ref.mask())
+            st, r, d, _ = env.step(a)
+            rs, rr, rd, _ = ref.step(a)
+            assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)) and (r, d) == (rr, rd)
+            assert env.available_mask.tolist() == [(ref.mask() >> k) & 1 for k in range(9)]
+        env.close()
