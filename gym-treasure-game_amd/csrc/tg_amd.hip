@@ -1628,12 +1628,14 @@ __global__ __launch_bounds__(64) void k_py1(Soa S, Level L, const uint32_t* __re
 }
 
 // ---- the N = 1 server (tg_batch::serve) ------------------------------------------------------
-// One wave, resident for a 1-env handle's tg_step1 / tg_step1_py / tg_reset1_py: it polls the
+// One wave, resident for a 1-env handle's tg_step1 / tg_step1_py / tg_step1_pywords /
+// tg_reset1_py / tg_available_mask1: it polls the
 // mailbox's seq (a system-scope load of pinned host memory), serves a new command with the same
 // device code as k_step<POL_IMMEDIATE> / k_py1 (step_env, py_call), writes the result row and
 // the stream state into pinned host memory, releases them at system scope and then stores
-// done = seq, which the host spins on.  The level, the code window and the Python stream's ring
-// (rotated by off) stay in LDS between commands.  Every lane leaves together, on SRV_QUIT or
+// done = seq, which the host spins on.  The level, the env's state and the Python stream's ring
+// (rotated by off) stay in LDS between commands (the private stream's code window is primed
+// afresh by each step, as in k_step).  Every lane leaves together, on SRV_QUIT or
 // after `idle` ticks of s_memrealtime (100 MHz) without a command; a leaving server writes the
 // ring to pyc (generation j in slot j), where the next server or k_py1 finds it.
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
