@@ -31,7 +31,7 @@ NUM_ACTIONS = 9
 
 # every symbol include/tg_amd.h declares (tests check the library exports all of them)
 EXPORTS = ("tg_create", "tg_destroy", "tg_num_envs", "tg_reset", "tg_step", "tg_step1", "tg_step1_py",
-           "tg_reset1_py", "tg_set_serve", "tg_step1_pywords", "tg_available_mask1", "tg_rollout", "tg_set_groups",
+           "tg_reset1_py", "tg_set_serve", "tg_step1_pywords", "tg_available_mask1", "tg_reset1", "tg_rollout", "tg_set_groups",
            "tg_available_mask",
            "tg_observe", "tg_policy_actions", "tg_episodes", "tg_errors", "tg_set_mode", "tg_set_timing", "tg_regenerate",
            "tg_set_episode_capacity", "tg_predicate_table",
@@ -95,6 +95,7 @@ def load():
         "tg_set_serve": (i32, [P, i32]),
         "tg_step1_pywords": (i32, [P, i32, P, P, P, P, P, P, P]),
         "tg_available_mask1": (i32, [P, P, P]),
+        "tg_reset1": (i32, [P, P, P]),
         "tg_rollout": (i32, [P, i32, u64, i64, i32, u32, P, P, P, P, P, P]),
         "tg_available_mask": (i32, [P, P, P]),
         "tg_observe": (i32, [P, P, P]),

@@ -1714,6 +1714,29 @@ __global__ __launch_bounds__(64) void k_serve1(Soa Sg, Level Lg, const uint32_t*
         unpack(S.st4[0], S.ang[0], e);
         box->mask = available_mask(L, m, e);
       }
+    } else if (kind == SRV_RESET) {  // reset() on the env's own stream, as k_reset
+      Env e;
+      e.mti = 0u;
+      if (lane == 0) {
+        unpack(S.st4[0], S.ang[0], e);
+        Rng rng(S.mt, e.mti, S.mc);
+        reset_env(L, e, rng);
+        e.mti = rng.finish();
+        double o[9];
+        observe(level_div(L), e, o);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) row->obs[k] = o[k];
+        row->reward = 0;
+        row->valid = 0;
+        row->done = 0;
+      }
+      wave_refill(__ballot(lane == 0 && (e.mti & MT_STALE)), S.mt, S.mc, e.mti, (lds_u32*)win);
+      if (lane == 0) {
+        e.mti &= ~(MT_STALE | MT_LISTED);
+        S.st4[0] = pack(e);
+        S.ang[0] = make_double2(e.ang0, e.ang1);
+        S.ep[0] = make_int2(0, (int32_t)tstep);  // the episode starts with the next step
+      }
     } else if (kind == SRV_STEP) {
       const StepIO io{nullptr, row->obs, &row->reward, &row->valid, &row->done, nullptr,
                       POL_IMMEDIATE, (uint64_t)(int64_t)action, 0, tstep};
@@ -2595,6 +2618,25 @@ int tg_available_mask1(tg_batch* h, uint16_t* mask, void* stream) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   *mask = *h->mask1;
+  return TG_OK;
+}
+
+int tg_reset1(tg_batch* h, double* obs, void* stream) {
+  BIND_SERVE(h);
+  if (h->n != 1) return fail(TG_E_INVAL, "tg_reset1: a 1-env handle");
+  if (h->serve) {
+    SrvBox c{};
+    c.word = srv_word(SRV_RESET, 0, false, false, 0);
+    c.tstep = h->tstep;  // the next step's index: the new episode's start (as tg_reset)
+    if (const int rc = srv_call(h, c, (hipStream_t)stream)) return rc;
+  } else {
+    if (const int rc = one_row(h)) return rc;
+    hipLaunchKernelGGL(k_reset, dim3(1), dim3(BLOCK), 0, (hipStream_t)stream, h->S, h->n, h->L,
+                       (const uint8_t*)nullptr, h->one_dev->obs, h->tstep);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  }
+  if (obs) memcpy(obs, h->one->obs, sizeof h->one->obs);
   return TG_OK;
 }
 

@@ -52,7 +52,8 @@ static_assert(sizeof(TgOne) == 80, "TgOne: ten 8-B words (k_serve1 copies it out
 // and a group whose seq is new carries the command's fields) and, for a reset, gauss_next
 // (read after the group).  Line 1 is the server's: done, the last command it served (a server
 // that starts reads it, so a command posted while none ran is served by the next one).
-enum : uint32_t { SRV_STEP = 1, SRV_STEP_PY = 2, SRV_RESET_PY = 3, SRV_QUIT = 4, SRV_MASK = 5 };
+enum : uint32_t { SRV_STEP = 1, SRV_STEP_PY = 2, SRV_RESET_PY = 3, SRV_QUIT = 4, SRV_MASK = 5,
+                  SRV_RESET = 6 };
 // the command word: kind | (action + 16) << 4 | warm << 9 | has_gauss << 10 | q0 << 11
 inline uint32_t srv_word(uint32_t kind, int32_t action, bool warm, bool has_gauss, uint32_t q0) {
   return kind | (uint32_t)((action + 16) & 31) << 4 | (warm ? 1u : 0u) << 9 |

@@ -651,7 +651,10 @@ class TreasureGame:
         if self._shared:
             self._reset_py(self._h_obs)
             return self._h_obs.tolist()
-        return self._vec.reset().cpu().numpy()[0].tolist()
+        # tg_reset1: through the resident server (a reset between episodes does not stop it)
+        v = self._vec
+        check(v._L.tg_reset1(v.handle, self._h_obs.ctypes.data, None), "tg_reset1")
+        return self._h_obs.tolist()
 
     def _mask_bits(self):
         # tg_available_mask1: through the resident server (a mask read between steps does not

@@ -203,6 +203,12 @@ int tg_available_mask(tg_batch *h, uint16_t *mask, void *stream);
  * does not stop it), or one launch + synchronisation with serving off. */
 int tg_available_mask1(tg_batch *h, uint16_t *mask, void *stream);
 
+/* reset() of a 1-env handle on its own stream (the N=1 drop-in's TreasureGame(seed=s).reset(),
+ * TG/:78-81) with the obs row into HOST memory (obs f64 [9], may be NULL): tg_reset of the one
+ * env, served by the resident server like tg_step1, or one launch + synchronisation with
+ * serving off. */
+int tg_reset1(tg_batch *h, double *obs, void *stream);
+
 /* current observation of every env, f64 [N][9]. */
 int tg_observe(tg_batch *h, double *obs, void *stream);
 

@@ -143,3 +143,29 @@ def test_mask_first_then_steps(tg, oracle):
             assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)) and (r, d) == (rr, rd)
             assert env.available_mask.tolist() == [(ref.mask() >> k) & 1 for k in range(9)]
         env.close()
+
+
+@pytest.mark.parametrize("idle_us", [None, "1"])
+def test_private_resets_through_the_server(tg, oracle, monkeypatch, idle_us):
+    """TreasureGame(seed=s).reset() (tg_reset1, SRV_RESET: k_reset's work on the server) between
+    steps, with the server and without, against the oracle's resets"""
+    if idle_us:
+        monkeypatch.setenv("TG_SERVE_IDLE_US", idle_us)
+    for serve in (True, False):
+        env = tg.TreasureGame(seed=21)
+        env._vec.set_serve(serve)
+        ref = oracle.OracleEnv(21)
+        s0 = env.reset()
+        assert np.array_equal(np.array(s0).view(np.uint64), ref.obs.view(np.uint64))
+        for t in range(150):
+            if t % 17 == 9:
+                s0 = env.reset()
+                ref.reset()
+                assert np.array_equal(np.array(s0).view(np.uint64), ref.obs.view(np.uint64)), (serve, t)
+            a = oracle.pick_action(0x3C, 21, t, True, ref.mask())
+            st, r, d, _ = env.step(a)
+            rs, rr, rd, _ = ref.step(a)
+            assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)), (serve, t)
+            assert (r, d) == (rr, rd), (serve, t)
+        assert env._vec.errors() == 0
+        env.close()
