@@ -730,8 +730,12 @@ class ObservationWrapper:
             env.render_init(sprites)
             self._frames = torch.empty((env.num_envs,) + env.frame_shape, dtype=torch.uint8,
                                        device=env.device)
-        elif sprites is not None:
-            env._sprites = sprites
+        else:
+            if sprites is not None:
+                env._sprites = sprites
+            # every step renders, and a render (a full-GPU kernel) stops the resident N = 1
+            # server: one launch per step costs less than a server stop + relaunch per step
+            env._vec.set_serve(False)
         self.action_space = env.action_space
         self.observation_space = env.observation_space
 
