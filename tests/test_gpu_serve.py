@@ -169,3 +169,45 @@ def test_private_resets_through_the_server(tg, oracle, monkeypatch, idle_us):
             assert (r, d) == (rr, rd), (serve, t)
         assert env._vec.errors() == 0
         env.close()
+
+
+def test_one_env_calls_reject_bad_arguments(tg):
+    """tg_step1_pywords / tg_available_mask1 / tg_reset1 are 1-env calls: a batch handle, a
+    null output or an index outside [0, 624] is an error (TgError), not a launch"""
+    import ctypes
+    from gym_treasure_game_amd import _lib
+    L = _lib.load()
+    words = (ctypes.c_uint32 * 624)()
+    idx = ctypes.c_int32(624)
+    obs = np.zeros(9)
+    r, va, d, m = ctypes.c_int32(), ctypes.c_uint8(), ctypes.c_uint8(), ctypes.c_uint16()
+    v = tg.TreasureGameVec(2, seed=0)
+    for call, name in ((lambda h: L.tg_available_mask1(h, ctypes.byref(m), None), "mask1"),
+                       (lambda h: L.tg_reset1(h, obs.ctypes.data, None), "reset1"),
+                       (lambda h: L.tg_step1_pywords(h, 0, words, ctypes.byref(idx), obs.ctypes.data,
+                                                     ctypes.byref(r), ctypes.byref(va),
+                                                     ctypes.byref(d), None), "pywords")):
+        with pytest.raises(tg.TgError):
+            _lib.check(call(v.handle), name)
+    v.close()
+    one = tg.TreasureGameVec(1, seed=0)
+    with pytest.raises(tg.TgError):
+        _lib.check(L.tg_available_mask1(one.handle, None, None), "mask1")
+    with pytest.raises(tg.TgError):
+        _lib.check(L.tg_step1_pywords(one.handle, 0, None, ctypes.byref(idx), obs.ctypes.data,
+                                      ctypes.byref(r), ctypes.byref(va), ctypes.byref(d), None),
+                   "pywords")
+    for bad in (-1, 625):
+        idx.value = bad
+        with pytest.raises(tg.TgError):
+            _lib.check(L.tg_step1_pywords(one.handle, 0, words, ctypes.byref(idx), obs.ctypes.data,
+                                          ctypes.byref(r), ctypes.byref(va), ctypes.byref(d), None),
+                       "pywords")
+    # the handle still steps after the refusals (with and without the server)
+    for serve in (True, False):
+        _lib.check(L.tg_set_serve(one.handle, int(serve)), "serve")
+        _lib.check(L.tg_step1(one.handle, 1, obs.ctypes.data, ctypes.byref(r), ctypes.byref(va),
+                              ctypes.byref(d), None), "step1")
+        _lib.check(L.tg_available_mask1(one.handle, ctypes.byref(m), None), "mask1")
+        assert m.value < 512
+    one.close()
