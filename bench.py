@@ -31,8 +31,10 @@ Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (tg_ste
 algorithmic bytes per launch over their HIP-event-timed duration vs the 8 TB/s HBM peak),
 ``cpu_baseline`` (the C oracle timed on this box's host cores, a bounded sample) and, at
 N = 1, ``parity_check`` (4,096 envs x 200 steps replayed on the GPU and compared bit-for-bit
-with the oracle's run in the cpu_baseline leg) and ``masked_policy`` (the same measurement
-with the masked-uniform policy: every step runs an option).
+with the oracle's run in the cpu_baseline leg), ``masked_policy`` (the same measurement
+with the masked-uniform policy: every step runs an option) and ``dropin_n1`` (the N = 1
+drop-in's TreasureGame.step latency through the resident server kernel, with the same calls
+launch-per-call beside it).
 
 ``--workload c5`` is config C5 instead: 65,536 envs per GPU whose step also renders every
 env's screen (ObservationWrapper, TG/:38-51: tg_render -> k_render, 1,257,984 B per frame,
