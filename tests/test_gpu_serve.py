@@ -211,3 +211,31 @@ def test_one_env_calls_reject_bad_arguments(tg):
         _lib.check(L.tg_available_mask1(one.handle, ctypes.byref(m), None), "mask1")
         assert m.value < 512
     one.close()
+
+
+@pytest.mark.parametrize("level", ["corridor", "gen1", "exit", "cascade"])
+def test_serve_other_levels(tg, oracle, level):
+    """The server on the reference's other levels (tests/golden/levels): a level too wide for
+    the bitmasks (no Map::mk), GoTables of other sizes (staged in the server's LDS when they
+    fit), with and without the server, against the oracle"""
+    import os
+    ld = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", level)
+    for serve in (True, False):
+        env = tg.TreasureGame(seed=7, level_dir=ld)
+        env._vec.set_serve(serve)
+        ref = oracle.OracleEnv(7, level_dir=ld)
+        s0 = env.reset()
+        assert np.array_equal(np.array(s0).view(np.uint64), ref.obs.view(np.uint64))
+        for t in range(80):
+            assert env.available_mask.tolist() == [(ref.mask() >> k) & 1 for k in range(9)], (level, serve, t)
+            a = oracle.pick_action(0x77, 7, t, True, ref.mask())
+            st, r, d, _ = env.step(a)
+            rs, rr, rd, _ = ref.step(a)
+            assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)), (level, serve, t)
+            assert (r, d) == (rr, rd), (level, serve, t)
+            if d or t % 37 == 20:
+                s0 = env.reset()
+                ref.reset()
+                assert np.array_equal(np.array(s0).view(np.uint64), ref.obs.view(np.uint64)), (level, serve, t)
+        assert env._vec.errors() == 0
+        env.close()
