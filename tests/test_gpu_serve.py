@@ -239,3 +239,37 @@ def test_serve_other_levels(tg, oracle, level):
                 assert np.array_equal(np.array(s0).view(np.uint64), ref.obs.view(np.uint64)), (level, serve, t)
         assert env._vec.errors() == 0
         env.close()
+
+
+def test_serve_wide_level_gotable_over_64k(tg, oracle, tmp_path):
+    """gen1 widened to 60 cells: its GoTable (60 x 11 x 32 x 4 B = 84 KB) exceeds 64 KB, so the
+    server's dynamic LDS needs hipFuncSetAttribute (the staging path a default-size level never
+    takes); no level bitmasks at that width.  Server and launch-per-call vs the oracle."""
+    import os
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "levels", "gen1")
+    rows = [r.rstrip("\n") for r in open(os.path.join(src, "domain.txt")) if r.strip()]
+    extra = 60 - len(rows[0])
+    wide = [r[:-1] + ("/" if y % 2 == 0 else " ") * extra + r[-1] for y, r in enumerate(rows)]
+    ld = tmp_path / "gen1_wide"
+    ld.mkdir()
+    (ld / "domain.txt").write_text("\n".join(wide) + "\n")
+    for f in ("domain-objects.txt", "domain-interactions.txt"):
+        (ld / f).write_text(open(os.path.join(src, f)).read())
+    for serve in (True, False):
+        env = tg.TreasureGame(seed=5, level_dir=str(ld))
+        env._vec.set_serve(serve)
+        ref = oracle.OracleEnv(5, level_dir=str(ld))
+        s0 = env.reset()
+        assert np.array_equal(np.array(s0).view(np.uint64), ref.obs.view(np.uint64))
+        for t in range(60):
+            assert env.available_mask.tolist() == [(ref.mask() >> k) & 1 for k in range(9)], (serve, t)
+            a = oracle.pick_action(0x99, 5, t, True, ref.mask())
+            st, r, d, _ = env.step(a)
+            rs, rr, rd, _ = ref.step(a)
+            assert np.array_equal(np.array(st).view(np.uint64), rs.view(np.uint64)), (serve, t)
+            assert (r, d) == (rr, rd), (serve, t)
+            if d:
+                env.reset()
+                ref.reset()
+        assert env._vec.errors() == 0
+        env.close()
